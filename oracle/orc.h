@@ -1,0 +1,200 @@
+/*
+ * orc.h -- CPU ORACLE for the PINC per-timestep PIC hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This directory is a plain-C restatement of the
+ * reference algorithm (trymen/PINC, /root/reference/src) used as the checker
+ * for the MI355X path in pinc_amd/.  Only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load it.  The product never links it.
+ *
+ * Pinning: the reference itself cannot be compiled here (core.h:12 includes
+ * <gsl/gsl_rng.h>; GSL is absent from the image, and a reference build would
+ * need stand-in headers, which this project does not write).  The oracle is
+ * therefore pinned against (1) the known-answer values in the reference's own
+ * unit tests (test/pusher.test.c, test/grid.test.c) and (2) the reference
+ * outputs recorded in SURVEY.md Appendix B (KE/PE of step 1, Langmuir
+ * frequencies, V-cycle counts).  See DESIGN.md "Oracle".
+ *
+ * Multi-rank runs are emulated in one process: a "world" holds one rank
+ * context per subdomain and every MPI exchange of the reference becomes a
+ * copy between rank contexts (same message contents, deterministic order).
+ */
+#ifndef ORC_H
+#define ORC_H
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------ ini -- */
+/* Dictionary with iniparser-3.1 semantics: keys are "section:key",
+ * lower-cased; values are raw strings (io.c:254-560, iniparser.c:555-613). */
+typedef struct OIni OIni;
+
+OIni *oini_load(const char *path);
+OIni *oini_from_string(const char *text);
+void oini_free(OIni *ini);
+void oini_set(OIni *ini, const char *key, const char *value);
+int oini_has(const OIni *ini, const char *key);
+const char *oini_raw(const OIni *ini, const char *key); /* aborts if absent */
+int oini_nelem(const OIni *ini, const char *key);
+int oini_int(const OIni *ini, const char *key);
+long oini_long(const OIni *ini, const char *key);
+double oini_double(const OIni *ini, const char *key);
+char **oini_strarr(const OIni *ini, const char *key, int n); /* free w/ oini_freestrarr */
+void oini_freestrarr(char **arr);
+int *oini_intarr(const OIni *ini, const char *key, int n);
+long *oini_longarr(const OIni *ini, const char *key, int n);
+double *oini_doublearr(const OIni *ini, const char *key, int n);
+void oini_setdoublearr(OIni *ini, const char *key, const double *v, int n);
+void oini_setdouble(OIni *ini, const char *key, double v);
+void oini_scaledouble(OIni *ini, const char *key, double factor);
+void oini_applysuffix(OIni *ini, const char *key, const char *suffix,
+                      const double *mul, int mullen);
+void orc_die(const char *fmt, ...);
+
+/* ---------------------------------------------------------------- types -- */
+typedef struct {
+	int rank;          /* nDims+1 */
+	int size[4];       /* [nValues, nx+2g, ny+2g, nz+2g] */
+	int trueSize[4];
+	long sizeProd[5];
+	int nGhost[8];     /* 2*rank entries */
+	double *val;
+} OGrid;
+
+typedef struct {
+	int nDims, nSpecies;
+	double *pos, *vel;       /* AoS, nDims doubles per particle */
+	long *iStart;            /* nSpecies+1 */
+	long *iStop;             /* nSpecies   */
+	double *charge, *mass;
+	double *kinEnergy, *potEnergy; /* nSpecies+1 */
+	long *id;                /* shadow ids (oracle-only bookkeeping) */
+} OPop;
+
+typedef struct {
+	int mpiRank, mpiSize, nDims, nSpecies;
+	int subdomain[3], nSubdomains[3], nSubdomainsProd[4], offset[3];
+	double posToSubdomain[3];
+	int nNeighbors, center;
+	long *nEmigrants;      /* nNeighbors*nSpecies */
+	long *nEmigrantsAlloc; /* nNeighbors */
+	long *nImmigrants;     /* nNeighbors*nSpecies */
+	double **emigrants;    /* nNeighbors buffers, 2*nDims doubles/particle */
+	long **emigrantIds;
+	double thresholds[6];
+} OMpi;
+
+/* Multigrid hierarchy of one rank: grids[0] aliases the user grid. */
+typedef struct {
+	int nLevels;
+	OGrid **grids;
+} OMg;
+
+typedef struct {
+	OMpi mpi;
+	OPop pop;
+	OGrid E, rho, phi, res;
+	OMg mgRho, mgPhi, mgRes;
+} ORank;
+
+enum { ORC_ACC_3D1KE, ORC_ACC_ND1KE, ORC_ACC_3D1, ORC_ACC_ND1 };
+enum { ORC_DISTR_3D1, ORC_DISTR_ND1 };
+enum { ORC_MIG_3D, ORC_MIG_ND };
+enum { ORC_SMOOTH_GS3D, ORC_SMOOTH_GSND };
+enum { ORC_RESTR_3D, ORC_RESTR_ND };
+enum { ORC_PROL_3D, ORC_PROL_ND };
+enum { ORC_POISSON_MG, ORC_POISSON_SPECTRAL };
+
+typedef struct {
+	int P;              /* number of subdomains (emulated ranks) */
+	int nDims, nSpecies;
+	ORank *r;
+	OIni *ini;
+	/* selected operators */
+	int acc, distr, migrate, poisson;
+	int preSmooth, postSmooth, coarseSolv, restrictor, prolongator;
+	int nLevels, nPre, nPost, nCoarse, mgCycles;
+	double maxVel;
+	/* diagnostics */
+	long cycles;        /* V-cycles run so far */
+	long solves;
+	double lastKE, lastPE;
+	double *keSpecies;  /* nSpecies */
+	double weights[8];
+	double unitCharge, unitMass, unitLength, unitTime;
+	int literal;        /* 1: reproduce main.c double FROMHALO + 2nd solve */
+	double *spectralFactor; /* 1-D spectral solver (spectral.c:29-37) */
+} OWorld;
+
+/* ---------------------------------------------------------------- grid -- */
+void og_alloc(OGrid *g, const OIni *ini, int nValues);
+void og_alloc_sub(OGrid *g, const OGrid *fine, int q);
+void og_free(OGrid *g);
+void og_zero(OGrid *g);
+void og_mul(OGrid *g, double num);
+void og_sub(OGrid *g, double num);
+void og_addto(OGrid *res, const OGrid *add);
+void og_square(OGrid *g);
+double og_sum_true(const OGrid *g);
+double og_pot_energy_inner(const OGrid *rho, const OGrid *phi);
+void og_findiff1st(const OGrid *scalar, OGrid *field);
+void og_findiff2nd(OGrid *res, const OGrid *phi);
+enum { OP_SET = 0, OP_ADD = 1 };
+enum { TOHALO = 0, FROMHALO = 1 };
+void ow_halo(OWorld *w, OGrid **grids, int op, int dir);
+void ow_halo_dim(OWorld *w, OGrid **grids, int d, int op, int dir);
+void ow_neutralize(OWorld *w, OGrid **grids);
+long og_tot_truesize(const OGrid *g, const OMpi *mpi);
+
+/* ----------------------------------------------------------- population -- */
+void op_alloc(OPop *p, const OIni *ini, int mpiSize);
+void op_free(OPop *p);
+void op_pos_lattice(OPop *p, const OIni *ini, const OMpi *mpi);
+void op_pos_perturb(OPop *p, const OIni *ini, const OMpi *mpi);
+void op_vel_zero(OPop *p);
+void op_vel_maxwell(OPop *p, const OIni *ini, unsigned long long seed);
+void op_to_local(OPop *p, const OMpi *mpi);
+void op_to_global(OPop *p, const OMpi *mpi);
+void op_sum_kin(OPop *p);
+
+/* ------------------------------------------------------------- pusher -- */
+void opu_move(OPop *p);
+void opu_acc3d1(OPop *p, OGrid *E, int ke);
+void opu_accnd1(OPop *p, OGrid *E, int ke);
+void opu_distr3d1(const OPop *p, OGrid *rho);
+void opu_distrnd1(const OPop *p, OGrid *rho);
+void opu_extract3d(OPop *p, OMpi *mpi);
+void opu_extractnd(OPop *p, OMpi *mpi);
+void ow_migrate(OWorld *w);
+int opu_neighbor_to_rank(const OMpi *mpi, int neighbor);
+int opu_rank_to_neighbor(const OMpi *mpi, int rank);
+int opu_neighbor_to_reciprocal(int neighbor, int nDims);
+void om_create_neighborhood(OMpi *mpi, const OIni *ini, const OGrid *g);
+
+/* ----------------------------------------------------------- multigrid -- */
+void ow_mg_alloc(OWorld *w);
+void ow_mg_solve(OWorld *w);
+void ow_spectral_solve(OWorld *w);
+/* single-grid stencil primitives (exported for unit tests) */
+void omg_gs_pass(OGrid *phi, const OGrid *rho, int color, int nd3);
+void omg_residual(OGrid *res, const OGrid *rho, const OGrid *phi);
+void omg_restrict(const OGrid *fine, OGrid *coarse, int nd3);
+void omg_inject(OGrid *fine, const OGrid *coarse);
+void omg_prolong_dim(OGrid *fine, int r);
+
+/* ------------------------------------------------------------ driver -- */
+OWorld *ow_create(OIni *ini, int literal);
+void ow_free(OWorld *w);
+void ow_init(OWorld *w, int perturb, int maxwell, unsigned long long seed);
+void ow_init_fields(OWorld *w);
+void ow_step(OWorld *w);
+
+/* Splittable counter-based RNG shared with the product's initialiser (the
+ * reference's GSL mt19937+ziggurat is absent: parity of draws is unpinned,
+ * SURVEY.md 8(c)).  normal = Box-Muller on two 53-bit uniforms of
+ * splitmix64(seed, counter). */
+double orc_uniform(unsigned long long seed, unsigned long long counter);
+double orc_normal(unsigned long long seed, unsigned long long counter);
+
+#endif
