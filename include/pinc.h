@@ -1,0 +1,240 @@
+/*
+ * pinc.h -- host operator surface of the MI355X PINC hot path (libpinc.so).
+ *
+ * Mirrors the reference's C API so a main.c-style loop drops in unchanged
+ * (reference: src/core.h, pusher.h, grid.h, population.h, multigrid.h,
+ * io.h, units.h).  The structs keep the reference's fields and meaning;
+ * each gains a device twin (dev*) that the operators act on.  Host arrays
+ * (Population.pos/vel, Grid.val) are only refreshed by the explicit
+ * *SyncToHost calls (diagnostics, parity dumps), never inside a step.
+ *
+ * Errors follow the reference (io.c:170-217): msg(ERROR,...) prints and
+ * exits.  The PincSim API at the end returns error codes instead and is
+ * what Python (bench.py, tests) drives through ctypes.
+ */
+#ifndef PINC_H
+#define PINC_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#include "pinc_hip.h"
+
+/* ------------------------------------------------------- core.h types -- */
+typedef void (*funPtr)();
+typedef struct dictionary dictionary;  /* iniparser-compatible dictionary */
+typedef struct ObjectOpaque Object;    /* immersed objects: out of scope */
+
+typedef enum { STATUS = 0x00, WARNING = 0x01, ERROR = 0x02, TIMER = 0x03, ALL = 0x10 } msgKind;
+typedef enum { PERIODIC = 0x01, DIRICHLET = 0x02, NEUMANN = 0x03, NONE = 0x10 } bndType;
+typedef enum { SCALAR = 1, VECTOR = -1 } gValueKind;          /* grid.h:14-17 */
+typedef enum { TOHALO = 0, FROMHALO = 1 } opDirection;       /* grid.h:22-25 */
+
+typedef struct PincDevPop PincDevPop;
+typedef struct PincDevGrid PincDevGrid;
+
+/* core.h:72-86 */
+typedef struct {
+	double *pos;         /* host mirror (AoS, nDims per particle)        */
+	double *vel;
+	long *iStart;        /* nSpecies+1 */
+	long *iStop;         /* nSpecies   */
+	double *charge;      /* normalised, nSpecies */
+	double *mass;
+	double *kinEnergy;   /* nSpecies+1 */
+	double *potEnergy;   /* nSpecies+1 */
+	int nSpecies;
+	int nDims;
+	PincDevPop *dev;     /* device twin */
+} Population;
+
+/* core.h:112-138 (MPI request/handle fields replaced by the RCCL context) */
+typedef struct {
+	int mpiRank, mpiSize, nDims;
+	int *subdomain, *nSubdomains, *nSubdomainsProd, *offset;
+	double *posToSubdomain;
+	int nSpecies, nNeighbors, neighborhoodCenter;
+	long *nEmigrants;       /* nNeighbors*nSpecies */
+	long *nEmigrantsAlloc;  /* nNeighbors */
+	long *nImmigrants;      /* nNeighbors*nSpecies */
+	double *thresholds;     /* 2*nDims (+ nDims upper bounds for the assert) */
+	void *comm;             /* RCCL communicator (NULL with one rank) */
+} MpiInfo;
+
+/* core.h:261-277 */
+typedef struct {
+	double *val;         /* host mirror, reference layout incl. ghosts */
+	int rank;            /* nDims+1 */
+	int *size, *trueSize;
+	long *sizeProd;
+	int *nGhostLayers;
+	bndType *bnd;
+	PincDevGrid *dev;    /* device twin */
+} Grid;
+
+/* core.h:392-417 */
+typedef struct {
+	int nDims, nSpecies;
+	double *weights;
+	double charge, mass, length, time;
+	double hyperArea, hyperVolume, frequency, velocity, acceleration, density,
+	       chargeDensity, potential, eField, bField, energy;
+} Units;
+
+/* ---------------------------------------------------------------- io -- */
+void msg(msgKind kind, const char *format, ...);
+dictionary *iniOpen(int argc, char *argv[]);
+dictionary *iniFromString(const char *text);
+void iniClose(dictionary *ini);
+void iniSet(dictionary *ini, const char *key, const char *value);
+int iniHas(const dictionary *ini, const char *key);
+int iniGetNElements(const dictionary *ini, const char *key);
+int iniGetInt(const dictionary *ini, const char *key);
+long iniGetLongInt(const dictionary *ini, const char *key);
+double iniGetDouble(const dictionary *ini, const char *key);
+char *iniGetStr(const dictionary *ini, const char *key);
+int *iniGetIntArr(const dictionary *ini, const char *key, int nElements);
+long *iniGetLongIntArr(const dictionary *ini, const char *key, int nElements);
+double *iniGetDoubleArr(const dictionary *ini, const char *key, int nElements);
+char **iniGetStrArr(const dictionary *ini, const char *key, int nElements);
+void freeStrArr(char **strArr);
+void iniSetDouble(dictionary *ini, const char *key, double value);
+void iniSetDoubleArr(dictionary *ini, const char *key, const double *values, int nElements);
+void iniScaleDouble(dictionary *ini, const char *key, double factor);
+void iniApplySuffix(dictionary *ini, const char *key, const char *suffix, const double *mul, int mulLen);
+/* select(ini,"methods:acc", puAcc3D1_set, ...) as io.h:105 */
+funPtr selectInner(const dictionary *ini, const char *key, const char *list, ...);
+/* The reference defines select() as a macro (io.h:105); include system
+ * headers that declare POSIX select() before this header, or define
+ * PINC_NO_SELECT_MACRO and call selectInner directly. */
+#ifndef PINC_NO_SELECT_MACRO
+#define select(ini, key, ...) selectInner(ini, key, #__VA_ARGS__, __VA_ARGS__)
+#endif
+
+/* ------------------------------------------------------------- units -- */
+Units *uAlloc(dictionary *ini);
+void uFree(Units *units);
+void uNormalize(dictionary *ini, const Units *units);
+
+/* -------------------------------------------------------------- grid -- */
+Grid *gAlloc(const dictionary *ini, int nValues);
+void gFree(Grid *grid);
+MpiInfo *gAllocMpi(const dictionary *ini);
+void gFreeMpi(MpiInfo *mpiInfo);
+void gCreateNeighborhood(const dictionary *ini, MpiInfo *mpiInfo, Grid *grid);
+void gDestroyNeighborhood(MpiInfo *mpiInfo);
+void gSetBndSlices(Grid *grid, MpiInfo *mpiInfo);
+/* slice operators are tokens selecting the halo semantics (grid.c:72-147) */
+void setSlice(const double *slice, Grid *grid, int d, int offset);
+void addSlice(const double *slice, Grid *grid, int d, int offset);
+void gHaloOp(funPtr sliceOp, Grid *grid, const MpiInfo *mpiInfo, opDirection dir);
+void gFinDiff1st(const Grid *scalar, Grid *field);
+void gMul(Grid *grid, double num);
+void gZero(Grid *grid);
+void gAddTo(Grid *result, Grid *addition);
+void gNeutralizeGrid(Grid *grid, const MpiInfo *mpiInfo);
+void gPotEnergy(const Grid *rho, const Grid *phi, Population *pop);
+void gSyncToHost(Grid *grid);       /* device -> reference-layout host mirror */
+void gSyncToDevice(Grid *grid);     /* host mirror (true nodes) -> device */
+
+/* -------------------------------------------------------- population -- */
+Population *pAlloc(const dictionary *ini);
+void pFree(Population *pop);
+void pPosLattice(const dictionary *ini, Population *pop, const MpiInfo *mpiInfo);
+void pPosPerturb(const dictionary *ini, Population *pop, const MpiInfo *mpiInfo);
+void pVelZero(Population *pop);
+void pVelMaxwell(const dictionary *ini, Population *pop, unsigned long long seed);
+void pToLocalFrame(Population *pop, const MpiInfo *mpiInfo);
+void pToGlobalFrame(Population *pop, const MpiInfo *mpiInfo);
+void pSumKinEnergy(Population *pop);
+void pSyncToHost(Population *pop);
+void pSyncToDevice(Population *pop);
+/* generate lattice (+perturbation, +Maxwellian) directly on the device */
+void pInitDevice(const dictionary *ini, Population *pop, const MpiInfo *mpiInfo, int perturb,
+                 int maxwell, unsigned long long seed);
+
+/* ------------------------------------------------------------ pusher -- */
+void puMove(Population *pop, Object *obj);
+funPtr puAcc3D1_set(dictionary *ini);
+funPtr puAcc3D1KE_set(dictionary *ini);
+funPtr puAccND1_set(dictionary *ini);
+funPtr puAccND1KE_set(dictionary *ini);
+void puAcc3D1(Population *pop, Grid *E);
+void puAcc3D1KE(Population *pop, Grid *E);
+void puAccND1(Population *pop, Grid *E);
+void puAccND1KE(Population *pop, Grid *E);
+funPtr puDistr3D1_set(dictionary *ini);
+funPtr puDistrND1_set(dictionary *ini);
+void puDistr3D1(const Population *pop, Grid *rho);
+void puDistrND1(const Population *pop, Grid *rho);
+funPtr puExtractEmigrants3D_set(dictionary *ini);
+funPtr puExtractEmigrantsND_set(dictionary *ini);
+void puExtractEmigrants3D(Population *pop, MpiInfo *mpiInfo);
+void puExtractEmigrantsND(Population *pop, MpiInfo *mpiInfo);
+void puMigrate(Population *pop, MpiInfo *mpiInfo, Grid *grid);
+int puNeighborToReciprocal(int neighbor, int nDims);
+int puNeighborToRank(MpiInfo *mpiInfo, int neighbor);
+int puRankToNeighbor(MpiInfo *mpiInfo, int rank);
+
+/* --------------------------------------------------------- multigrid -- */
+typedef struct MultigridSolver MultigridSolver;
+void mgSolver(void (**solve)(), void *(**solverAlloc)(), void (**solverFree)());
+funPtr mgSolver_set(dictionary *ini);
+MultigridSolver *mgAllocSolver(const dictionary *ini, Grid *rho, Grid *phi);
+void mgFreeSolver(MultigridSolver *solver);
+void mgSolve(MultigridSolver *solver, Grid *rho, Grid *phi, const MpiInfo *mpiInfo);
+long mgCycleCount(const MultigridSolver *solver);
+
+/* ---------------------------------------------------------- run mode -- */
+void regular(dictionary *ini);
+funPtr regular_set(dictionary *ini);
+
+/* ====================================================== PincSim API ===== */
+/* One process per GPU.  A simulation owns the ini, units, population, grids
+ * and solver of one rank and runs main.c's loop (objects compiled out). */
+typedef struct PincSim PincSim;
+
+typedef struct {
+	int literal;        /* 1: main.c's double FROMHALO add + extra solve */
+	int perturb;        /* apply pPosPerturb at init (Langmuir runs) */
+	int maxwell;        /* Maxwellian velocities from the counter RNG */
+	int deviceInit;     /* generate the initial state on the device */
+	unsigned long long seed;
+	int rank, nranks;   /* slab decomposition along the last dimension */
+	int device;         /* HIP device ordinal */
+	const unsigned char *commId; /* PINC_COMM_ID_BYTES, NULL if nranks==1 */
+	int timing;         /* record per-phase HIP events */
+} PincSimOpts;
+
+const char *pinc_last_error(void);
+PincSim *pinc_sim_create(const char *iniPath, int nOver, const char **over, const PincSimOpts *opts);
+void pinc_sim_free(PincSim *sim);
+int pinc_sim_init(PincSim *sim);            /* initial conditions + fields + half step */
+int pinc_sim_step(PincSim *sim);            /* one iteration of main.c:197-274 */
+int pinc_sim_op(PincSim *sim, const char *op);
+int pinc_sim_energy(PincSim *sim, double *ke, double *pe, double *keSpecies); /* rank-summed */
+long pinc_sim_cycles(const PincSim *sim);
+int pinc_sim_nspecies(const PincSim *sim);
+int pinc_sim_ndims(const PincSim *sim);
+long pinc_sim_pop_count(PincSim *sim, int s);
+int pinc_sim_pop_get(PincSim *sim, int s, double *pos, double *vel);
+int pinc_sim_pop_set(PincSim *sim, int s, long n, const double *pos, const double *vel);
+long pinc_sim_grid_shape(PincSim *sim, int which, int *size4);   /* 0 rho,1 phi,2 E */
+int pinc_sim_grid_get(PincSim *sim, int which, double *out);
+int pinc_sim_grid_set(PincSim *sim, int which, const double *in);
+int pinc_sim_emigrants(PincSim *sim, long *nEmigrants);
+int pinc_sim_species(PincSim *sim, double *charge, double *mass);
+int pinc_sim_sync(PincSim *sim);
+/* per-phase device times accumulated since the last reset (ms):
+ * 0 move+classify, 1 extract, 2 migrate, 3 deposit(+fold), 4 solve,
+ * 5 efield, 6 accelerate, 7 energy */
+#define PINC_NPHASES 8
+int pinc_sim_timers(PincSim *sim, double *ms);
+int pinc_sim_timers_reset(PincSim *sim);
+long pinc_sim_total_particles(PincSim *sim);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,232 @@
+/*
+ * pinc_hip.h -- C ABI of the MI355X kernel library (libpinc_hip.so).
+ *
+ * Plain C: pointers, sizes and small POD structs only; no HIP or torch types
+ * cross this boundary (streams are opaque void*).  Every entry point returns
+ * 0 on success or a nonzero HIP/RCCL error code; pinc_hip_error_string()
+ * describes the last failure.  The host operator surface (include/pinc.h)
+ * is built on these calls; each entry cites the reference loop it replaces.
+ *
+ * Device data layout (DESIGN.md "Layout"):
+ *   particles  SoA per component, species s in [iStart[s], iStart[s+1]) with
+ *              live particles [iStart[s], iStop[s]) -- the reference's
+ *              Population ranges (core.h:72-86) with x,y,z,vx,vy,vz split.
+ *              Positions are in the reference's local frame (true nodes at
+ *              1..T, ghosts 0 and T+1).
+ *   slab grid  the decomposed (last) dimension keeps its two ghost planes,
+ *              the other dimensions are periodic and stored without ghosts:
+ *              3-D [nloc+2][Ty][Tx], 2-D [nloc+2][Tx], 1-D [nloc+2].
+ *              Vector grids (E) hold 3 doubles per node (xyz, value-major as
+ *              grid.c:413-500).
+ *   global     the whole periodic domain without ghosts [Tz][Ty][Tx] (MG,
+ *              spectral); with one rank it aliases the slab's true planes.
+ */
+#ifndef PINC_HIP_H
+#define PINC_HIP_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PINC_MAX_SPECIES 8
+#define PINC_MAX_LEVELS 12
+
+/* geometry of one rank's slab; dims ordered x,y,z; slab dim = nd-1 */
+typedef struct {
+	int nd;        /* 1..3 */
+	int T[3];      /* global true size per dim (1 for unused dims) */
+	int nloc;      /* true cells of this rank along the slab dimension */
+	int off;       /* first true cell of this rank along the slab dim */
+	int nranks;    /* slabs along the slab dimension */
+} pinc_geom_t;
+
+/* a population on the device (by value; pointers are device pointers) */
+typedef struct {
+	double *x[3];
+	double *v[3];
+	int nSpecies;
+	int nd;
+	long iStart[PINC_MAX_SPECIES + 1];
+	long iStop[PINC_MAX_SPECIES];
+} pinc_pop_t;
+
+/* ------------------------------------------------------------ runtime -- */
+const char *pinc_hip_error_string(void);
+int pinc_hip_set_device(int dev);
+int pinc_hip_device_count(int *n);
+int pinc_hip_stream_create(void **stream);
+int pinc_hip_stream_destroy(void *stream);
+int pinc_hip_stream_sync(void *stream);
+int pinc_hip_device_sync(void);
+int pinc_hip_malloc(void **ptr, unsigned long bytes);
+int pinc_hip_free(void *ptr);
+int pinc_hip_memset(void *ptr, int value, unsigned long bytes, void *stream);
+int pinc_hip_h2d(void *dst, const void *src, unsigned long bytes, void *stream);
+int pinc_hip_d2h(void *dst, const void *src, unsigned long bytes, void *stream);
+int pinc_hip_d2d(void *dst, const void *src, unsigned long bytes, void *stream);
+/* events for per-phase device timing (replaces Timer, aux.c:48-85) */
+int pinc_hip_event_create(void **ev);
+int pinc_hip_event_destroy(void *ev);
+int pinc_hip_event_record(void *ev, void *stream);
+int pinc_hip_event_elapsed(float *ms, void *start, void *stop);
+int pinc_hip_mem_info(unsigned long *freeBytes, unsigned long *totalBytes);
+
+/* --------------------------------------------------------- particles -- */
+/* puMove (pusher.c:86-119, as compiled: pos += vel) fused with the
+ * neighbour classification of puExtractEmigrants3D/ND (pusher.c:782-910):
+ * flags[i] = ne in 0..3^nd-1, center = stays.  chunkCount[b] = emigrants of
+ * chunk b (PINC_CHUNK particles).  If doMove is 0 only classifies. */
+#define PINC_CHUNK 2048
+int pinc_hip_move_classify(pinc_pop_t pop, int s, int doMove, const double *thr,
+                           unsigned char *flags, int *chunkCount, double maxVel,
+                           int *errFlag, void *stream);
+
+/* Emigrant extraction with the reference's back-fill order (pusher.c:
+ * 782-855): survivors fill holes from the tail, emigrants are listed in the
+ * exact order the serial loop extracts them, then stably bucketed by
+ * direction.  Work arrays: see DESIGN.md "Migration".  Outputs:
+ *   buf   (6 doubles per emigrant, SoA blocks of cap entries: x,y,z,vx,vy,vz)
+ *   bufNe direction of each buffered emigrant
+ *   neCount[27] emigrants per direction (species s)
+ * Returns the number of emigrants in *nEmig.  Compacts species s in place
+ * (iStop[s] decreases by *nEmig on the host side). */
+typedef struct {
+	int *chunkOffset;   /* nChunks+1 */
+	int *tail;          /* >= nEmig+1 */
+	int *holes;         /* >= nEmig+1 */
+	int *order;         /* >= nEmig   */
+	int *blockHist;     /* >= 27*ceil(nEmig/1024)+27 */
+	int *scratch;       /* >= 64 ints */
+	double *buf;        /* 6*cap doubles */
+	unsigned char *bufNe;
+	long cap;
+} pinc_extract_ws_t;
+#define PINC_ERR_CAPACITY 77  /* *nEmig emigrants exceed ws.cap: grow and retry */
+int pinc_hip_extract(pinc_pop_t pop, int s, const unsigned char *flags, int *chunkCount,
+                     int center, int nNeighbors, pinc_extract_ws_t ws, long *nEmig,
+                     long *neCount, void *stream);
+
+/* multi-rank migration payload: records of 7 doubles (nd positions, nd
+ * velocities, padding, direction) packed from buffer entries [first,
+ * first+n), and appended to species s at index dst with the receiver's
+ * shift (1-digit_d(ne))*T_d in every dimension (pusher.c:941-985) */
+#define PINC_REC 7
+int pinc_hip_pack(const double *buf, long cap, const unsigned char *bufNe, long first, long n,
+                  int nd, double *out, void *stream);
+int pinc_hip_import_rec(pinc_pop_t pop, int s, long dst, const double *rec, long n,
+                        const int *shiftT, void *stream);
+
+/* importParticles + shiftImmigrants (pusher.c:941-985): append n buffered
+ * particles (buffer entries [first, first+n)) at index dst of species s,
+ * shifting each position by -(digit_d(ne)-1)*T_d for the dims that wrap
+ * locally (shiftMask bit d set). */
+int pinc_hip_import(pinc_pop_t pop, int s, long dst, const double *buf, long cap,
+                    const unsigned char *bufNe, long first, long n,
+                    const int *shiftT, int shiftMask, void *stream);
+
+/* CIC charge assignment puDistr3D1 / puDistrND1 (pusher.c:512-638) into the
+ * slab grid; accumulates raw weights of species s (the caller applies the
+ * reference's 1/q, q rescaling with pinc_hip_scale). */
+int pinc_hip_deposit(pinc_pop_t pop, int s, pinc_geom_t g, double *rhoSlab, void *stream);
+
+/* puAcc3D1KE / puAccND1KE (pusher.c:178-265) with puInterp3D1/ND1
+ * (pusher.c:1089-1162).  E node values are rescaled on the fly exactly as
+ * the reference's sequence of in-place gMul(E, q/m), gMul(E, m/q) does:
+ * value = E*pre; for t<s: value = (value*qm[t])*mq[t]; value *= qm[s].
+ * kePartial receives per-block partial sums of v.(v+dv); nBlocks returned. */
+int pinc_hip_accelerate(pinc_pop_t pop, int s, pinc_geom_t g, const double *Eslab,
+                        const double *qm, const double *mq, double pre,
+                        double *kePartial, int *nBlocks, void *stream);
+
+/* device-side initial conditions (pPosLattice population.c:172-240,
+ * pPosPerturb 242-276, pVelZero/Maxwell): generates the lattice indices of
+ * this rank, optional cosine perturbation, zero or Maxwellian velocities
+ * from the counter RNG shared with the oracle.  Returns count in *n. */
+int pinc_hip_init_species(pinc_pop_t pop, int s, pinc_geom_t g, long nGlobal, double latticeStep,
+                          const int *subdomain, const int *nSubdomains, const int *offset,
+                          const double *amp, const double *mode, int perturb,
+                          int maxwell, double drift, double vth, unsigned long long seed,
+                          long *n, void *stream);
+
+/* -------------------------------------------------------------- grids -- */
+int pinc_hip_zero(double *a, long n, void *stream);
+int pinc_hip_scale(double *a, long n, double f, void *stream);
+/* a = (a*f1)*f2 in one pass (two roundings, as two gMul calls) */
+int pinc_hip_scale2(double *a, long n, double f1, double f2, void *stream);
+/* gHaloOp(addSlice, rho, FROMHALO) along the slab dim for a self-periodic
+ * slab (grid.c:340-406): plane 0 += into nloc, plane nloc+1 += into 1 */
+int pinc_hip_fold_self(double *slab, pinc_geom_t g, void *stream);
+/* a += b elementwise (gAddTo, grid.c:781-789) */
+int pinc_hip_add(double *a, const double *b, long n, void *stream);
+/* every slab node (incl. ghost planes) from the global periodic grid:
+ * gHaloOp(setSlice, TOHALO) for a grid whose truth lives in the global
+ * array (phi after the solve) */
+int pinc_hip_slab_from_global(double *slab, const double *global, pinc_geom_t g, int nValues,
+                              void *stream);
+/* add a received plane into a slab plane */
+int pinc_hip_add_plane(double *slab, pinc_geom_t g, int plane, const double *in, void *stream);
+int pinc_hip_copy_plane(double *dst, const double *slab, pinc_geom_t g, int plane, int nValues, void *stream);
+/* gFinDiff1st + TOHALO (grid.c:226-261, main.c:245-246):
+ * E = 0.5*(phi[+d]-phi[-d]) on every slab plane incl. ghosts, from the
+ * global periodic phi (ghost planes then equal the neighbours' values
+ * bit for bit, so the TOHALO is implied). */
+int pinc_hip_efield(const double *phiGlobal, pinc_geom_t g, double *Eslab, void *stream);
+/* deterministic two-stage sums: *out = sum(a) ; sum(a*b) */
+int pinc_hip_sum(const double *a, long n, double *partial, double *out, void *stream);
+int pinc_hip_dot(const double *a, const double *b, long n, double *partial, double *out, void *stream);
+/* *out = sum(a)/div  (the mean of gNeutralizeGrid, grid.c:746) */
+int pinc_hip_sum_div(const double *a, long n, double div, double *partial, double *out, void *stream);
+/* *out = (sum of the first n entries of partial) / div */
+int pinc_hip_reduce(const double *partial, int n, double div, double *out, void *stream);
+
+/* --------------------------------------------------------- multigrid -- */
+/* One level of the global periodic grid. */
+typedef struct { int nd; int T[3]; } pinc_lvl_t;
+/* Red-black Gauss-Seidel colour pass (mgGS3D multigrid.c:683-767 when nd3,
+ * mgGSND 553-621 otherwise) on true points of colour `pass`, reading the
+ * other colour with the pending neutralisation shift *muPrev (exactly the
+ * reference's stored value - mu), writing block partial sums of the
+ * resulting logical grid into partial. nBlocks returned. */
+int pinc_hip_gs_pass(double *phi, const double *rho, pinc_lvl_t L, int pass, int nd3,
+                     const double *muPrev, double *partial, int *nBlocks, void *stream);
+/* phi = (phi - muA) - muB on colour `pass`'s complement and phi - muB on
+ * colour `pass` (materialise pending shifts after a smoothing sequence) */
+int pinc_hip_gs_materialize(double *phi, pinc_lvl_t L, int lastPass, const double *muA,
+                            const double *muB, void *stream);
+/* phi -= *mu over all points */
+int pinc_hip_sub_dev(double *a, long n, const double *mu, void *stream);
+/* mgResidual (multigrid.c:1385-1403): res = lap(phi) + rho */
+int pinc_hip_residual(double *res, const double *phi, const double *rho, pinc_lvl_t L,
+                      void *stream);
+/* residual sum of squares only (mgSumTrueSquared, multigrid.c:1471-1481) */
+int pinc_hip_residual_sumsq(const double *phi, const double *rho, pinc_lvl_t L,
+                            double *partial, int *nBlocks, void *stream);
+/* mgHalfRestrict3D / ND (multigrid.c:844-1022) */
+int pinc_hip_restrict(const double *fine, double *coarse, pinc_lvl_t Lc, int nd3, void *stream);
+/* mgBilinProl3D/ND + gAddTo (multigrid.c:1024-1238, 1535): phi_f += P(phi_c) */
+int pinc_hip_prolong_add(double *phiFine, const double *phiCoarse, pinc_lvl_t Lf, void *stream);
+
+/* ------------------------------------------------------------ comm -- */
+/* RCCL communicator over xGMI (one process per GPU).  id is the 128-byte
+ * ncclUniqueId produced by pinc_hip_comm_unique_id on rank 0 and
+ * distributed by the launcher. */
+#define PINC_COMM_ID_BYTES 128
+int pinc_hip_comm_unique_id(unsigned char *id);
+int pinc_hip_comm_init(void **comm, const unsigned char *id, int nranks, int rank);
+int pinc_hip_comm_destroy(void *comm);
+int pinc_hip_comm_sendrecv(void *comm, const void *sendbuf, long sendBytes, int peerSend,
+                           void *recvbuf, long recvBytes, int peerRecv, void *stream);
+/* grouped point-to-point exchange: op i sends sendBytes[i] to sendPeer[i]
+ * and receives recvBytes[i] from recvPeer[i].  Transfers between one pair of
+ * ranks match in op order, so with two slabs (up == down) pair each send
+ * with the receive from the opposite direction. */
+int pinc_hip_comm_exchange(void *comm, int nOps, const int *sendPeer, void *const *sendbuf,
+                           const long *sendBytes, const int *recvPeer, void *const *recvbuf,
+                           const long *recvBytes, void *stream);
+int pinc_hip_comm_allgather(void *comm, const double *send, double *recv, long count, void *stream);
+int pinc_hip_comm_allreduce_sum(void *comm, const double *send, double *recv, long count, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,171 @@
+"""ctypes wrapper of the CPU oracle (oracle/build/liborc.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py.  The product (pinc_amd) never imports it.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import subprocess
+from pathlib import Path
+from typing import Sequence
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB_PATH = HERE / "build" / "liborc.so"
+
+
+def _load() -> C.CDLL:
+    if not LIB_PATH.exists():
+        subprocess.run(["make", "-s", "-C", str(HERE), "-j4"], check=True)
+    lib = C.CDLL(str(LIB_PATH))
+    vp = C.c_void_p
+    sigs = {
+        "orc_world_new": (vp, [C.c_char_p, C.c_int, C.POINTER(C.c_char_p), C.c_int]),
+        "orc_world_free": (None, [vp]),
+        "orc_world_init": (None, [vp, C.c_int, C.c_int, C.c_ulonglong]),
+        "orc_world_init_fields": (None, [vp]),
+        "orc_world_step": (None, [vp]),
+        "orc_world_nranks": (C.c_int, [vp]),
+        "orc_world_cycles": (C.c_long, [vp]),
+        "orc_world_solves": (C.c_long, [vp]),
+        "orc_world_energy": (None, [vp, C.POINTER(C.c_double), C.POINTER(C.c_double), vp]),
+        "orc_world_species": (None, [vp, vp, vp]),
+        "orc_op": (None, [vp, C.c_char_p]),
+        "orc_grid_shape": (C.c_long, [vp, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int)]),
+        "orc_grid_get": (None, [vp, C.c_int, C.c_int, C.c_int, vp]),
+        "orc_grid_set": (None, [vp, C.c_int, C.c_int, C.c_int, vp]),
+        "orc_pop_count": (C.c_long, [vp, C.c_int, C.c_int]),
+        "orc_pop_get": (None, [vp, C.c_int, C.c_int, vp, vp, vp]),
+        "orc_pop_set": (None, [vp, C.c_int, C.c_int, C.c_long, vp, vp, vp]),
+        "orc_mpi_emigrants": (None, [vp, C.c_int, vp]),
+        "orc_mpi_thresholds": (None, [vp, C.c_int, vp]),
+        "orc_mpi_alloc": (None, [vp, C.c_int, vp]),
+        "orc_kat_acc": (None, [C.c_int, vp, C.c_int, vp, C.c_long, vp, vp, C.c_double, C.c_double, C.c_int, vp]),
+        "orc_kat_distr": (None, [C.c_int, vp, C.c_int, vp, C.c_long, vp, C.c_double, C.c_int]),
+        "orc_kat_neighbor_to_rank": (C.c_int, [vp, vp, C.c_int]),
+        "orc_kat_rank_to_neighbor": (C.c_int, [vp, vp, C.c_int]),
+        "orc_kat_reciprocal": (C.c_int, [C.c_int, C.c_int]),
+        "orc_kat_neighborhood": (None, [C.c_char_p, vp, vp]),
+        "orc_world_ndims": (C.c_int, [vp]),
+        "orc_world_nspecies": (C.c_int, [vp]),
+    }
+    for n, (r, a) in sigs.items():
+        f = getattr(lib, n)
+        f.restype = r
+        f.argtypes = a
+    return lib
+
+
+LIB = _load()
+
+
+class World:
+    """All subdomains of a run, emulated in one process (orc_sim.c)."""
+
+    def __init__(self, ini: str, overrides: Sequence[str] = (), literal: bool = False):
+        arr = (C.c_char_p * max(1, len(overrides)))(*[o.encode() for o in overrides])
+        self._h = LIB.orc_world_new(str(ini).encode(), len(overrides), arr, int(literal))
+        self.nranks = LIB.orc_world_nranks(self._h)
+
+    def close(self):
+        if self._h:
+            LIB.orc_world_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def init(self, perturb=True, maxwell=False, seed=0):
+        LIB.orc_world_init(self._h, int(perturb), int(maxwell), seed)
+
+    def init_fields(self):
+        LIB.orc_world_init_fields(self._h)
+
+    def step(self, n=1):
+        for _ in range(n):
+            LIB.orc_world_step(self._h)
+
+    def op(self, name: str):
+        LIB.orc_op(self._h, name.encode())
+
+    @property
+    def cycles(self):
+        return LIB.orc_world_cycles(self._h)
+
+    def energy(self):
+        ke, pe = C.c_double(), C.c_double()
+        LIB.orc_world_energy(self._h, C.byref(ke), C.byref(pe), None)
+        return ke.value, pe.value
+
+    def grid(self, which: int, rank: int = 0, level: int = 0) -> np.ndarray:
+        size = (C.c_int * 4)()
+        n = LIB.orc_grid_shape(self._h, rank, which, level, size)
+        out = np.zeros(n)
+        LIB.orc_grid_get(self._h, rank, which, level, out.ctypes.data)
+        rank = self.ndims + 1
+        # reference layout: value index fastest -> reversed shape
+        return out.reshape(tuple(reversed([size[i] for i in range(rank)])))
+
+    def set_grid(self, which: int, values: np.ndarray, rank: int = 0, level: int = 0):
+        v = np.ascontiguousarray(values, dtype=np.float64).ravel()
+        LIB.orc_grid_set(self._h, rank, which, level, v.ctypes.data)
+
+    def count(self, s: int, rank: int = 0) -> int:
+        return LIB.orc_pop_count(self._h, rank, s)
+
+    def particles(self, s: int, rank: int = 0):
+        n = self.count(s, rank)
+        nd = self.ndims
+        pos = np.zeros((n, nd))
+        vel = np.zeros((n, nd))
+        ids = np.zeros(n, dtype=np.int64)
+        LIB.orc_pop_get(self._h, rank, s, pos.ctypes.data, vel.ctypes.data, ids.ctypes.data)
+        return pos, vel, ids
+
+    def set_particles(self, s: int, pos, vel, ids=None, rank: int = 0):
+        pos = np.ascontiguousarray(pos, dtype=np.float64)
+        vel = np.ascontiguousarray(vel, dtype=np.float64)
+        idp = None
+        if ids is not None:
+            ids = np.ascontiguousarray(ids, dtype=np.int64)
+            idp = ids.ctypes.data
+        LIB.orc_pop_set(self._h, rank, s, pos.shape[0], pos.ctypes.data, vel.ctypes.data, idp)
+
+    def emigrants(self, rank: int = 0) -> np.ndarray:
+        n = 3 ** self.ndims * self.nspecies
+        out = np.zeros(n, dtype=np.int64)
+        LIB.orc_mpi_emigrants(self._h, rank, out.ctypes.data)
+        return out.reshape(3 ** self.ndims, self.nspecies)
+
+    @property
+    def ndims(self) -> int:
+        return LIB.orc_world_ndims(self._h)
+
+    @property
+    def nspecies(self) -> int:
+        return LIB.orc_world_nspecies(self._h)
+
+    def species(self):
+        q = np.zeros(self.nspecies)
+        m = np.zeros(self.nspecies)
+        LIB.orc_world_species(self._h, q.ctypes.data, m.ctypes.data)
+        return q, m
+
+
+def run_steps(ini: str, overrides: Sequence[str], steps: int, literal=False, perturb=True,
+              maxwell=False, seed=0):
+    """KE/PE history of a run (n = 1..steps) and the V-cycle counts."""
+    w = World(ini, overrides, literal)
+    w.init(perturb, maxwell, seed)
+    w.init_fields()
+    ke, pe, cyc = [], [], []
+    for _ in range(steps):
+        w.step()
+        k, p = w.energy()
+        ke.append(k)
+        pe.append(p)
+        cyc.append(w.cycles)
+    w.close()
+    return np.array(ke), np.array(pe), np.array(cyc)

@@ -552,3 +552,6 @@ void orc_kat_neighborhood(const char *iniText, double *thr, long *alloc){
 	og_free(&g);
 	oini_free(ini);
 }
+
+int orc_world_ndims(const OWorld *w){ return w->nDims; }
+int orc_world_nspecies(const OWorld *w){ return w->nSpecies; }

@@ -1,0 +1,95 @@
+"""ctypes binding of the native MI355X PINC libraries (pinc_amd/lib).
+
+The product path has no fallback: if libpinc.so / libpinc_hip.so are missing
+or fail to load, importing this module raises.  Build with
+``python -m pinc_amd.build``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+
+LIBDIR = Path(__file__).resolve().parent / "lib"
+PINC_COMM_ID_BYTES = 128
+NPHASES = 8
+PHASES = ["move", "extract", "migrate", "deposit", "solve", "efield", "accelerate", "energy"]
+
+
+class PincSimOpts(C.Structure):
+    _fields_ = [
+        ("literal", C.c_int),
+        ("perturb", C.c_int),
+        ("maxwell", C.c_int),
+        ("deviceInit", C.c_int),
+        ("seed", C.c_ulonglong),
+        ("rank", C.c_int),
+        ("nranks", C.c_int),
+        ("device", C.c_int),
+        ("commId", C.c_void_p),
+        ("timing", C.c_int),
+    ]
+
+
+def _load() -> tuple[C.CDLL, C.CDLL]:
+    hip_path = LIBDIR / "libpinc_hip.so"
+    host_path = LIBDIR / "libpinc.so"
+    if not hip_path.exists() or not host_path.exists():
+        raise ImportError(f"native PINC libraries not built ({LIBDIR}); run python -m pinc_amd.build")
+    hip = C.CDLL(str(hip_path), mode=C.RTLD_GLOBAL)
+    host = C.CDLL(str(host_path), mode=C.RTLD_GLOBAL)
+    return hip, host
+
+
+HIP, HOST = _load()
+
+_sigs = {
+    "pinc_last_error": (C.c_char_p, []),
+    "pinc_sim_create": (C.c_void_p, [C.c_char_p, C.c_int, C.POINTER(C.c_char_p), C.POINTER(PincSimOpts)]),
+    "pinc_sim_free": (None, [C.c_void_p]),
+    "pinc_sim_init": (C.c_int, [C.c_void_p]),
+    "pinc_sim_step": (C.c_int, [C.c_void_p]),
+    "pinc_sim_op": (C.c_int, [C.c_void_p, C.c_char_p]),
+    "pinc_sim_energy": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+    "pinc_sim_cycles": (C.c_long, [C.c_void_p]),
+    "pinc_sim_nspecies": (C.c_int, [C.c_void_p]),
+    "pinc_sim_ndims": (C.c_int, [C.c_void_p]),
+    "pinc_sim_pop_count": (C.c_long, [C.c_void_p, C.c_int]),
+    "pinc_sim_pop_get": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]),
+    "pinc_sim_pop_set": (C.c_int, [C.c_void_p, C.c_int, C.c_long, C.c_void_p, C.c_void_p]),
+    "pinc_sim_grid_shape": (C.c_long, [C.c_void_p, C.c_int, C.POINTER(C.c_int)]),
+    "pinc_sim_grid_get": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p]),
+    "pinc_sim_grid_set": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p]),
+    "pinc_sim_emigrants": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "pinc_sim_species": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "pinc_sim_sync": (C.c_int, [C.c_void_p]),
+    "pinc_sim_timers": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "pinc_sim_timers_reset": (C.c_int, [C.c_void_p]),
+    "pinc_sim_total_particles": (C.c_long, [C.c_void_p]),
+}
+for _n, (_r, _a) in _sigs.items():
+    _f = getattr(HOST, _n)
+    _f.restype = _r
+    _f.argtypes = _a
+
+HIP.pinc_hip_comm_unique_id.restype = C.c_int
+HIP.pinc_hip_comm_unique_id.argtypes = [C.c_void_p]
+HIP.pinc_hip_error_string.restype = C.c_char_p
+HIP.pinc_hip_device_count.argtypes = [C.POINTER(C.c_int)]
+
+
+def comm_unique_id() -> bytes:
+    buf = (C.c_ubyte * PINC_COMM_ID_BYTES)()
+    rc = HIP.pinc_hip_comm_unique_id(buf)
+    if rc:
+        raise RuntimeError(f"ncclGetUniqueId failed: {HIP.pinc_hip_error_string().decode()}")
+    return bytes(buf)
+
+
+def header_symbols(header: Path) -> list[str]:
+    """Function names declared in one of the include/*.h headers."""
+    import re
+    text = header.read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    names = re.findall(r"^[A-Za-z_][\w \*]*?\b(\w+)\s*\(", text, flags=re.M)
+    skip = {"if", "for", "while", "return", "sizeof", "defined"}
+    return sorted({n for n in names if n not in skip and not n.startswith("__")})

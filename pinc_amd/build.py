@@ -1,0 +1,85 @@
+"""Build the in-tree native libraries of the MI355X PINC hot path.
+
+    pinc_amd/lib/libpinc_hip.so   gfx950 kernels + C ABI (include/pinc_hip.h)
+    pinc_amd/lib/libpinc.so       host operator surface in C (include/pinc.h)
+    oracle/build/liborc.so        CPU oracle (test infrastructure only)
+
+Run ``python -m pinc_amd.build`` (or ``__graft_entry__.build()``).
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+CSRC = ROOT / "pinc_amd" / "csrc"
+HOST = ROOT / "pinc_amd" / "host"
+LIB = ROOT / "pinc_amd" / "lib"
+OBJ = ROOT / "build" / "obj"
+INC = ROOT / "include"
+
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("PINC_ARCH", "gfx950")
+# -ffp-contract=off: the kernels reproduce the reference's fp64 association
+# order; a fused multiply-add would change the rounding.
+HIP_FLAGS = ["-std=c++17", "-O3", f"--offload-arch={ARCH}", "-ffp-contract=off", "-fPIC",
+             "-munsafe-fp-atomics", f"-I{INC}", f"-I{CSRC}"]
+C_FLAGS = ["-std=c11", "-O2", "-fPIC", "-Wall", "-ffp-contract=off", f"-I{INC}", f"-I{HOST}"]
+
+HIP_SRC = ["runtime.hip", "k_particles.hip", "k_grid.hip", "k_mg.hip"]
+C_SRC = ["pinc_core.c", "pinc_grid.c", "pinc_pop.c", "pinc_pusher.c", "pinc_mg.c", "pinc_regular.c"]
+
+
+def _run(cmd: list[str]) -> None:
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"command failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+
+
+def _newer(src: Path, dst: Path, deps: list[Path]) -> bool:
+    if not dst.exists():
+        return True
+    t = dst.stat().st_mtime
+    return src.stat().st_mtime > t or any(d.stat().st_mtime > t for d in deps)
+
+
+def build(verbose: bool = False, jobs: int = 8) -> dict:
+    LIB.mkdir(parents=True, exist_ok=True)
+    OBJ.mkdir(parents=True, exist_ok=True)
+    hip_deps = [INC / "pinc_hip.h", CSRC / "common.h"]
+    c_deps = [INC / "pinc.h", INC / "pinc_hip.h", HOST / "pinc_internal.h"]
+    jobs_list = []
+    for f in HIP_SRC:
+        src, obj = CSRC / f, OBJ / (f + ".o")
+        if _newer(src, obj, hip_deps):
+            jobs_list.append([HIPCC, *HIP_FLAGS, "-c", str(src), "-o", str(obj)])
+    for f in C_SRC:
+        src, obj = HOST / f, OBJ / (f + ".o")
+        if _newer(src, obj, c_deps):
+            jobs_list.append(["gcc", *C_FLAGS, "-c", str(src), "-o", str(obj)])
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        list(ex.map(_run, jobs_list))
+    hip_objs = [str(OBJ / (f + ".o")) for f in HIP_SRC]
+    c_objs = [str(OBJ / (f + ".o")) for f in C_SRC]
+    libhip = LIB / "libpinc_hip.so"
+    libhost = LIB / "libpinc.so"
+    if jobs_list or not libhip.exists() or not libhost.exists():
+        _run([HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", str(libhip), *hip_objs,
+              "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"])
+        _run(["gcc", "-shared", "-o", str(libhost), *c_objs, f"-L{LIB}", "-lpinc_hip", "-lm",
+              "-Wl,-rpath,$ORIGIN"])
+    # oracle (plain C, test infrastructure)
+    _run(["make", "-s", "-C", str(ROOT / "oracle"), "-j4"])
+    out = {"libpinc_hip": str(libhip), "libpinc": str(libhost),
+           "liborc": str(ROOT / "oracle" / "build" / "liborc.so")}
+    if verbose:
+        print(out)
+    return out
+
+
+if __name__ == "__main__":
+    build(verbose=True)
+    sys.exit(0)

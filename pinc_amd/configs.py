@@ -1,0 +1,134 @@
+"""Run configurations of the BASELINE.json workloads, as ini text.
+
+The reference's input files are not available at run time (the GPU box has
+no /root/reference), so the keys the hot path reads are restated here with
+the values of the reference inputs and the overrides of SURVEY.md 8(d):
+
+  langmuir1d   input/langmuirCold1D.ini + C1 overrides (1-D, 32 cells, 64 ppc)
+  langmuir2d   input/langmuir2D.ini as shipped (32^2, 64 ppc) + overrides
+  c2           langmuir2D at 128^2, 32 ppc (config C2)
+  cold3d       langmuirCold.ini (3-D 32x16x16 per subdomain, 64 ppc)
+  warm         warm_big.ini family: 3-D warm Maxwellian plasma, 64 ppc
+               (config C4 at 256^3; bench.py sizes it per GPU count)
+"""
+from __future__ import annotations
+
+import math
+import os
+import tempfile
+from typing import Mapping
+
+ELEMENTARY_CHARGE = 1.60217733e-19
+ELECTRON_MASS = 9.10938188e-31
+VACUUM_PERMITTIVITY = 8.854187817e-12
+
+_MG_ND = {
+    "cycle": "mgVRecursive", "preSmooth": "gaussSeidelRBND", "postSmooth": "gaussSeidelRBND",
+    "coarseSolver": "gaussSeidelRBND", "mgLevels": "5", "mgCycles": "150", "nPreSmooth": "10",
+    "nPostSmooth": "10", "nCoarseSolve": "10", "prolongator": "bilinearND", "restrictor": "halfWeightND",
+}
+_MG_3D = {
+    "cycle": "mgVRecursive", "preSmooth": "gaussSeidelRB", "postSmooth": "gaussSeidelRB",
+    "coarseSolver": "gaussSeidelRB", "mgLevels": "4", "mgCycles": "15", "nPreSmooth": "10",
+    "nPostSmooth": "10", "nCoarseSolve": "10", "prolongator": "bilinear", "restrictor": "halfWeight",
+}
+
+
+def _langmuir_nd(nd: int) -> dict:
+    per = ",".join(["1 pc", "2 pc", "4 pc"][:nd])
+    zeros = ",".join(["0"] * (2 * nd - 1))
+    return {
+        "time": {"nTimeSteps": "150", "timeStep": "0.2"},
+        "grid": {"nDims": str(nd), "nSubdomains": ",".join(["1"] * nd), "nEmigrantsAlloc": per,
+                 "trueSize": ",".join(["32"] * nd), "stepSize": "6.28 tot", "nGhostLayers": "1",
+                 "thresholds": "0.1", "boundaries": "PERIODIC"},
+        "fields": {"BExt": "0,0,0", "EExt": "0,0,0"},
+        "population": {"nSpecies": "2", "nParticles": "64 pc", "nAlloc": "96 pc" if nd == 1 else "64 pc",
+                       "charge": "-1,1", "mass": "1,1836", "density": "1e11,1e11", "drift": "0",
+                       "perturbAmplitude": "0.001," + zeros, "perturbMode": "1," + zeros,
+                       "thermalVelocity": "0,0", "maxVel": "1"},
+        "methods": {"mode": "regular", "normalization": "semiSI", "poisson": "mgSolver",
+                    "acc": "puAccND1KE", "distr": "puDistrND1", "migrate": "puExtractEmigrantsND"},
+        "multigrid": dict(_MG_ND, mgCycles="15" if nd == 1 else "150"),
+    }
+
+
+def _cold3d() -> dict:
+    return {
+        "time": {"nTimeSteps": "45", "timeStep": "0.2"},
+        "grid": {"nDims": "3", "nSubdomains": "1,1,1", "nEmigrantsAlloc": "1 pc, 2 pc, 4 pc",
+                 "trueSize": "32,16,16", "stepSize": "0.005", "nGhostLayers": "1", "thresholds": "0.1",
+                 "boundaries": "PERIODIC"},
+        "fields": {"BExt": "0,0,0", "EExt": "0,0,0"},
+        "population": {"nSpecies": "2", "nParticles": "64 pc", "nAlloc": "96 pc", "charge": "-1,1",
+                       "mass": "1,1836", "density": "1e11,1e11", "drift": "0",
+                       "perturbAmplitude": "1e-5,0,0,0,0,0", "perturbMode": "1,0,0,0,0,0",
+                       "thermalVelocity": "123000,2872", "maxVel": "1"},
+        "methods": {"mode": "regular", "normalization": "semiSI", "poisson": "mgSolver",
+                    "acc": "puAcc3D1KE", "distr": "puDistr3D1", "migrate": "puExtractEmigrants3D"},
+        "multigrid": dict(_MG_3D),
+    }
+
+
+def thermal_velocity_si(vth_cells_per_step: float, step_size: float, time_step: float, density: float) -> float:
+    """SI thermal speed giving vth cells/step after semiSI normalisation
+    (units.c:159-252: X = stepSize, T = timeStep/omega_pe)."""
+    wpe = math.sqrt(ELEMENTARY_CHARGE ** 2 * density / (VACUUM_PERMITTIVITY * ELECTRON_MASS))
+    T = time_step / wpe
+    return vth_cells_per_step * step_size / T
+
+
+def _warm(true_size=(256, 256, 256), nsub=(1, 1, 1), ppc=64, nalloc_pc=72, vth=0.05, levels=5) -> dict:
+    ve = thermal_velocity_si(vth, 0.2, 0.1, 1e11)
+    vi = ve * math.sqrt(1.0 / 1836)
+    return {
+        "time": {"nTimeSteps": "130", "timeStep": "0.1"},
+        "grid": {"nDims": "3", "nSubdomains": ",".join(map(str, nsub)),
+                 "nEmigrantsAlloc": "0.01 pc,0.02 pc,0.2 pc",
+                 "trueSize": ",".join(map(str, true_size)), "stepSize": "0.2", "nGhostLayers": "1",
+                 "thresholds": "0.1", "boundaries": "PERIODIC"},
+        "fields": {"BExt": "0,0,0", "EExt": "0,0,0"},
+        "population": {"nSpecies": "2", "nParticles": f"{ppc} pc", "nAlloc": f"{nalloc_pc} pc",
+                       "charge": "-1,1", "mass": "1,1836", "density": "1e11,1e11", "drift": "0",
+                       "perturbAmplitude": "0,0,0,0,0,0", "perturbMode": "0,0,0,0,0,0",
+                       "thermalVelocity": f"{ve!r},{vi!r}", "maxVel": "1"},
+        "methods": {"mode": "regular", "normalization": "semiSI", "poisson": "mgSolver",
+                    "acc": "puAcc3D1KE", "distr": "puDistr3D1", "migrate": "puExtractEmigrants3D"},
+        "multigrid": dict(_MG_3D, mgLevels=str(levels)),
+    }
+
+
+def config(name: str, **kw) -> dict:
+    if name == "langmuir1d":
+        return _langmuir_nd(1)
+    if name == "langmuir2d":
+        return _langmuir_nd(2)
+    if name == "c2":
+        c = _langmuir_nd(2)
+        c["grid"]["trueSize"] = "128,128"
+        c["population"]["nParticles"] = "32 pc"
+        c["population"]["nAlloc"] = "48 pc"
+        return c
+    if name == "cold3d":
+        return _cold3d()
+    if name == "warm":
+        return _warm(**kw)
+    raise KeyError(name)
+
+
+def to_ini(cfg: Mapping[str, Mapping[str, str]]) -> str:
+    out = []
+    for sec, kv in cfg.items():
+        out.append(f"[{sec}]")
+        out.extend(f"{k} = {v}" for k, v in kv.items())
+        out.append("")
+    return "\n".join(out)
+
+
+def write_ini(cfg: Mapping[str, Mapping[str, str]], path: str | None = None) -> str:
+    if path is None:
+        fd, path = tempfile.mkstemp(suffix=".ini", prefix="pinc_")
+        os.close(fd)
+    with open(path, "w") as f:
+        f.write(to_ini(cfg))
+    return path

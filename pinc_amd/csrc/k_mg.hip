@@ -1,0 +1,311 @@
+// k_mg.hip -- multigrid Poisson kernels for MI355X (gfx950), periodic grid
+// without ghost cells (every halo of the reference is an index wrap here).
+//
+//   gs_pass        one colour of mgGS3D (multigrid.c:683-767) or mgGSND
+//                  (553-621).  The reference neutralises phi after every
+//                  colour (gBnd -> gNeutralizeGrid, grid.c:730-779).  Here the
+//                  mean is subtracted lazily: the colour that was just
+//                  written is stored raw with its pending mean mu, and every
+//                  read of it evaluates (raw - mu) -- the same rounding as
+//                  the reference's stored value.  Each pass also produces the
+//                  block partial sums of the resulting grid, from which the
+//                  next mean is formed.
+//   materialize    applies the pending means after the last pass
+//   residual       mgResidual + gFinDiff2nd3D/ND (multigrid.c:1385-1403,
+//                  grid.c:264-334)
+//   restrict       mgHalfRestrict3D (1/12 weights) / ND (multigrid.c:844-1022)
+//   prolong_add    mgBilinProl3D/ND followed by gAddTo (multigrid.c:1024-1238,
+//                  1535): the separable z, y, x interpolation is evaluated in
+//                  registers with the reference's intermediate roundings.
+#include "common.h"
+
+using namespace pinc;
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kMaxBlocks = 2048;
+
+inline long ceil_div(long a, long b) { return (a + b - 1) / b; }
+
+struct Lv {
+	int T[3];
+	long s[3];
+};
+
+__device__ __forceinline__ Lv make_lv(const pinc_lvl_t &L) {
+	Lv r;
+	for (int d = 0; d < 3; d++) r.T[d] = L.T[d];
+	r.s[0] = 1;
+	r.s[1] = L.T[0];
+	r.s[2] = (long)L.T[0] * L.T[1];
+	return r;
+}
+
+// neighbour offsets of point (c) along dim d with periodic wrap
+__device__ __forceinline__ long nb_up(const Lv &L, const int *c, int d) {
+	return (c[d] + 1 < L.T[d]) ? L.s[d] : -(long)(L.T[d] - 1) * L.s[d];
+}
+__device__ __forceinline__ long nb_dn(const Lv &L, const int *c, int d) {
+	return (c[d] > 0) ? -L.s[d] : (long)(L.T[d] - 1) * L.s[d];
+}
+
+template <int ND, bool GS3D>
+__global__ __launch_bounds__(kThreads) void k_gs_pass(double *__restrict__ phi,
+                                                      const double *__restrict__ rho, pinc_lvl_t Lp,
+                                                      int pass, const double *__restrict__ muPrev,
+                                                      double *__restrict__ partial) {
+	__shared__ double red[kThreads / 64];
+	Lv L = make_lv(Lp);
+	double mu = muPrev ? *muPrev : 0.0;
+	long half = L.T[0] / 2;
+	long nPairs = half * L.T[1] * L.T[2];
+	double acc = 0.;
+	for (long q = (long)blockIdx.x * blockDim.x + threadIdx.x; q < nPairs; q += (long)gridDim.x * blockDim.x) {
+		int c[3];
+		long r = q / half;
+		int i = (int)(q - r * half);
+		c[1] = (int)(r % L.T[1]);
+		c[2] = (int)(r / L.T[1]);
+		int par = (pass + c[1] + c[2]) & 1;
+		c[0] = 2 * i + par;            // point of the colour being updated
+		int xo = 2 * i + 1 - par;      // point of the other colour
+		long g = (long)c[0] + c[1] * L.s[1] + c[2] * L.s[2];
+		double v;
+		if (GS3D) {
+			double xp = phi[g + nb_up(L, c, 0)] - mu, xm = phi[g + nb_dn(L, c, 0)] - mu;
+			double yp = phi[g + nb_up(L, c, 1)] - mu, ym = phi[g + nb_dn(L, c, 1)] - mu;
+			double zp = phi[g + nb_up(L, c, 2)] - mu, zm = phi[g + nb_dn(L, c, 2)] - mu;
+			v = (1. / 6.) * (xp + xm + yp + ym + zp + zm + rho[g]);
+		} else {
+			v = 0;
+#pragma unroll
+			for (int d = 0; d < ND; d++) {
+				double a = phi[g + nb_up(L, c, d)] - mu, b = phi[g + nb_dn(L, c, d)] - mu;
+				v += a + b;
+			}
+			v += rho[g];
+			v *= 1. / (2 * ND);
+		}
+		phi[g] = v;
+		long go = g + (xo - c[0]);
+		acc += v + (phi[go] - mu);
+	}
+	double t = block_sum(acc, red);
+	if (threadIdx.x == 0) partial[blockIdx.x] = t;
+}
+
+__global__ void k_gs_materialize(double *__restrict__ phi, pinc_lvl_t Lp, int lastPass,
+                                 const double *__restrict__ muA, const double *__restrict__ muB) {
+	Lv L = make_lv(Lp);
+	long n = (long)L.T[0] * L.T[1] * L.T[2];
+	double a = muA ? *muA : 0.0, b = *muB;
+	for (long g = (long)blockIdx.x * blockDim.x + threadIdx.x; g < n; g += (long)gridDim.x * blockDim.x) {
+		int x = (int)(g % L.T[0]);
+		long r = g / L.T[0];
+		int y = (int)(r % L.T[1]), z = (int)(r / L.T[1]);
+		if (((x + y + z) & 1) == lastPass) phi[g] = phi[g] - b;
+		else phi[g] = (phi[g] - a) - b;
+	}
+}
+
+template <int ND>
+__device__ __forceinline__ double residual_at(const double *__restrict__ phi,
+                                              const double *__restrict__ rho, const Lv &L,
+                                              const int *c, long g) {
+	double r;
+	if (ND == 3) {
+		r = -6. * phi[g];
+		r += phi[g + nb_up(L, c, 0)] + phi[g + nb_dn(L, c, 0)] + phi[g + nb_up(L, c, 1)] +
+		     phi[g + nb_dn(L, c, 1)] + phi[g + nb_up(L, c, 2)] + phi[g + nb_dn(L, c, 2)];
+	} else {
+		r = -(2. * ND) * phi[g];
+#pragma unroll
+		for (int d = 0; d < ND; d++) r += phi[g + nb_up(L, c, d)] + phi[g + nb_dn(L, c, d)];
+	}
+	return r + rho[g];
+}
+
+template <int ND>
+__global__ void k_residual(double *__restrict__ res, const double *__restrict__ phi,
+                           const double *__restrict__ rho, pinc_lvl_t Lp) {
+	Lv L = make_lv(Lp);
+	long n = (long)L.T[0] * L.T[1] * L.T[2];
+	for (long g = (long)blockIdx.x * blockDim.x + threadIdx.x; g < n; g += (long)gridDim.x * blockDim.x) {
+		int c[3];
+		c[0] = (int)(g % L.T[0]);
+		long r = g / L.T[0];
+		c[1] = (int)(r % L.T[1]);
+		c[2] = (int)(r / L.T[1]);
+		res[g] = residual_at<ND>(phi, rho, L, c, g);
+	}
+}
+
+template <int ND>
+__global__ __launch_bounds__(kThreads) void k_residual_sumsq(const double *__restrict__ phi,
+                                                             const double *__restrict__ rho,
+                                                             pinc_lvl_t Lp,
+                                                             double *__restrict__ partial) {
+	__shared__ double red[kThreads / 64];
+	Lv L = make_lv(Lp);
+	long n = (long)L.T[0] * L.T[1] * L.T[2];
+	double acc = 0.;
+	for (long g = (long)blockIdx.x * blockDim.x + threadIdx.x; g < n; g += (long)gridDim.x * blockDim.x) {
+		int c[3];
+		c[0] = (int)(g % L.T[0]);
+		long r = g / L.T[0];
+		c[1] = (int)(r % L.T[1]);
+		c[2] = (int)(r / L.T[1]);
+		double v = residual_at<ND>(phi, rho, L, c, g);
+		acc += v * v;
+	}
+	double t = block_sum(acc, red);
+	if (threadIdx.x == 0) partial[blockIdx.x] = t;
+}
+
+template <int ND, bool HW3D>
+__global__ void k_restrict(const double *__restrict__ fine, double *__restrict__ coarse, pinc_lvl_t Lc) {
+	Lv C = make_lv(Lc);
+	pinc_lvl_t Lfp = Lc;
+	for (int d = 0; d < ND; d++) Lfp.T[d] = 2 * Lc.T[d];
+	Lv F = make_lv(Lfp);
+	long n = (long)C.T[0] * C.T[1] * C.T[2];
+	for (long gc = (long)blockIdx.x * blockDim.x + threadIdx.x; gc < n; gc += (long)gridDim.x * blockDim.x) {
+		int cc[3], cf[3] = {0, 0, 0};
+		cc[0] = (int)(gc % C.T[0]);
+		long r = gc / C.T[0];
+		cc[1] = (int)(r % C.T[1]);
+		cc[2] = (int)(r / C.T[1]);
+		long gf = 0;
+		for (int d = 0; d < ND; d++) {
+			cf[d] = 2 * cc[d];
+			gf += (long)cf[d] * F.s[d];
+		}
+		double v;
+		if (HW3D) {
+			v = (1. / 12.) * (6 * fine[gf] + fine[gf + nb_up(F, cf, 0)] + fine[gf + nb_dn(F, cf, 0)] +
+			                  fine[gf + nb_up(F, cf, 1)] + fine[gf + nb_dn(F, cf, 1)] +
+			                  fine[gf + nb_up(F, cf, 2)] + fine[gf + nb_dn(F, cf, 2)]);
+		} else {
+			v = (2. * ND) * fine[gf];
+#pragma unroll
+			for (int d = 0; d < ND; d++) v += fine[gf + nb_up(F, cf, d)] + fine[gf + nb_dn(F, cf, d)];
+			v *= 1. / (ND * 4);
+		}
+		coarse[gc] = v;
+	}
+}
+
+// Value of the prolongated coarse grid at fine point cf.  The reference
+// interpolates the highest dimension first (z, then y, then x, each pass
+// preceded by a TOHALO of that dimension), so a point that is odd in several
+// dimensions is the average, along its LOWEST odd dimension, of values
+// already interpolated along the higher ones.  Evaluating from dim 0 upward
+// reproduces every intermediate rounding of the reference.
+template <int ND, int D>
+__device__ __forceinline__ double prol_low(const double *__restrict__ cv, const Lv &C, const int *cf) {
+	if constexpr (D == ND) {
+		long g = 0;
+		for (int d = 0; d < ND; d++) g += (long)(cf[d] >> 1) * C.s[d];
+		return cv[g];
+	} else {
+		if (!(cf[D] & 1)) return prol_low<ND, D + 1>(cv, C, cf);
+		int a[3] = {cf[0], cf[1], cf[2]}, b[3] = {cf[0], cf[1], cf[2]};
+		a[D] = cf[D] - 1;
+		b[D] = cf[D] + 1;
+		if (b[D] >= 2 * C.T[D]) b[D] -= 2 * C.T[D];
+		return 0.5 * (prol_low<ND, D + 1>(cv, C, a) + prol_low<ND, D + 1>(cv, C, b));
+	}
+}
+
+template <int ND>
+__global__ void k_prolong_add(double *__restrict__ phiF, const double *__restrict__ phiC, pinc_lvl_t Lf) {
+	pinc_lvl_t Lcp = Lf;
+	for (int d = 0; d < ND; d++) Lcp.T[d] = Lf.T[d] / 2;
+	Lv C = make_lv(Lcp);
+	Lv F = make_lv(Lf);
+	long n = (long)F.T[0] * F.T[1] * F.T[2];
+	for (long g = (long)blockIdx.x * blockDim.x + threadIdx.x; g < n; g += (long)gridDim.x * blockDim.x) {
+		int cf[3];
+		cf[0] = (int)(g % F.T[0]);
+		long r = g / F.T[0];
+		cf[1] = (int)(r % F.T[1]);
+		cf[2] = (int)(r / F.T[1]);
+		phiF[g] += prol_low<ND, 0>(phiC, C, cf);
+	}
+}
+
+inline unsigned blocks_for(long n) {
+	long b = ceil_div(n, (long)kThreads * 4);
+	if (b < 1) b = 1;
+	if (b > kMaxBlocks) b = kMaxBlocks;
+	return (unsigned)b;
+}
+
+inline long npts(const pinc_lvl_t &L) { return (long)L.T[0] * L.T[1] * L.T[2]; }
+
+}  // namespace
+
+extern "C" int pinc_hip_gs_pass(double *phi, const double *rho, pinc_lvl_t L, int pass, int nd3,
+                                const double *muPrev, double *partial, int *nBlocks, void *stream) {
+	long nPairs = npts(L) / 2;
+	unsigned nb = blocks_for(nPairs);
+	*nBlocks = (int)nb;
+	hipStream_t st = (hipStream_t)stream;
+	if (L.nd == 3 && nd3)
+		hipLaunchKernelGGL((k_gs_pass<3, true>), dim3(nb), dim3(kThreads), 0, st, phi, rho, L, pass, muPrev, partial);
+	else if (L.nd == 3)
+		hipLaunchKernelGGL((k_gs_pass<3, false>), dim3(nb), dim3(kThreads), 0, st, phi, rho, L, pass, muPrev, partial);
+	else if (L.nd == 2)
+		hipLaunchKernelGGL((k_gs_pass<2, false>), dim3(nb), dim3(kThreads), 0, st, phi, rho, L, pass, muPrev, partial);
+	else
+		hipLaunchKernelGGL((k_gs_pass<1, false>), dim3(nb), dim3(kThreads), 0, st, phi, rho, L, pass, muPrev, partial);
+	return check_launch("gs_pass");
+}
+
+extern "C" int pinc_hip_gs_materialize(double *phi, pinc_lvl_t L, int lastPass, const double *muA,
+                                       const double *muB, void *stream) {
+	hipLaunchKernelGGL(k_gs_materialize, dim3(blocks_for(npts(L))), dim3(kThreads), 0,
+	                   (hipStream_t)stream, phi, L, lastPass, muA, muB);
+	return check_launch("gs_materialize");
+}
+
+extern "C" int pinc_hip_residual(double *res, const double *phi, const double *rho, pinc_lvl_t L,
+                                 void *stream) {
+	hipStream_t st = (hipStream_t)stream;
+	unsigned nb = blocks_for(npts(L));
+	if (L.nd == 3) hipLaunchKernelGGL(k_residual<3>, dim3(nb), dim3(kThreads), 0, st, res, phi, rho, L);
+	else if (L.nd == 2) hipLaunchKernelGGL(k_residual<2>, dim3(nb), dim3(kThreads), 0, st, res, phi, rho, L);
+	else hipLaunchKernelGGL(k_residual<1>, dim3(nb), dim3(kThreads), 0, st, res, phi, rho, L);
+	return check_launch("residual");
+}
+
+extern "C" int pinc_hip_residual_sumsq(const double *phi, const double *rho, pinc_lvl_t L,
+                                       double *partial, int *nBlocks, void *stream) {
+	hipStream_t st = (hipStream_t)stream;
+	unsigned nb = blocks_for(npts(L));
+	*nBlocks = (int)nb;
+	if (L.nd == 3) hipLaunchKernelGGL(k_residual_sumsq<3>, dim3(nb), dim3(kThreads), 0, st, phi, rho, L, partial);
+	else if (L.nd == 2) hipLaunchKernelGGL(k_residual_sumsq<2>, dim3(nb), dim3(kThreads), 0, st, phi, rho, L, partial);
+	else hipLaunchKernelGGL(k_residual_sumsq<1>, dim3(nb), dim3(kThreads), 0, st, phi, rho, L, partial);
+	return check_launch("residual_sumsq");
+}
+
+extern "C" int pinc_hip_restrict(const double *fine, double *coarse, pinc_lvl_t Lc, int nd3, void *stream) {
+	hipStream_t st = (hipStream_t)stream;
+	unsigned nb = blocks_for(npts(Lc));
+	if (Lc.nd == 3 && nd3) hipLaunchKernelGGL((k_restrict<3, true>), dim3(nb), dim3(kThreads), 0, st, fine, coarse, Lc);
+	else if (Lc.nd == 3) hipLaunchKernelGGL((k_restrict<3, false>), dim3(nb), dim3(kThreads), 0, st, fine, coarse, Lc);
+	else if (Lc.nd == 2) hipLaunchKernelGGL((k_restrict<2, false>), dim3(nb), dim3(kThreads), 0, st, fine, coarse, Lc);
+	else hipLaunchKernelGGL((k_restrict<1, false>), dim3(nb), dim3(kThreads), 0, st, fine, coarse, Lc);
+	return check_launch("restrict");
+}
+
+extern "C" int pinc_hip_prolong_add(double *phiF, const double *phiC, pinc_lvl_t Lf, void *stream) {
+	hipStream_t st = (hipStream_t)stream;
+	unsigned nb = blocks_for(npts(Lf));
+	if (Lf.nd == 3) hipLaunchKernelGGL(k_prolong_add<3>, dim3(nb), dim3(kThreads), 0, st, phiF, phiC, Lf);
+	else if (Lf.nd == 2) hipLaunchKernelGGL(k_prolong_add<2>, dim3(nb), dim3(kThreads), 0, st, phiF, phiC, Lf);
+	else hipLaunchKernelGGL(k_prolong_add<1>, dim3(nb), dim3(kThreads), 0, st, phiF, phiC, Lf);
+	return check_launch("prolong_add");
+}

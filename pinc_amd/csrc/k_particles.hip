@@ -1,0 +1,817 @@
+// k_particles.hip -- particle kernels of the PINC hot path for MI355X (gfx950).
+//
+//   move + classify     puMove (pusher.c:86-119) fused with the neighbour test
+//                       of puExtractEmigrants3D/ND (pusher.c:782-910)
+//   extract             the reference's serial back-fill compaction, made
+//                       parallel without changing its result or the order in
+//                       which emigrants are listed (DESIGN.md "Migration")
+//   import              shiftImmigrants + importParticles (pusher.c:941-985)
+//   deposit             puDistr3D1 / puDistrND1 (pusher.c:512-638)
+//   accelerate          puAcc3D1KE / puAccND1KE + interpolators
+//                       (pusher.c:178-265, 1089-1162)
+//   init                pPosLattice / pPosPerturb / pVel* (population.c)
+//
+// All arithmetic is fp64 in the reference's association order; the library
+// is compiled with -ffp-contract=off so no multiply-add is fused.
+#include "common.h"
+
+using namespace pinc;
+
+namespace {
+
+struct Thr {
+	double lo[3], up[3], hi[3];
+};
+
+constexpr int kThreads = 256;
+constexpr int kItems = PINC_CHUNK / kThreads;
+
+__device__ __forceinline__ unsigned long long lanemask_lt() {
+	return (1ull << (threadIdx.x & 63)) - 1ull;
+}
+
+// ------------------------------------------------------------ move --------
+template <int ND>
+__global__ __launch_bounds__(kThreads) void k_move_classify(
+		double *__restrict__ x0, double *__restrict__ x1, double *__restrict__ x2,
+		const double *__restrict__ v0, const double *__restrict__ v1,
+		const double *__restrict__ v2, long n, int doMove, Thr thr, int center,
+		unsigned char *__restrict__ flags, int *__restrict__ chunkCount, double maxVel,
+		int *__restrict__ err) {
+	__shared__ int wcnt[kThreads / 64];
+	double *xs[3] = {x0, x1, x2};
+	const double *vs[3] = {v0, v1, v2};
+	long base = (long)blockIdx.x * PINC_CHUNK;
+	int cnt = 0;
+	int bad = 0;
+#pragma unroll 2
+	for (int k = 0; k < kItems; k++) {
+		long i = base + k * kThreads + threadIdx.x;
+		if (i >= n) break;
+		double p[ND];
+#pragma unroll
+		for (int d = 0; d < ND; d++) {
+			p[d] = xs[d][i];
+			if (doMove) {
+				double v = vs[d][i];
+				bad |= (v > maxVel);  // pVelAssertMax (population.c:342-365)
+				p[d] += v;
+				xs[d][i] = p[d];
+			}
+		}
+		int ne = 0;
+#pragma unroll
+		for (int d = ND - 1; d >= 0; d--) {
+			int dig = 1 - (p[d] < thr.lo[d]) + (p[d] >= thr.up[d]);
+			ne = ne * 3 + dig;
+			// pPosAssertInLocalFrame after the periodic shift (population.c:316-340)
+			double q = p[d] - (double)(dig - 1) * (thr.hi[d] - 1.0);
+			bad |= (q < 0.0 || q > thr.hi[d]) << 1;
+		}
+		flags[i] = (unsigned char)ne;
+		cnt += (ne != center);
+	}
+	if (bad) atomicOr(err, bad);
+	int wsum = wave_sum(cnt);
+	if ((threadIdx.x & 63) == 0) wcnt[threadIdx.x >> 6] = wsum;
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		int t = 0;
+		for (int w = 0; w < kThreads / 64; w++) t += wcnt[w];
+		chunkCount[blockIdx.x] = t;
+	}
+}
+
+// --------------------------------------------------- single-block scans ---
+// exclusive scan of in[0..n) into out[0..n], out[n] = total
+__global__ __launch_bounds__(1024) void k_scan_single(const int *__restrict__ in,
+                                                      int *__restrict__ out, int n) {
+	__shared__ long part[1024];
+	int t = threadIdx.x;
+	int seg = (n + 1023) / 1024;
+	int a = t * seg, b = min(n, a + seg);
+	long s = 0;
+	for (int i = a; i < b; i++) s += in[i];
+	part[t] = s;
+	__syncthreads();
+	for (int o = 1; o < 1024; o <<= 1) {
+		long v = (t >= o) ? part[t - o] : 0;
+		__syncthreads();
+		part[t] += v;
+		__syncthreads();
+	}
+	long run = part[t] - s;
+	for (int i = a; i < b; i++) {
+		int v = in[i];
+		out[i] = (int)run;
+		run += v;
+	}
+	if (t == 1023) out[n] = (int)part[1023];
+}
+
+// ----------------------------------------------------------- extract ------
+// Per particle j (relative to the species start) with E(j) = emigrants
+// before j, n particles, E emigrants, m = n-E survivors:
+//   emigrant j<m   is hole number k=E(j)+1
+//   survivor j>=m  is tail survivor number r = n-j-E+E(j) (counted from the end)
+//   emigrant j>m   is extracted at position n-j
+// (derivation: DESIGN.md "Migration"; checked against the serial loop).
+__global__ __launch_bounds__(kThreads) void k_extract_a(
+		const unsigned char *__restrict__ flags, long n, int center,
+		const int *__restrict__ chunkOffset, int nChunks, int *__restrict__ tail,
+		int *__restrict__ holes, int *__restrict__ order, int *__restrict__ scratch) {
+	__shared__ int wtot[kThreads / 64];
+	long E = chunkOffset[nChunks];
+	long m = n - E;
+	long base = (long)blockIdx.x * PINC_CHUNK;
+	int running = chunkOffset[blockIdx.x];
+	int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+	for (int k = 0; k < kItems; k++) {
+		long i = base + k * kThreads + threadIdx.x;
+		bool in = i < n;
+		bool emig = in && flags[i] != center;
+		unsigned long long b = __ballot(emig);
+		int rw = __popcll(b & lanemask_lt());
+		if (lane == 0) wtot[w] = __popcll(b);
+		__syncthreads();
+		int before = 0, tot = 0;
+		for (int q = 0; q < kThreads / 64; q++) {
+			before += (q < w) ? wtot[q] : 0;
+			tot += wtot[q];
+		}
+		long Ej = running + before + rw;
+		if (in) {
+			if (emig) {
+				if (i < m) holes[Ej + 1] = (int)i;
+				else if (i > m) order[n - i] = (int)i;
+			} else if (i >= m) {
+				tail[n - i - E + Ej] = (int)i;
+			}
+			if (i == m) scratch[0] = (int)Ej;  // number of holes
+		}
+		running += tot;
+		__syncthreads();
+	}
+}
+
+__global__ void k_extract_b(const unsigned char *__restrict__ flags, long n, long E, int center,
+                            const int *__restrict__ tail, const int *__restrict__ holes,
+                            int *__restrict__ order, const int *__restrict__ scratch) {
+	long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
+	long m = n - E;
+	int h = scratch[0];
+	if (q >= 1 && q <= h) {
+		long prevT = (q == 1) ? n : tail[q - 1];
+		order[n - prevT] = holes[q];
+	}
+	if (q == 0 && m < n && flags[m] != center) {
+		long t = h ? tail[h] : n;
+		order[n - t] = (int)m;
+	}
+}
+
+// per-block direction histogram over the extraction order
+constexpr int kRankItems = 4;
+constexpr int kRankChunk = kThreads * kRankItems;
+constexpr int kMaxNe = 27;
+
+__global__ __launch_bounds__(kThreads) void k_rank_hist(const unsigned char *__restrict__ flags,
+                                                        const int *__restrict__ order, long E,
+                                                        int *__restrict__ blockHist) {
+	__shared__ int hist[kMaxNe];
+	if (threadIdx.x < kMaxNe) hist[threadIdx.x] = 0;
+	__syncthreads();
+	long base = (long)blockIdx.x * kRankChunk;
+	for (int k = 0; k < kRankItems; k++) {
+		long p = base + k * kThreads + threadIdx.x;
+		if (p < E) atomicAdd(&hist[flags[order[p]]], 1);
+	}
+	__syncthreads();
+	if (threadIdx.x < kMaxNe) blockHist[(long)blockIdx.x * kMaxNe + threadIdx.x] = hist[threadIdx.x];
+}
+
+// exclusive scan per direction over blocks; bases per direction; counts
+__global__ __launch_bounds__(kMaxNe * 32) void k_hist_scan(int *__restrict__ blockHist, int nb,
+                                                           int *__restrict__ scratch) {
+	// scratch[32..32+27): base of each direction, scratch[64..64+27): count
+	__shared__ int tot[kMaxNe];
+	int ne = threadIdx.x >> 5, l = threadIdx.x & 31;
+	if (ne < kMaxNe && l == 0) {
+		int run = 0;
+		for (int b = 0; b < nb; b++) {
+			int v = blockHist[(long)b * kMaxNe + ne];
+			blockHist[(long)b * kMaxNe + ne] = run;
+			run += v;
+		}
+		tot[ne] = run;
+	}
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		int run = 0;
+		for (int q = 0; q < kMaxNe; q++) {
+			scratch[32 + q] = run;
+			scratch[64 + q] = tot[q];
+			run += tot[q];
+		}
+	}
+}
+
+// stable scatter of emigrants into the direction-ordered buffer
+__global__ __launch_bounds__(kThreads) void k_rank_scatter(
+		const unsigned char *__restrict__ flags, const int *__restrict__ order, long E,
+		const int *__restrict__ blockHist, const int *__restrict__ scratch, pinc_pop_t pop,
+		long sbase, double *__restrict__ buf, long cap, unsigned char *__restrict__ bufNe) {
+	__shared__ int waveCnt[kThreads / 64][kMaxNe];
+	__shared__ int running[kMaxNe];
+	int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+	if (threadIdx.x < kMaxNe) running[threadIdx.x] = 0;
+	long base = (long)blockIdx.x * kRankChunk;
+	for (int k = 0; k < kRankItems; k++) {
+		for (int q = threadIdx.x; q < (kThreads / 64) * kMaxNe; q += kThreads)
+			(&waveCnt[0][0])[q] = 0;
+		__syncthreads();
+		long p = base + k * kThreads + threadIdx.x;
+		bool in = p < E;
+		int j = in ? order[p] : 0;
+		int ne = in ? flags[j] : 31;
+		// lanes with the same direction (match-any over 5 bits)
+		unsigned long long same = __ballot(in);
+#pragma unroll
+		for (int bit = 0; bit < 5; bit++) {
+			unsigned long long bb = __ballot((ne >> bit) & 1);
+			same &= ((ne >> bit) & 1) ? bb : ~bb;
+		}
+		int rw = __popcll(same & lanemask_lt());
+		if (in && rw == 0) waveCnt[w][ne] = __popcll(same);
+		__syncthreads();
+		if (in) {
+			int off = running[ne] + rw;
+			for (int q = 0; q < w; q++) off += waveCnt[q][ne];
+			long dst = (long)scratch[32 + ne] + blockHist[(long)blockIdx.x * kMaxNe + ne] + off;
+			long src = sbase + j;
+			for (int d = 0; d < pop.nd; d++) {
+				buf[d * cap + dst] = pop.x[d][src];
+				buf[(3 + d) * cap + dst] = pop.v[d][src];
+			}
+			bufNe[dst] = (unsigned char)ne;
+		}
+		__syncthreads();
+		if (threadIdx.x < kMaxNe) {
+			int t = 0;
+			for (int q = 0; q < kThreads / 64; q++) t += waveCnt[q][threadIdx.x];
+			running[threadIdx.x] += t;
+		}
+		__syncthreads();
+	}
+}
+
+__global__ void k_fill_holes(pinc_pop_t pop, long sbase, const int *__restrict__ tail,
+                             const int *__restrict__ holes, const int *__restrict__ scratch) {
+	long k = (long)blockIdx.x * blockDim.x + threadIdx.x + 1;
+	int h = scratch[0];
+	if (k > h) return;
+	long src = sbase + tail[k], dst = sbase + holes[k];
+	for (int d = 0; d < pop.nd; d++) {
+		pop.x[d][dst] = pop.x[d][src];
+		pop.v[d][dst] = pop.v[d][src];
+	}
+}
+
+__global__ void k_import(pinc_pop_t pop, long dst, const double *__restrict__ buf, long cap,
+                         const unsigned char *__restrict__ bufNe, long first, long n, int T0,
+                         int T1, int T2, int shiftMask) {
+	long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
+	if (q >= n) return;
+	long e = first + q;
+	int ne = bufNe[e];
+	int T[3] = {T0, T1, T2};
+	for (int d = 0; d < pop.nd; d++) {
+		int dig = ne % 3;
+		ne /= 3;
+		// receiver tag t = reciprocal(ne): shift = (digit_d(t)-1)*T_d = (1-dig)*T_d
+		double shift = ((shiftMask >> d) & 1) ? (double)((1 - dig) * T[d]) : 0.0;
+		pop.x[d][dst + q] = buf[d * cap + e] + shift;
+		pop.v[d][dst + q] = buf[(3 + d) * cap + e];
+	}
+}
+
+__global__ void k_pack(const double *__restrict__ buf, long cap, const unsigned char *__restrict__ bufNe,
+                       long first, long n, int nd, double *__restrict__ out) {
+	long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
+	if (q >= n) return;
+	long e = first + q;
+	double *r = out + q * PINC_REC;
+	for (int d = 0; d < 3; d++) {
+		r[d] = d < nd ? buf[d * cap + e] : 0.0;
+		r[3 + d] = d < nd ? buf[(3 + d) * cap + e] : 0.0;
+	}
+	r[6] = (double)bufNe[e];
+}
+
+__global__ void k_import_rec(pinc_pop_t pop, long dst, const double *__restrict__ rec, long n, int T0,
+                             int T1, int T2) {
+	long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
+	if (q >= n) return;
+	const double *r = rec + q * PINC_REC;
+	int ne = (int)r[6];
+	int T[3] = {T0, T1, T2};
+	for (int d = 0; d < pop.nd; d++) {
+		int dig = ne % 3;
+		ne /= 3;
+		pop.x[d][dst + q] = r[d] + (double)((1 - dig) * T[d]);
+		pop.v[d][dst + q] = r[3 + d];
+	}
+}
+
+// ---------------------------------------------------------- deposit -------
+struct Geo {
+	int T[3];      // storage extent per dim (slab dim: nloc)
+	long stride[3];
+	int slab;      // slab dimension
+};
+
+__device__ __forceinline__ Geo make_geo(const pinc_geom_t &g) {
+	Geo r;
+	for (int d = 0; d < 3; d++) r.T[d] = g.T[d];
+	r.slab = g.nd - 1;
+	r.T[r.slab] = g.nloc;
+	long s = 1;
+	for (int d = 0; d < g.nd; d++) {
+		r.stride[d] = s;
+		s *= (d == r.slab) ? (long)(g.nloc + 2) : (long)r.T[d];
+	}
+	return r;
+}
+
+// storage coordinate of padded node coordinate p in dim d
+__device__ __forceinline__ long node_off(const Geo &G, int d, int p) {
+	int s = (d == G.slab) ? p : wrap_pad(p, G.T[d]);
+	return (long)s * G.stride[d];
+}
+
+template <int ND, bool V3D>
+__global__ __launch_bounds__(kThreads) void k_deposit(const double *__restrict__ x0,
+                                                      const double *__restrict__ x1,
+                                                      const double *__restrict__ x2, long n,
+                                                      pinc_geom_t g, double *__restrict__ rho) {
+	Geo G = make_geo(g);
+	const double *xs[3] = {x0, x1, x2};
+	for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+	     i += (long)gridDim.x * blockDim.x) {
+		double dec[3], comp[3];
+		long o0[3], o1[3];
+#pragma unroll
+		for (int d = 0; d < ND; d++) {
+			double p = xs[d][i];
+			int j = (int)p;
+			dec[d] = p - j;
+			comp[d] = 1 - dec[d];
+			o0[d] = node_off(G, d, j);
+			o1[d] = node_off(G, d, j + 1);
+		}
+		if (V3D) {
+			// puDistr3D1: weights (xc*yc)*zc etc. (pusher.c:550-565)
+			double xc = comp[0], yc = comp[1], zc = comp[2];
+			double x = dec[0], y = dec[1], z = dec[2];
+			unsafeAtomicAdd(&rho[o0[0] + o0[1] + o0[2]], xc * yc * zc);
+			unsafeAtomicAdd(&rho[o1[0] + o0[1] + o0[2]], x * yc * zc);
+			unsafeAtomicAdd(&rho[o0[0] + o1[1] + o0[2]], xc * y * zc);
+			unsafeAtomicAdd(&rho[o1[0] + o1[1] + o0[2]], x * y * zc);
+			unsafeAtomicAdd(&rho[o0[0] + o0[1] + o1[2]], xc * yc * z);
+			unsafeAtomicAdd(&rho[o1[0] + o0[1] + o1[2]], x * yc * z);
+			unsafeAtomicAdd(&rho[o0[0] + o1[1] + o1[2]], xc * y * z);
+			unsafeAtomicAdd(&rho[o1[0] + o1[1] + o1[2]], x * y * z);
+		} else {
+			// puDistrND1Inner: factor of the outer dims, then comp/dec of x
+			// (pusher.c:626-638): w = c_x*(c_y*(c_z*1))
+#pragma unroll
+			for (int c = 0; c < (1 << ND); c++) {
+				double f = 1.0;
+				long off = 0;
+#pragma unroll
+				for (int d = ND - 1; d >= 1; d--) {
+					int b = (c >> d) & 1;
+					f = (b ? dec[d] : comp[d]) * f;
+					off += b ? o1[d] : o0[d];
+				}
+				int b0 = c & 1;
+				double wgt = (b0 ? dec[0] : comp[0]) * f;
+				off += b0 ? o1[0] : o0[0];
+				unsafeAtomicAdd(&rho[off], wgt);
+			}
+		}
+	}
+}
+
+// ------------------------------------------------------- accelerate -------
+constexpr int kAccItems = 8;
+constexpr int kAccChunk = kThreads * kAccItems;
+
+__device__ __forceinline__ double chain(double e, double pre, const double *qm, const double *mq,
+                                        int s) {
+	double v = e * pre;
+	for (int t = 0; t < s; t++) v = (v * qm[t]) * mq[t];
+	return v * qm[s];
+}
+
+template <int ND, bool V3D, bool KE>
+__global__ __launch_bounds__(kThreads) void k_accel(const double *__restrict__ x0,
+                                                    const double *__restrict__ x1,
+                                                    const double *__restrict__ x2,
+                                                    double *__restrict__ v0, double *__restrict__ v1,
+                                                    double *__restrict__ v2, long n, pinc_geom_t g,
+                                                    const double *__restrict__ E, int s,
+                                                    const double *__restrict__ qmArr,
+                                                    const double *__restrict__ mqArr, double pre,
+                                                    double *__restrict__ kePartial) {
+	__shared__ double red[kThreads / 64];
+	__shared__ double sqm[PINC_MAX_SPECIES], smq[PINC_MAX_SPECIES];
+	if (threadIdx.x < PINC_MAX_SPECIES) {
+		sqm[threadIdx.x] = qmArr[threadIdx.x];
+		smq[threadIdx.x] = mqArr[threadIdx.x];
+	}
+	__syncthreads();
+	Geo G = make_geo(g);
+	const double *xs[3] = {x0, x1, x2};
+	double *vs[3] = {v0, v1, v2};
+	double ke = 0.;
+	long base = (long)blockIdx.x * kAccChunk;
+	for (int k = 0; k < kAccItems; k++) {
+		long i = base + k * kThreads + threadIdx.x;
+		if (i >= n) break;
+		double dec[3], comp[3];
+		long o0[3], o1[3];
+#pragma unroll
+		for (int d = 0; d < ND; d++) {
+			double p = xs[d][i];
+			int j = (int)p;
+			dec[d] = p - j;
+			comp[d] = 1 - dec[d];
+			o0[d] = node_off(G, d, j) * ND;
+			o1[d] = node_off(G, d, j + 1) * ND;
+		}
+		double dv[ND];
+		if (V3D) {
+			double x = dec[0], y = dec[1], z = dec[2];
+			double xc = comp[0], yc = comp[1], zc = comp[2];
+			long p000 = o0[0] + o0[1] + o0[2], p100 = o1[0] + o0[1] + o0[2];
+			long p010 = o0[0] + o1[1] + o0[2], p110 = o1[0] + o1[1] + o0[2];
+			long p001 = o0[0] + o0[1] + o1[2], p101 = o1[0] + o0[1] + o1[2];
+			long p011 = o0[0] + o1[1] + o1[2], p111 = o1[0] + o1[1] + o1[2];
+#pragma unroll
+			for (int v = 0; v < ND; v++) {
+				double e000 = chain(E[p000 + v], pre, sqm, smq, s);
+				double e100 = chain(E[p100 + v], pre, sqm, smq, s);
+				double e010 = chain(E[p010 + v], pre, sqm, smq, s);
+				double e110 = chain(E[p110 + v], pre, sqm, smq, s);
+				double e001 = chain(E[p001 + v], pre, sqm, smq, s);
+				double e101 = chain(E[p101 + v], pre, sqm, smq, s);
+				double e011 = chain(E[p011 + v], pre, sqm, smq, s);
+				double e111 = chain(E[p111 + v], pre, sqm, smq, s);
+				dv[v] = zc * (yc * (xc * e000 + x * e100) + y * (xc * e010 + x * e110)) +
+				        z * (yc * (xc * e001 + x * e101) + y * (xc * e011 + x * e111));
+			}
+		} else {
+			// puInterpND1Inner: result accumulated corner by corner in the
+			// recursion order (outer dims first), (c_x*f)*val
+#pragma unroll
+			for (int v = 0; v < ND; v++) dv[v] = 0;
+#pragma unroll
+			for (int c = 0; c < (1 << (ND - 1)); c++) {
+				double f = 1.0;
+				long off = 0;
+#pragma unroll
+				for (int d = ND - 1; d >= 1; d--) {
+					int b = (c >> (d - 1)) & 1;
+					f = (b ? dec[d] : comp[d]) * f;
+					off += b ? o1[d] : o0[d];
+				}
+#pragma unroll
+				for (int v = 0; v < ND; v++) {
+					double ea = chain(E[off + o0[0] + v], pre, sqm, smq, s);
+					double eb = chain(E[off + o1[0] + v], pre, sqm, smq, s);
+					dv[v] += comp[0] * f * ea;
+					dv[v] += dec[0] * f * eb;
+				}
+			}
+		}
+		double vsq = 0;
+#pragma unroll
+		for (int d = 0; d < ND; d++) {
+			double v = vs[d][i];
+			vsq += v * (v + dv[d]);
+			vs[d][i] = v + dv[d];
+		}
+		ke += vsq;
+	}
+	if (KE) {
+		double t = block_sum(ke, red);
+		if (threadIdx.x == 0) kePartial[blockIdx.x] = t;
+	}
+}
+
+// ------------------------------------------------------------- init -------
+__device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
+	z += 0x9E3779B97F4A7C15ULL;
+	z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+	z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+	return z ^ (z >> 31);
+}
+__device__ __forceinline__ double uni(unsigned long long seed, unsigned long long c) {
+	unsigned long long x = mix64(seed ^ mix64(c));
+	return ((double)(x >> 11) + 0.5) * (1.0 / 9007199254740992.0);
+}
+__device__ __forceinline__ double normal(unsigned long long seed, unsigned long long c) {
+	double u1 = uni(seed, 2 * c), u2 = uni(seed, 2 * c + 1);
+	return sqrt(-2.0 * log(u1)) * cos(2.0 * M_PI * u2);
+}
+
+struct LatticeArgs {
+	int nd;
+	int L[3];
+	int sub[3];
+	int off[3];
+	double posToSub[3];
+	double l;
+	double amp[3], mode[3];
+	int perturb, maxwell;
+	double drift, vth;
+	unsigned long long seed;
+	int species;
+};
+
+__device__ __forceinline__ bool lattice_pos(const LatticeArgs &a, long i, double *x) {
+	double lin = a.l * (double)i;
+	for (int d = 0; d < a.nd; d++) {
+		x[d] = fmod(lin, (double)a.L[d]);
+		lin /= a.L[d];
+	}
+	int ok = 0;
+	for (int d = 0; d < a.nd; d++) ok += (a.sub[d] == (int)(a.posToSub[d] * x[d]));
+	return ok == a.nd;
+}
+
+__global__ __launch_bounds__(kThreads) void k_lattice_count(LatticeArgs a, long nGlobal,
+                                                            int *__restrict__ chunkCount) {
+	__shared__ int wcnt[kThreads / 64];
+	long base = (long)blockIdx.x * PINC_CHUNK;
+	int cnt = 0;
+	for (int k = 0; k < kItems; k++) {
+		long i = base + k * kThreads + threadIdx.x;
+		double x[3];
+		if (i < nGlobal && lattice_pos(a, i, x)) cnt++;
+	}
+	int ws = wave_sum(cnt);
+	if ((threadIdx.x & 63) == 0) wcnt[threadIdx.x >> 6] = ws;
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		int t = 0;
+		for (int q = 0; q < kThreads / 64; q++) t += wcnt[q];
+		chunkCount[blockIdx.x] = t;
+	}
+}
+
+__global__ __launch_bounds__(kThreads) void k_lattice_write(LatticeArgs a, long nGlobal,
+                                                            const int *__restrict__ chunkOffset,
+                                                            pinc_pop_t pop, long sbase) {
+	__shared__ int wtot[kThreads / 64];
+	long base = (long)blockIdx.x * PINC_CHUNK;
+	int running = chunkOffset[blockIdx.x];
+	int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+	for (int k = 0; k < kItems; k++) {
+		long i = base + k * kThreads + threadIdx.x;
+		double x[3] = {0, 0, 0};
+		bool keep = i < nGlobal && lattice_pos(a, i, x);
+		unsigned long long b = __ballot(keep);
+		int rw = __popcll(b & lanemask_lt());
+		if (lane == 0) wtot[w] = __popcll(b);
+		__syncthreads();
+		int before = 0, tot = 0;
+		for (int q = 0; q < kThreads / 64; q++) {
+			before += (q < w) ? wtot[q] : 0;
+			tot += wtot[q];
+		}
+		if (keep) {
+			long dst = sbase + running + before + rw;
+			for (int d = 0; d < a.nd; d++) {
+				double p = x[d];  // global frame
+				if (a.perturb) {
+					double theta = 2.0 * M_PI * a.mode[d] * p / a.L[d];
+					p += a.amp[d] * cos(theta);
+				}
+				pop.x[d][dst] = p - a.off[d];
+				double v = 0.0;
+				if (a.maxwell) {
+					unsigned long long c =
+						(((unsigned long long)a.species << 40) | (unsigned long long)i) * 3ULL + d;
+					v = a.drift + a.vth * normal(a.seed, c);
+				}
+				pop.v[d][dst] = v;
+			}
+		}
+		running += tot;
+		__syncthreads();
+	}
+}
+
+inline long ceil_div(long a, long b) { return (a + b - 1) / b; }
+
+}  // namespace
+
+// =========================================================== C ABI ========
+extern "C" int pinc_hip_move_classify(pinc_pop_t pop, int s, int doMove, const double *thr,
+                                      unsigned char *flags, int *chunkCount, double maxVel,
+                                      int *errFlag, void *stream) {
+	long n = pop.iStop[s] - pop.iStart[s];
+	if (n <= 0) return 0;
+	long b0 = pop.iStart[s];
+	Thr t;
+	int nd = pop.nd;
+	for (int d = 0; d < 3; d++) {
+		t.lo[d] = d < nd ? thr[d] : 0;
+		t.up[d] = d < nd ? thr[nd + d] : 0;
+		t.hi[d] = d < nd ? thr[2 * nd + d] : 0;
+	}
+	int center = 0;
+	for (int d = 0, p = 1; d < nd; d++, p *= 3) center += p;
+	dim3 grid((unsigned)ceil_div(n, PINC_CHUNK));
+	hipStream_t st = (hipStream_t)stream;
+#define LAUNCH_MC(ND)                                                                          \
+	hipLaunchKernelGGL(k_move_classify<ND>, grid, dim3(kThreads), 0, st, pop.x[0] + b0,        \
+	                   nd > 1 ? pop.x[1] + b0 : nullptr, nd > 2 ? pop.x[2] + b0 : nullptr,     \
+	                   pop.v[0] + b0, nd > 1 ? pop.v[1] + b0 : nullptr,                        \
+	                   nd > 2 ? pop.v[2] + b0 : nullptr, n, doMove, t, center, flags + b0,     \
+	                   chunkCount, maxVel, errFlag)
+	if (nd == 3) LAUNCH_MC(3);
+	else if (nd == 2) LAUNCH_MC(2);
+	else LAUNCH_MC(1);
+#undef LAUNCH_MC
+	return check_launch("move_classify");
+}
+
+extern "C" int pinc_hip_extract(pinc_pop_t pop, int s, const unsigned char *flags, int *chunkCount,
+                                int center, int nNeighbors, pinc_extract_ws_t ws, long *nEmig,
+                                long *neCount, void *stream) {
+	(void)nNeighbors;
+	hipStream_t st = (hipStream_t)stream;
+	long n = pop.iStop[s] - pop.iStart[s];
+	long sb = pop.iStart[s];
+	*nEmig = 0;
+	for (int q = 0; q < kMaxNe; q++) neCount[q] = 0;
+	if (n <= 0) return 0;
+	int nChunks = (int)ceil_div(n, PINC_CHUNK);
+	hipLaunchKernelGGL(k_scan_single, dim3(1), dim3(1024), 0, st, chunkCount, ws.chunkOffset,
+	                   nChunks);
+	int E = 0;
+	hipError_t e = hipMemcpyAsync(&E, ws.chunkOffset + nChunks, sizeof(int), hipMemcpyDeviceToHost, st);
+	if (e != hipSuccess) return set_error(e, "extract: count readback");
+	e = hipStreamSynchronize(st);
+	if (e != hipSuccess) return set_error(e, "extract: sync");
+	*nEmig = E;
+	if (E == 0) return check_launch("extract(scan)");
+	if (E > ws.cap) return PINC_ERR_CAPACITY;
+	hipLaunchKernelGGL(k_extract_a, dim3(nChunks), dim3(kThreads), 0, st, flags + sb, n, center,
+	                   ws.chunkOffset, nChunks, ws.tail, ws.holes, ws.order, ws.scratch);
+	hipLaunchKernelGGL(k_extract_b, dim3((unsigned)ceil_div(E + 1, 256)), dim3(256), 0, st,
+	                   flags + sb, n, (long)E, center, ws.tail, ws.holes, ws.order, ws.scratch);
+	int nb = (int)ceil_div(E, kRankChunk);
+	hipLaunchKernelGGL(k_rank_hist, dim3(nb), dim3(kThreads), 0, st, flags + sb, ws.order, (long)E,
+	                   ws.blockHist);
+	hipLaunchKernelGGL(k_hist_scan, dim3(1), dim3(kMaxNe * 32), 0, st, ws.blockHist, nb,
+	                   ws.scratch);
+	hipLaunchKernelGGL(k_rank_scatter, dim3(nb), dim3(kThreads), 0, st, flags + sb, ws.order,
+	                   (long)E, ws.blockHist, ws.scratch, pop, sb, ws.buf, ws.cap, ws.bufNe);
+	hipLaunchKernelGGL(k_fill_holes, dim3((unsigned)ceil_div(E, 256)), dim3(256), 0, st, pop, sb,
+	                   ws.tail, ws.holes, ws.scratch);
+	int cnt[kMaxNe];
+	e = hipMemcpyAsync(cnt, ws.scratch + 64, sizeof(cnt), hipMemcpyDeviceToHost, st);
+	if (e != hipSuccess) return set_error(e, "extract: direction counts");
+	e = hipStreamSynchronize(st);
+	if (e != hipSuccess) return set_error(e, "extract: sync 2");
+	for (int q = 0; q < kMaxNe; q++) neCount[q] = cnt[q];
+	return check_launch("extract");
+}
+
+extern "C" int pinc_hip_import(pinc_pop_t pop, int s, long dst, const double *buf, long cap,
+                               const unsigned char *bufNe, long first, long n, const int *shiftT,
+                               int shiftMask, void *stream) {
+	if (n <= 0) return 0;
+	hipLaunchKernelGGL(k_import, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0,
+	                   (hipStream_t)stream, pop, pop.iStart[s] + dst, buf, cap, bufNe, first, n,
+	                   shiftT[0], shiftT[1], shiftT[2], shiftMask);
+	return check_launch("import");
+}
+
+extern "C" int pinc_hip_pack(const double *buf, long cap, const unsigned char *bufNe, long first, long n,
+                             int nd, double *out, void *stream) {
+	if (n <= 0) return 0;
+	hipLaunchKernelGGL(k_pack, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, (hipStream_t)stream, buf, cap,
+	                   bufNe, first, n, nd, out);
+	return check_launch("pack");
+}
+
+extern "C" int pinc_hip_import_rec(pinc_pop_t pop, int s, long dst, const double *rec, long n,
+                                   const int *shiftT, void *stream) {
+	if (n <= 0) return 0;
+	hipLaunchKernelGGL(k_import_rec, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, (hipStream_t)stream, pop,
+	                   pop.iStart[s] + dst, rec, n, shiftT[0], shiftT[1], shiftT[2]);
+	return check_launch("import_rec");
+}
+
+extern "C" int pinc_hip_deposit(pinc_pop_t pop, int s, pinc_geom_t g, double *rho, void *stream) {
+	long n = pop.iStop[s] - pop.iStart[s];
+	if (n <= 0) return 0;
+	long b0 = pop.iStart[s];
+	long nb = ceil_div(n, kThreads * 4);
+	if (nb > 65536L * 4) nb = 65536L * 4;
+	hipStream_t st = (hipStream_t)stream;
+	const double *x0 = pop.x[0] + b0;
+	const double *x1 = g.nd > 1 ? pop.x[1] + b0 : nullptr;
+	const double *x2 = g.nd > 2 ? pop.x[2] + b0 : nullptr;
+	if (g.nd == 3)
+		hipLaunchKernelGGL((k_deposit<3, true>), dim3(nb), dim3(kThreads), 0, st, x0, x1, x2, n, g, rho);
+	else if (g.nd == 2)
+		hipLaunchKernelGGL((k_deposit<2, false>), dim3(nb), dim3(kThreads), 0, st, x0, x1, x2, n, g, rho);
+	else
+		hipLaunchKernelGGL((k_deposit<1, false>), dim3(nb), dim3(kThreads), 0, st, x0, x1, x2, n, g, rho);
+	return check_launch("deposit");
+}
+
+extern "C" int pinc_hip_accelerate(pinc_pop_t pop, int s, pinc_geom_t g, const double *E,
+                                   const double *qm, const double *mq, double pre,
+                                   double *kePartial, int *nBlocks, void *stream) {
+	long n = pop.iStop[s] - pop.iStart[s];
+	*nBlocks = 0;
+	if (n <= 0) return 0;
+	long b0 = pop.iStart[s];
+	long nb = ceil_div(n, kAccChunk);
+	*nBlocks = (int)nb;
+	hipStream_t st = (hipStream_t)stream;
+	const double *x0 = pop.x[0] + b0;
+	const double *x1 = g.nd > 1 ? pop.x[1] + b0 : nullptr;
+	const double *x2 = g.nd > 2 ? pop.x[2] + b0 : nullptr;
+	double *v0 = pop.v[0] + b0;
+	double *v1 = g.nd > 1 ? pop.v[1] + b0 : nullptr;
+	double *v2 = g.nd > 2 ? pop.v[2] + b0 : nullptr;
+	if (g.nd == 3)
+		hipLaunchKernelGGL((k_accel<3, true, true>), dim3(nb), dim3(kThreads), 0, st, x0, x1, x2, v0,
+		                   v1, v2, n, g, E, s, qm, mq, pre, kePartial);
+	else if (g.nd == 2)
+		hipLaunchKernelGGL((k_accel<2, false, true>), dim3(nb), dim3(kThreads), 0, st, x0, x1, x2,
+		                   v0, v1, v2, n, g, E, s, qm, mq, pre, kePartial);
+	else
+		hipLaunchKernelGGL((k_accel<1, false, true>), dim3(nb), dim3(kThreads), 0, st, x0, x1, x2,
+		                   v0, v1, v2, n, g, E, s, qm, mq, pre, kePartial);
+	return check_launch("accelerate");
+}
+
+extern "C" int pinc_hip_init_species(pinc_pop_t pop, int s, pinc_geom_t g, long nGlobal,
+                                     double latticeStep, const int *subdomain,
+                                     const int *nSubdomains, const int *offset, const double *amp,
+                                     const double *mode, int perturb, int maxwell, double drift,
+                                     double vth, unsigned long long seed, long *nOut,
+                                     void *stream) {
+	hipStream_t st = (hipStream_t)stream;
+	LatticeArgs a;
+	a.nd = g.nd;
+	for (int d = 0; d < 3; d++) {
+		a.L[d] = d < g.nd ? g.T[d] : 1;
+		a.sub[d] = d < g.nd ? subdomain[d] : 0;
+		a.off[d] = d < g.nd ? offset[d] : 0;
+		int tsd = d < g.nd ? (g.T[d] / nSubdomains[d]) : 1;
+		a.posToSub[d] = (double)1 / tsd;
+		a.amp[d] = d < g.nd ? amp[d] : 0;
+		a.mode[d] = d < g.nd ? mode[d] : 0;
+	}
+	a.l = latticeStep;
+	a.perturb = perturb;
+	a.maxwell = maxwell;
+	a.drift = drift;
+	a.vth = vth;
+	a.seed = seed;
+	a.species = s;
+	long nChunks = ceil_div(nGlobal, PINC_CHUNK);
+	int *cnt = nullptr, *off = nullptr;
+	hipError_t e = hipMallocAsync((void **)&cnt, (nChunks + 1) * sizeof(int), st);
+	if (e != hipSuccess) return set_error(e, "init: alloc");
+	e = hipMallocAsync((void **)&off, (nChunks + 1) * sizeof(int), st);
+	if (e != hipSuccess) return set_error(e, "init: alloc");
+	hipLaunchKernelGGL(k_lattice_count, dim3((unsigned)nChunks), dim3(kThreads), 0, st, a, nGlobal, cnt);
+	hipLaunchKernelGGL(k_scan_single, dim3(1), dim3(1024), 0, st, cnt, off, (int)nChunks);
+	int total = 0;
+	e = hipMemcpyAsync(&total, off + nChunks, sizeof(int), hipMemcpyDeviceToHost, st);
+	if (e == hipSuccess) e = hipStreamSynchronize(st);
+	if (e != hipSuccess) return set_error(e, "init: count readback");
+	long capS = pop.iStart[s + 1] - pop.iStart[s];
+	if (total > capS) {
+		(void)hipFreeAsync(cnt, st);
+		(void)hipFreeAsync(off, st);
+		return set_error(hipErrorOutOfMemory, "init: species capacity too small");
+	}
+	hipLaunchKernelGGL(k_lattice_write, dim3((unsigned)nChunks), dim3(kThreads), 0, st, a, nGlobal,
+	                   off, pop, pop.iStart[s]);
+	(void)hipFreeAsync(cnt, st);
+	(void)hipFreeAsync(off, st);
+	*nOut = total;
+	return check_launch("init_species");
+}

@@ -1,0 +1,93 @@
+/*
+ * pinc_internal.h -- private state behind include/pinc.h (host side, C).
+ */
+#ifndef PINC_INTERNAL_H
+#define PINC_INTERNAL_H
+
+/* system headers first: pinc.h defines the reference's select() macro */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/select.h>
+#include "pinc.h"
+
+#define PINC_NNE 27
+
+/* one process drives one GPU: stream, communicator and scratch are global,
+ * as the reference relies on MPI_COMM_WORLD */
+typedef struct {
+	int initialised;
+	int device;
+	void *stream;
+	void *comm;
+	int rank, nranks;
+	double *dScratch;   /* device: 8192 partials + 256 scalar slots */
+	int *dErr;          /* device error word (asserts) */
+	double maxVel;
+	double thr[9];      /* migration thresholds lo[nd], up[nd], assert bound[nd] */
+	int thrSet;
+	int timing;
+	void *ev[2*PINC_NPHASES];
+	double phaseMs[PINC_NPHASES];
+	int phaseOpen[PINC_NPHASES];
+} PincCtx;
+
+extern PincCtx g_pinc;
+
+#define PINC_PARTIALS 8192
+#define PINC_SLOT(i) (g_pinc.dScratch + PINC_PARTIALS + (i))
+
+struct PincDevPop {
+	pinc_pop_t p;                 /* device pointers; ranges mirrored per call */
+	long cap;                     /* total capacity */
+	unsigned char *flags;
+	int *chunkCount;              /* per species at chunkBase[s] */
+	long chunkBase[PINC_MAX_SPECIES + 1];
+	int flagsValid;
+	pinc_extract_ws_t ws[PINC_MAX_SPECIES];
+	long nEmig[PINC_MAX_SPECIES];
+	long neCount[PINC_MAX_SPECIES][PINC_NNE];
+	double *qm, *mq;              /* device q/m and m/q per species */
+	double *kePartial;
+	pinc_geom_t geom;
+	/* multi-rank migration buffers (AoS records: nd pos, nd vel, ne) */
+	double *sendBuf[2], *recvBuf[2];
+	long sendCap, recvCap;
+};
+
+struct PincDevGrid {
+	int nValues;
+	double *d;          /* slab storage [nloc+2] planes (nValues per node) */
+	long n;             /* elements of d */
+	long planeSize;     /* nodes per plane */
+	pinc_geom_t geom;
+	double *global;     /* global periodic view (rho, phi) */
+	int ownsGlobal;
+	int ghostsValid;    /* slab ghost planes already hold periodic images */
+	double *recv[2];    /* halo receive planes (multi-rank) */
+};
+
+struct MultigridSolver {
+	int nLevels, nPre, nPost, nCoarse, mgCycles;
+	int pre3d, post3d, coarse3d, restr3d;
+	pinc_lvl_t L[PINC_MAX_LEVELS];
+	long N[PINC_MAX_LEVELS];
+	double *rho[PINC_MAX_LEVELS], *phi[PINC_MAX_LEVELS], *res[PINC_MAX_LEVELS];
+	long cycles;
+	Grid *rhoGrid, *phiGrid;
+	int native;
+};
+
+/* helpers shared by the host translation units */
+void pinc_ctx_require(void);
+void pinc_check(int rc, const char *where);
+void pinc_phase_begin(int phase);
+void pinc_phase_end(int phase);
+pinc_geom_t pinc_geom_from_grid(const Grid *g, const MpiInfo *mpi);
+pinc_geom_t pinc_geom_current(void);
+void pinc_geom_set(pinc_geom_t g);
+pinc_pop_t pinc_devpop(const Population *pop);
+double pinc_reduce_host(int nParts, double div);
+int pinc_ipow3(int d);
+
+#endif

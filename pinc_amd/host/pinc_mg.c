@@ -1,0 +1,211 @@
+/*
+ * pinc_mg.c -- multigrid Poisson solver of the MI355X PINC hot path (host C).
+ *
+ * Parity mode (default) runs the reference algorithm of src/multigrid.c:
+ *   mgAllocSolver      multigrid.c:364-384, levels T/2^q (mgAllocSubGrids 128-214)
+ *   mgSolve/mgSolveRaw multigrid.c:403-407, 1688-1724: V-cycles until the RMS
+ *                      residual over true nodes is <= 1e-10 (at least one)
+ *   vrec               mgVRecursiveInner 1496-1556: neutralise rho, presmooth,
+ *                      residual, restrict, recurse, add the prolongated
+ *                      correction, neutralise, postsmooth, neutralise
+ *   smoothers          mgGS3D / mgGSND red-black Gauss-Seidel with a
+ *                      neutralisation after every colour (gBnd -> grid.c:730)
+ * Coarse-level potentials persist between cycles and steps (warm start) as in
+ * the reference.  The solve runs on the whole periodic domain on every rank:
+ * with several ranks the slabs of rho are all-gathered first (RCCL) and every
+ * rank computes the same potential, replacing the reference's per-colour
+ * halo exchanges (DESIGN.md "Multi-GPU").
+ */
+#define _GNU_SOURCE
+#include "pinc_internal.h"
+#include <math.h>
+
+#define MU_SLOT 32   /* two alternating mean slots of the smoother */
+#define TMP_SLOT 40
+
+void mgSolver(void (**solve)(), void *(**solverAlloc)(), void (**solverFree)()) {
+	*solve = (void (*)())mgSolve;
+	*solverAlloc = (void *(*)())mgAllocSolver;
+	*solverFree = (void (*)())mgFreeSolver;
+}
+
+funPtr mgSolver_set(dictionary *ini) {
+	(void)ini;
+	return (funPtr)mgSolver;
+}
+
+static int smootherIs3D(const dictionary *ini, const char *key, int nd) {
+	char *v = iniGetStr(ini, key);
+	int r = -1;
+	if (!strcmp(v, "gaussSeidelRB")) {
+		if (nd != 3) msg(ERROR, "%s=gaussSeidelRB is 2-D/3-D specific; the device path implements 3-D (use gaussSeidelRBND)", key);
+		r = 1;
+	} else if (!strcmp(v, "gaussSeidelRBND")) r = 0;
+	else msg(ERROR, "%s=%s is not on the MI355X hot path", key, v);
+	free(v);
+	return r;
+}
+
+MultigridSolver *mgAllocSolver(const dictionary *ini, Grid *rho, Grid *phi) {
+	MultigridSolver *S = calloc(1, sizeof(*S));
+	int nd = rho->rank - 1;
+	char *cycle = iniGetStr(ini, "multigrid:cycle");
+	if (strcmp(cycle, "mgVRecursive")) msg(ERROR, "multigrid:cycle=%s: only mgVRecursive is on the hot path", cycle);
+	free(cycle);
+	S->nLevels = iniGetInt(ini, "multigrid:mgLevels");
+	S->mgCycles = iniGetInt(ini, "multigrid:mgCycles");
+	S->nPre = iniGetInt(ini, "multigrid:nPreSmooth");
+	S->nPost = iniGetInt(ini, "multigrid:nPostSmooth");
+	S->nCoarse = iniGetInt(ini, "multigrid:nCoarseSolve");
+	if (S->nLevels < 1) msg(ERROR, "Multi Grid levels is 0, need 1 grid level");
+	if (S->nLevels > PINC_MAX_LEVELS) msg(ERROR, "multigrid:mgLevels > %d", PINC_MAX_LEVELS);
+	if (!S->mgCycles) msg(ERROR, "MG cycles is 0");
+	S->pre3d = smootherIs3D(ini, "multigrid:preSmooth", nd);
+	S->post3d = smootherIs3D(ini, "multigrid:postSmooth", nd);
+	S->coarse3d = smootherIs3D(ini, "multigrid:coarseSolver", nd);
+	char *re = iniGetStr(ini, "multigrid:restrictor");
+	char *pr = iniGetStr(ini, "multigrid:prolongator");
+	if (!strcmp(re, "halfWeight")) {
+		if (nd != 3) msg(ERROR, "halfWeight is implemented for 3-D on the device path (use halfWeightND)");
+		S->restr3d = 1;
+	} else if (!strcmp(re, "halfWeightND")) S->restr3d = 0;
+	else msg(ERROR, "multigrid:restrictor=%s not supported", re);
+	if (strcmp(pr, "bilinear") && strcmp(pr, "bilinearND")) msg(ERROR, "multigrid:prolongator=%s not supported", pr);
+	if (!strcmp(pr, "bilinear") && nd != 3) msg(ERROR, "bilinear is implemented for 3-D on the device path (use bilinearND)");
+	free(re);
+	free(pr);
+	S->native = iniHas(ini, "multigrid:native") ? iniGetInt(ini, "multigrid:native") : 0;
+	for (int d = 1; d <= nd; d++)
+		if (rho->trueSize[d] % (1 << S->nLevels))
+			msg(ERROR, "All elements in grid:trueSize must be a multiple of 2^mgLevels=%d", 1 << S->nLevels);
+	pinc_geom_t g = rho->dev->geom;
+	for (int q = 0; q < S->nLevels; q++) {
+		S->L[q].nd = nd;
+		S->N[q] = 1;
+		for (int d = 0; d < 3; d++) {
+			S->L[q].T[d] = d < nd ? g.T[d] >> q : 1;
+			S->N[q] *= S->L[q].T[d];
+		}
+	}
+	long ps = rho->dev->planeSize;
+	if (g_pinc.nranks == 1) {
+		rho->dev->global = rho->dev->d + ps;
+		phi->dev->global = phi->dev->d + ps;
+	} else {
+		pinc_check(pinc_hip_malloc((void **)&rho->dev->global, S->N[0] * sizeof(double)), "global rho");
+		pinc_check(pinc_hip_malloc((void **)&phi->dev->global, S->N[0] * sizeof(double)), "global phi");
+		pinc_check(pinc_hip_memset(phi->dev->global, 0, S->N[0] * sizeof(double), g_pinc.stream), "global phi");
+		rho->dev->ownsGlobal = phi->dev->ownsGlobal = 1;
+	}
+	S->rho[0] = rho->dev->global;
+	S->phi[0] = phi->dev->global;
+	for (int q = 0; q < S->nLevels; q++) {
+		if (q > 0) {
+			pinc_check(pinc_hip_malloc((void **)&S->rho[q], S->N[q] * sizeof(double)), "mg level");
+			pinc_check(pinc_hip_malloc((void **)&S->phi[q], S->N[q] * sizeof(double)), "mg level");
+			pinc_check(pinc_hip_memset(S->rho[q], 0, S->N[q] * sizeof(double), g_pinc.stream), "mg level");
+			pinc_check(pinc_hip_memset(S->phi[q], 0, S->N[q] * sizeof(double), g_pinc.stream), "mg level");
+		}
+		pinc_check(pinc_hip_malloc((void **)&S->res[q], S->N[q] * sizeof(double)), "mg level");
+	}
+	S->rhoGrid = rho;
+	S->phiGrid = phi;
+	return S;
+}
+
+void mgFreeSolver(MultigridSolver *S) {
+	if (!S) return;
+	for (int q = 0; q < S->nLevels; q++) {
+		if (q > 0) {
+			pinc_hip_free(S->rho[q]);
+			pinc_hip_free(S->phi[q]);
+		}
+		pinc_hip_free(S->res[q]);
+	}
+	free(S);
+}
+
+long mgCycleCount(const MultigridSolver *S) { return S->cycles; }
+
+/* gNeutralizeGrid on a level of the global grid */
+static void neutralize(double *a, long N) {
+	pinc_check(pinc_hip_sum_div(a, N, (double)N, g_pinc.dScratch, PINC_SLOT(TMP_SLOT), g_pinc.stream), "mean");
+	pinc_check(pinc_hip_sub_dev(a, N, PINC_SLOT(TMP_SLOT), g_pinc.stream), "neutralize");
+}
+
+/* nIter red-black iterations, each colour followed by a neutralisation:
+ * the mean of pass k is formed from that pass's partial sums and applied
+ * lazily by pass k+1 (k_mg.hip), then materialised once at the end. */
+static void smooth(MultigridSolver *S, int q, int nIter, int nd3) {
+	if (nIter <= 0) return;
+	int nPass = 2 * nIter;
+	for (int k = 0; k < nPass; k++) {
+		const double *muPrev = k ? PINC_SLOT(MU_SLOT + ((k - 1) & 1)) : NULL;
+		int nb = 0;
+		pinc_check(pinc_hip_gs_pass(S->phi[q], S->rho[q], S->L[q], k & 1, nd3, muPrev, g_pinc.dScratch, &nb,
+		                            g_pinc.stream),
+		           "gs pass");
+		pinc_check(pinc_hip_reduce(g_pinc.dScratch, nb, (double)S->N[q], PINC_SLOT(MU_SLOT + (k & 1)), g_pinc.stream),
+		           "gs mean");
+	}
+	pinc_check(pinc_hip_gs_materialize(S->phi[q], S->L[q], 1, PINC_SLOT(MU_SLOT), PINC_SLOT(MU_SLOT + 1),
+	                                   g_pinc.stream),
+	           "gs materialize");
+}
+
+static void vrec(MultigridSolver *S, int q) {
+	int bottom = S->nLevels - 1;
+	if (q == bottom) {
+		neutralize(S->rho[q], S->N[q]);
+		smooth(S, q, S->nCoarse, S->coarse3d);
+		neutralize(S->phi[q], S->N[q]);
+		pinc_check(pinc_hip_prolong_add(S->phi[q - 1], S->phi[q], S->L[q - 1], g_pinc.stream), "prolong");
+		return;
+	}
+	neutralize(S->rho[q], S->N[q]);
+	smooth(S, q, S->nPre, S->pre3d);
+	pinc_check(pinc_hip_residual(S->res[q], S->phi[q], S->rho[q], S->L[q], g_pinc.stream), "residual");
+	pinc_check(pinc_hip_restrict(S->res[q], S->rho[q + 1], S->L[q + 1], S->restr3d, g_pinc.stream), "restrict");
+	if (S->native) pinc_check(pinc_hip_scale(S->rho[q + 1], S->N[q + 1], 4.0, g_pinc.stream), "native scale");
+	vrec(S, q + 1);
+	neutralize(S->phi[q], S->N[q]);
+	smooth(S, q, S->nPost, S->post3d);
+	neutralize(S->phi[q], S->N[q]);
+	if (q > 0) pinc_check(pinc_hip_prolong_add(S->phi[q - 1], S->phi[q], S->L[q - 1], g_pinc.stream), "prolong");
+}
+
+void mgSolve(MultigridSolver *S, Grid *rho, Grid *phi, const MpiInfo *mpiInfo) {
+	(void)mpiInfo;
+	(void)phi;
+	pinc_phase_begin(4);
+	if (g_pinc.nranks > 1) {
+		long ps = rho->dev->planeSize;
+		pinc_check(pinc_hip_comm_allgather(g_pinc.comm, rho->dev->d + ps, rho->dev->global, ps * rho->dev->geom.nloc,
+		                                   g_pinc.stream),
+		           "gather rho");
+	}
+	if (S->nLevels > 1) {
+		const long maxCycles = 1000000; /* the reference loops forever (multigrid.c:1698) */
+		double barRes = 2.;
+		long c = 0;
+		while (barRes > 1.E-10) {
+			vrec(S, 0);
+			S->cycles++;
+			int nb = 0;
+			pinc_check(pinc_hip_residual_sumsq(S->phi[0], S->rho[0], S->L[0], g_pinc.dScratch, &nb, g_pinc.stream),
+			           "residual norm");
+			pinc_check(pinc_hip_reduce(g_pinc.dScratch, nb, 1.0, PINC_SLOT(TMP_SLOT + 1), g_pinc.stream), "norm");
+			double sum = 0;
+			pinc_check(pinc_hip_d2h(&sum, PINC_SLOT(TMP_SLOT + 1), sizeof(double), g_pinc.stream), "norm");
+			barRes = sqrt(sum / S->N[0]);
+			if (++c > maxCycles || isnan(barRes)) msg(ERROR, "multigrid did not converge (residual %g)", barRes);
+		}
+	} else {
+		for (int c = 0; c < S->mgCycles; c++) {
+			neutralize(S->rho[0], S->N[0]);
+			smooth(S, 0, S->nCoarse, S->coarse3d);
+		}
+	}
+	phi->dev->ghostsValid = 0;
+	pinc_phase_end(4);
+}

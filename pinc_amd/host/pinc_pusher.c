@@ -1,0 +1,316 @@
+/*
+ * pinc_pusher.c -- particle operators of the MI355X PINC hot path (host C).
+ * Same names, signatures and _set selectors as src/pusher.c; each launches
+ * the gfx950 kernels of libpinc_hip on the device twin.
+ *
+ *   puMove                 pusher.c:86-119 (+ fused neighbour classification)
+ *   puAcc3D1(KE)/ND1(KE)   pusher.c:147-308
+ *   puDistr3D1/ND1         pusher.c:512-638
+ *   puExtractEmigrants*    pusher.c:782-910
+ *   puMigrate              pusher.c:914-1035: one rank imports its own
+ *                          emigrants (all neighbours are itself); with a slab
+ *                          decomposition the z+-1 payloads travel over RCCL
+ *   puNeighborToRank etc.  pusher.c:1181-1232
+ *   _set sanity checks     pusher.c:1047-1087
+ */
+#define _GNU_SOURCE
+#include "pinc_internal.h"
+#include <math.h>
+
+void pinc_pop_grow_ws(Population *pop, int s, long n);
+
+/* ------------------------------------------------------------- sanity -- */
+static void puSanity(dictionary *ini, const char *name, int dim, int order) {
+	int nd = iniGetInt(ini, "grid:nDims");
+	int *ng = iniGetIntArr(ini, "grid:nGhostLayers", 2 * nd);
+	double *th = iniGetDoubleArr(ini, "grid:thresholds", 2 * nd);
+	int minL = ng[0];
+	double mn = th[0], mx = th[0];
+	for (int i = 1; i < 2 * nd; i++) {
+		if (ng[i] < minL) minL = ng[i];
+		if (th[i] < mn) mn = th[i];
+		if (th[i] > mx) mx = th[i];
+	}
+	if (nd != dim && dim != 0) msg(ERROR, "%s only supports grid:nDims=%d", name, dim);
+	if (minL < 1) msg(ERROR, "%s requires grid:nGhostLayers >=%d", name, order ? 1 : 0);
+	double reqMin = order == 0 ? -0.5 : (order == 1 ? 0 : 0.5);
+	if (mn < reqMin) msg(ERROR, "%s requires grid:thresholds >=%.1f", name, reqMin);
+	if (mx > minL - 0.5) msg(ERROR, "%s requires grid:thresholds <= grid:nGhostLayers - 0.5", name);
+	free(ng);
+	free(th);
+}
+
+funPtr puAcc3D1_set(dictionary *ini) { puSanity(ini, "puAcc3D1", 3, 1); return (funPtr)puAcc3D1; }
+funPtr puAcc3D1KE_set(dictionary *ini) { puSanity(ini, "puAcc3D1KE", 3, 1); return (funPtr)puAcc3D1KE; }
+funPtr puAccND1_set(dictionary *ini) { puSanity(ini, "puAccND1", 0, 1); return (funPtr)puAccND1; }
+funPtr puAccND1KE_set(dictionary *ini) { puSanity(ini, "puAccND1KE", 0, 1); return (funPtr)puAccND1KE; }
+funPtr puDistr3D1_set(dictionary *ini) { puSanity(ini, "puDistr3D1", 3, 1); return (funPtr)puDistr3D1; }
+funPtr puDistrND1_set(dictionary *ini) { puSanity(ini, "puDistrND1", 0, 1); return (funPtr)puDistrND1; }
+funPtr puExtractEmigrants3D_set(dictionary *ini) {
+	if (iniGetInt(ini, "grid:nDims") != 3) msg(ERROR, "puExtractEmigrants3D requires grid:nDims=3");
+	return (funPtr)puExtractEmigrants3D;
+}
+funPtr puExtractEmigrantsND_set(dictionary *ini) {
+	(void)ini;
+	return (funPtr)puExtractEmigrantsND;
+}
+
+/* ----------------------------------------------------------- neighbours -- */
+int puNeighborToReciprocal(int neighbor, int nDims) {
+	int r = 0;
+	for (int d = 0; d < nDims; d++) {
+		r += (2 - (neighbor % 3)) * pinc_ipow3(d);
+		neighbor /= 3;
+	}
+	return r;
+}
+
+int puNeighborToRank(MpiInfo *m, int neighbor) {
+	int rank = 0;
+	for (int d = 0; d < m->nDims; d++) {
+		int n = (neighbor % 3) - 1;
+		neighbor /= 3;
+		n = (m->subdomain[d] + n + m->nSubdomains[d]) % m->nSubdomains[d];
+		rank += n * m->nSubdomainsProd[d];
+	}
+	return rank;
+}
+
+int puRankToNeighbor(MpiInfo *m, int rank) {
+	int neighbor = 0;
+	for (int d = 0; d < m->nDims; d++) {
+		int n = rank % m->nSubdomains[d];
+		n = (n - m->subdomain[d] + 1 + m->nSubdomains[d]) % m->nSubdomains[d];
+		rank /= m->nSubdomains[d];
+		neighbor += n * pinc_ipow3(d);
+	}
+	return neighbor;
+}
+
+/* ---------------------------------------------------------------- move -- */
+static void classify(Population *pop, int doMove) {
+	if (!g_pinc.thrSet) msg(ERROR, "gCreateNeighborhood must run before puMove/extract");
+	PincDevPop *dv = pop->dev;
+	pinc_pop_t p = pinc_devpop(pop);
+	for (int s = 0; s < pop->nSpecies; s++)
+		pinc_check(pinc_hip_move_classify(p, s, doMove, g_pinc.thr, dv->flags, dv->chunkCount + dv->chunkBase[s],
+		                                  g_pinc.maxVel, g_pinc.dErr, g_pinc.stream),
+		           "move/classify");
+	dv->flagsValid = 1;
+}
+
+void puMove(Population *pop, Object *obj) {
+	(void)obj; /* particle-object collisions are out of scope (fact 6) */
+	pinc_phase_begin(0);
+	classify(pop, 1);
+	pinc_phase_end(0);
+}
+
+/* ------------------------------------------------------------- extract -- */
+static void extract(Population *pop, MpiInfo *m) {
+	PincDevPop *dv = pop->dev;
+	if (!dv->flagsValid) classify(pop, 0);
+	pinc_phase_begin(1);
+	int ns = pop->nSpecies, nN = m->nNeighbors;
+	memset(m->nEmigrants, 0, nN * ns * sizeof(long));
+	for (int s = 0; s < ns; s++) {
+		for (int attempt = 0;; attempt++) {
+			pinc_pop_t p = pinc_devpop(pop);
+			long nEmig = 0;
+			int rc = pinc_hip_extract(p, s, dv->flags, dv->chunkCount + dv->chunkBase[s], m->neighborhoodCenter, nN,
+			                          dv->ws[s], &nEmig, dv->neCount[s], g_pinc.stream);
+			if (rc == PINC_ERR_CAPACITY && attempt == 0) {
+				pinc_pop_grow_ws(pop, s, nEmig);
+				continue;
+			}
+			pinc_check(rc, "extract emigrants");
+			dv->nEmig[s] = nEmig;
+			break;
+		}
+		pop->iStop[s] -= dv->nEmig[s];
+		for (int ne = 0; ne < nN; ne++) m->nEmigrants[ne * ns + s] = dv->neCount[s][ne];
+	}
+	dv->flagsValid = 0;
+	pinc_phase_end(1);
+}
+
+void puExtractEmigrants3D(Population *pop, MpiInfo *m) { extract(pop, m); }
+void puExtractEmigrantsND(Population *pop, MpiInfo *m) { extract(pop, m); }
+
+/* ------------------------------------------------------------- migrate -- */
+/* (re)allocate a pair of record buffers to hold at least `need` records */
+static void ensure_pair(double **buf, long *cap, long need) {
+	if (need <= *cap && buf[0]) return;
+	pinc_check(pinc_hip_stream_sync(g_pinc.stream), "buf sync");
+	long c = need + need / 4 + 1024;
+	for (int k = 0; k < 2; k++) {
+		pinc_hip_free(buf[k]);
+		pinc_check(pinc_hip_malloc((void **)&buf[k], c * PINC_REC * sizeof(double)), "migrant buffer");
+	}
+	*cap = c;
+}
+
+void puMigrate(Population *pop, MpiInfo *m, Grid *grid) {
+	(void)grid;
+	pinc_phase_begin(2);
+	PincDevPop *dv = pop->dev;
+	int ns = pop->nSpecies, nd = pop->nDims;
+	pinc_geom_t g = dv->geom;
+	int T[3] = {1, 1, 1};
+	for (int d = 0; d < nd; d++) T[d] = d == nd - 1 ? g.nloc : g.T[d];
+	int P3 = pinc_ipow3(nd - 1);
+	memset(m->nImmigrants, 0, m->nNeighbors * ns * sizeof(long));
+	if (g_pinc.nranks == 1) {
+		/* every neighbour is this rank: messages arrive in the order they
+		 * were sent (by direction ne), each shifted by its receive tag */
+		for (int s = 0; s < ns; s++) {
+			long E = dv->nEmig[s];
+			pinc_pop_t p = pinc_devpop(pop);
+			pinc_check(pinc_hip_import(p, s, pop->iStop[s] - pop->iStart[s], dv->ws[s].buf, dv->ws[s].cap,
+			                           dv->ws[s].bufNe, 0, E, T, (1 << nd) - 1, g_pinc.stream),
+			           "import");
+			pop->iStop[s] += E;
+			for (int ne = 0; ne < m->nNeighbors; ne++)
+				m->nImmigrants[puNeighborToReciprocal(ne, nd) * ns + s] = dv->neCount[s][ne];
+		}
+		dv->flagsValid = 0;
+		pinc_phase_end(2);
+		return;
+	}
+	/* slab decomposition: directions whose slab digit is 0 go down, 2 go up,
+	 * 1 stay.  The buffer of each species is sorted by direction, so these
+	 * are three contiguous segments. */
+	long nDown[PINC_MAX_SPECIES], nLocal[PINC_MAX_SPECIES], nUp[PINC_MAX_SPECIES];
+	long totDown = 0, totUp = 0;
+	for (int s = 0; s < ns; s++) {
+		nDown[s] = nLocal[s] = nUp[s] = 0;
+		for (int ne = 0; ne < m->nNeighbors; ne++) {
+			int dig = ne / P3;
+			long c = dv->neCount[s][ne];
+			if (dig == 0) nDown[s] += c;
+			else if (dig == 1) nLocal[s] += c;
+			else nUp[s] += c;
+		}
+		totDown += nDown[s];
+		totUp += nUp[s];
+	}
+	/* exchange counts (exchangeNMigrants, pusher.c:914-938) */
+	int P = g_pinc.nranks, r = g_pinc.rank;
+	int up = (r + 1) % P, dn = (r - 1 + P) % P;
+	double cnt[4 * PINC_MAX_SPECIES];
+	for (int s = 0; s < ns; s++) {
+		cnt[s] = (double)nUp[s];
+		cnt[PINC_MAX_SPECIES + s] = (double)nDown[s];
+	}
+	double *dc = PINC_SLOT(64);
+	pinc_check(pinc_hip_h2d(dc, cnt, 2 * PINC_MAX_SPECIES * sizeof(double), g_pinc.stream), "counts");
+	{
+		int sp[2] = {up, dn}, rp[2] = {dn, up};
+		void *sb[2] = {dc, dc + PINC_MAX_SPECIES};
+		void *rb[2] = {dc + 2 * PINC_MAX_SPECIES, dc + 3 * PINC_MAX_SPECIES};
+		long nb[2] = {ns * sizeof(double), ns * sizeof(double)};
+		pinc_check(pinc_hip_comm_exchange(g_pinc.comm, 2, sp, sb, nb, rp, rb, nb, g_pinc.stream), "count exchange");
+	}
+	pinc_check(pinc_hip_d2h(cnt, dc, 4 * PINC_MAX_SPECIES * sizeof(double), g_pinc.stream), "counts");
+	long fromDown[PINC_MAX_SPECIES], fromUp[PINC_MAX_SPECIES], totFromDown = 0, totFromUp = 0;
+	for (int s = 0; s < ns; s++) {
+		fromDown[s] = (long)cnt[2 * PINC_MAX_SPECIES + s];
+		fromUp[s] = (long)cnt[3 * PINC_MAX_SPECIES + s];
+		totFromDown += fromDown[s];
+		totFromUp += fromUp[s];
+	}
+	/* pack payloads: records of all species back to back */
+	ensure_pair(dv->sendBuf, &dv->sendCap, totUp > totDown ? totUp : totDown);
+	ensure_pair(dv->recvBuf, &dv->recvCap, totFromUp > totFromDown ? totFromUp : totFromDown);
+	long oUp = 0, oDown = 0;
+	for (int s = 0; s < ns; s++) {
+		pinc_extract_ws_t *w = &dv->ws[s];
+		pinc_check(pinc_hip_pack(w->buf, w->cap, w->bufNe, nDown[s] + nLocal[s], nUp[s], nd,
+		                         dv->sendBuf[0] + oUp * PINC_REC, g_pinc.stream), "pack up");
+		pinc_check(pinc_hip_pack(w->buf, w->cap, w->bufNe, 0, nDown[s], nd, dv->sendBuf[1] + oDown * PINC_REC,
+		                         g_pinc.stream), "pack down");
+		oUp += nUp[s];
+		oDown += nDown[s];
+	}
+	{
+		int sp[2] = {up, dn}, rp[2] = {dn, up};
+		void *sb[2] = {dv->sendBuf[0], dv->sendBuf[1]};
+		void *rb[2] = {dv->recvBuf[0], dv->recvBuf[1]};
+		long snb[2] = {totUp * PINC_REC * (long)sizeof(double), totDown * PINC_REC * (long)sizeof(double)};
+		long rnb[2] = {totFromDown * PINC_REC * (long)sizeof(double), totFromUp * PINC_REC * (long)sizeof(double)};
+		pinc_check(pinc_hip_comm_exchange(g_pinc.comm, 2, sp, sb, snb, rp, rb, rnb, g_pinc.stream), "migrant exchange");
+	}
+	/* import in receive-tag order 26..0: from above, then local, then from below */
+	long offUp = 0, offDown = 0;
+	for (int s = 0; s < ns; s++) {
+		pinc_pop_t p = pinc_devpop(pop);
+		long dst = pop->iStop[s] - pop->iStart[s];
+		if (dst + fromUp[s] + nLocal[s] + fromDown[s] > pop->iStart[s + 1] - pop->iStart[s])
+			msg(ERROR, "population overflow on migration (species %d): raise population:nAlloc", s);
+		pinc_check(pinc_hip_import_rec(p, s, dst, dv->recvBuf[1] + offUp * PINC_REC, fromUp[s], T, g_pinc.stream),
+		           "import from above");
+		dst += fromUp[s];
+		pinc_check(pinc_hip_import(p, s, dst, dv->ws[s].buf, dv->ws[s].cap, dv->ws[s].bufNe, nDown[s], nLocal[s], T,
+		                           (1 << nd) - 1, g_pinc.stream),
+		           "import local");
+		dst += nLocal[s];
+		pinc_check(pinc_hip_import_rec(p, s, dst, dv->recvBuf[0] + offDown * PINC_REC, fromDown[s], T,
+		                               g_pinc.stream),
+		           "import from below");
+		dst += fromDown[s];
+		pop->iStop[s] = pop->iStart[s] + dst;
+		offUp += fromUp[s];
+		offDown += fromDown[s];
+	}
+	dv->flagsValid = 0;
+	pinc_phase_end(2);
+}
+
+/* ------------------------------------------------------------- deposit -- */
+/* gZero; per species gMul(1/q), scatter, gMul(q) (pusher.c:512-572): the
+ * consecutive gMul(q_{s-1}), gMul(1/q_s) become one two-rounding pass. */
+static void distr(const Population *pop, Grid *rho) {
+	pinc_phase_begin(3);
+	PincDevGrid *g = rho->dev;
+	pinc_check(pinc_hip_zero(g->d, g->n, g_pinc.stream), "distr zero");
+	pinc_pop_t p = pinc_devpop(pop);
+	for (int s = 0; s < pop->nSpecies; s++) {
+		if (s > 0)
+			pinc_check(pinc_hip_scale2(g->d, g->n, pop->charge[s - 1], 1.0 / pop->charge[s], g_pinc.stream),
+			           "distr scale");
+		pinc_check(pinc_hip_deposit(p, s, g->geom, g->d, g_pinc.stream), "deposit");
+	}
+	pinc_check(pinc_hip_scale(g->d, g->n, pop->charge[pop->nSpecies - 1], g_pinc.stream), "distr scale");
+	g->ghostsValid = 0;
+	pinc_phase_end(3);
+}
+
+void puDistr3D1(const Population *pop, Grid *rho) { distr(pop, rho); }
+void puDistrND1(const Population *pop, Grid *rho) { distr(pop, rho); }
+
+/* ----------------------------------------------------------- accelerate -- */
+static void acc(Population *pop, Grid *E, int ke) {
+	pinc_phase_begin(6);
+	PincDevPop *dv = pop->dev;
+	pinc_pop_t p = pinc_devpop(pop);
+	int ns = pop->nSpecies;
+	for (int s = 0; s < ns; s++) {
+		int nb = 0;
+		pinc_check(pinc_hip_accelerate(p, s, E->dev->geom, E->dev->d, dv->qm, dv->mq, 1.0, dv->kePartial, &nb,
+		                               g_pinc.stream),
+		           "accelerate");
+		if (nb > 0) pinc_check(pinc_hip_reduce(dv->kePartial, nb, 1.0, PINC_SLOT(16 + s), g_pinc.stream), "ke");
+		else pinc_check(pinc_hip_memset(PINC_SLOT(16 + s), 0, sizeof(double), g_pinc.stream), "ke");
+	}
+	if (ke) {
+		double sums[PINC_MAX_SPECIES];
+		pinc_check(pinc_hip_d2h(sums, PINC_SLOT(16), ns * sizeof(double), g_pinc.stream), "ke readback");
+		for (int s = 0; s < ns; s++) pop->kinEnergy[s] = sums[s] * (0.5 * pop->mass[s]);
+	}
+	pinc_phase_end(6);
+}
+
+void puAcc3D1(Population *pop, Grid *E) { acc(pop, E, 0); }
+void puAcc3D1KE(Population *pop, Grid *E) { acc(pop, E, 1); }
+void puAccND1(Population *pop, Grid *E) { acc(pop, E, 0); }
+void puAccND1KE(Population *pop, Grid *E) { acc(pop, E, 1); }

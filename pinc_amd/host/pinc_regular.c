@@ -1,0 +1,345 @@
+/*
+ * pinc_regular.c -- the PIC run mode (main.c:50-304 with the immersed-object
+ * hooks compiled out) on the MI355X operator surface, and
+ * the PincSim C API that Python (bench.py, tests) drives through ctypes.
+ *
+ * Loop order per step (main.c:197-274, single-add harness of SURVEY.md
+ * Appendix A; literal=1 adds main.c:231-235's second FROMHALO add and the
+ * extra solve):
+ *   puMove -> extractEmigrants -> puMigrate -> distr -> gHaloOp(add,rho,FROM)
+ *   -> solve -> gHaloOp(set,phi,TO) -> gFinDiff1st -> gHaloOp(set,E,TO)
+ *   -> gMul(E,-1) -> acc (+KE) -> pSumKinEnergy -> gPotEnergy
+ * The per-step asserts pVelAssertMax / pPosAssertInLocalFrame are folded into
+ * the move kernel and checked once per step.
+ */
+#define _GNU_SOURCE
+#include "pinc_internal.h"
+#include <math.h>
+
+funPtr regular_set(dictionary *ini) {
+	(void)ini;
+	return (funPtr)regular;
+}
+
+struct PincSim {
+	dictionary *ini;
+	Units *units;
+	MpiInfo *mpi;
+	Population *pop;
+	Grid *E, *rho, *phi;
+	MultigridSolver *solver;
+	void (*acc)(Population *, Grid *);
+	void (*distr)(const Population *, Grid *);
+	void (*extractEmigrants)(Population *, MpiInfo *);
+	PincSimOpts opts;
+	int initialised;
+	long steps;
+};
+
+static int g_simActive = 0;
+
+static void check_errors(void) {
+	int err = 0;
+	pinc_check(pinc_hip_d2h(&err, g_pinc.dErr, sizeof(int), g_pinc.stream), "assert word");
+	if (err & 1) msg(ERROR, "Particle travels too fast (population:maxVel exceeded, population.c:342-365)");
+	if (err & 2) msg(ERROR, "Particle is out of bounds after migration (population.c:316-340)");
+}
+
+static PincSim *sim_build(dictionary *ini, const PincSimOpts *opts) {
+	PincSim *S = calloc(1, sizeof(*S));
+	S->ini = ini;
+	if (opts) S->opts = *opts;
+	else {
+		S->opts.nranks = 1;
+		S->opts.perturb = 1;
+	}
+	if (S->opts.nranks < 1) S->opts.nranks = 1;
+	g_pinc.device = S->opts.device;
+	g_pinc.rank = S->opts.rank;
+	g_pinc.nranks = S->opts.nranks;
+	g_pinc.timing = S->opts.timing;
+	pinc_ctx_require();
+	if (S->opts.nranks > 1 && !g_pinc.comm) {
+		if (!S->opts.commId) msg(ERROR, "multi-rank run without a communicator id");
+		pinc_check(pinc_hip_comm_init(&g_pinc.comm, S->opts.commId, S->opts.nranks, S->opts.rank), "comm init");
+	}
+	/* method selection (main.c:55-79) */
+	S->acc = (void (*)(Population *, Grid *))select(ini, "methods:acc", puAcc3D1_set, puAcc3D1KE_set, puAccND1_set,
+	                                                 puAccND1KE_set);
+	S->distr = (void (*)(const Population *, Grid *))select(ini, "methods:distr", puDistr3D1_set, puDistrND1_set);
+	S->extractEmigrants = (void (*)(Population *, MpiInfo *))select(ini, "methods:migrate", puExtractEmigrants3D_set,
+	                                                                puExtractEmigrantsND_set);
+	void (*solverInterface)() = select(ini, "methods:poisson", mgSolver_set);
+	void (*solve)() = NULL;
+	void *(*solverAlloc)() = NULL;
+	void (*solverFree)() = NULL;
+	((void (*)(void (**)(), void *(**)(), void (**)()))solverInterface)(&solve, &solverAlloc, &solverFree);
+	/* normalisation and allocation (main.c:84-107) */
+	S->units = uAlloc(ini);
+	uNormalize(ini, S->units);
+	S->mpi = gAllocMpi(ini);
+	S->pop = pAlloc(ini);
+	S->E = gAlloc(ini, VECTOR);
+	S->rho = gAlloc(ini, SCALAR);
+	S->phi = gAlloc(ini, SCALAR);
+	S->solver = (MultigridSolver *)((void *(*)(const dictionary *, Grid *, Grid *))solverAlloc)(ini, S->rho, S->phi);
+	gCreateNeighborhood(ini, S->mpi, S->rho);
+	gSetBndSlices(S->phi, S->mpi);
+	g_pinc.maxVel = iniHas(ini, "population:maxVel") ? iniGetDouble(ini, "population:maxVel") : INFINITY;
+	return S;
+}
+
+static void sim_init(PincSim *S) {
+	Population *pop = S->pop;
+	if (S->opts.deviceInit) {
+		pInitDevice(S->ini, pop, S->mpi, S->opts.perturb, S->opts.maxwell, S->opts.seed);
+	} else {
+		pPosLattice(S->ini, pop, S->mpi);
+		if (S->opts.maxwell) pVelMaxwell(S->ini, pop, S->opts.seed);
+		else pVelZero(pop);
+		if (S->opts.perturb) pPosPerturb(S->ini, pop, S->mpi);
+		pSyncToDevice(pop);
+	}
+	S->extractEmigrants(pop, S->mpi);
+	puMigrate(pop, S->mpi, S->rho);
+}
+
+static void sim_fields(PincSim *S) {
+	/* main.c:168-186 */
+	S->distr(S->pop, S->rho);
+	gHaloOp((funPtr)addSlice, S->rho, S->mpi, FROMHALO);
+	mgSolve(S->solver, S->rho, S->phi, S->mpi);
+	pinc_phase_begin(5);
+	gFinDiff1st(S->phi, S->E);
+	gHaloOp((funPtr)setSlice, S->E, S->mpi, TOHALO);
+	gMul(S->E, -1.);
+	pinc_phase_end(5);
+	gMul(S->E, 0.5);
+	S->acc(S->pop, S->E);
+	gMul(S->E, 2.0);
+}
+
+static void sim_step(PincSim *S) {
+	Population *pop = S->pop;
+	puMove(pop, NULL);
+	S->extractEmigrants(pop, S->mpi);
+	puMigrate(pop, S->mpi, S->rho);
+	S->distr(pop, S->rho);
+	gHaloOp((funPtr)addSlice, S->rho, S->mpi, FROMHALO);
+	if (S->opts.literal) {
+		gHaloOp((funPtr)addSlice, S->rho, S->mpi, FROMHALO);
+		mgSolve(S->solver, S->rho, S->phi, S->mpi);
+	}
+	mgSolve(S->solver, S->rho, S->phi, S->mpi);
+	pinc_phase_begin(5);
+	gHaloOp((funPtr)setSlice, S->phi, S->mpi, TOHALO);
+	gFinDiff1st(S->phi, S->E);
+	gHaloOp((funPtr)setSlice, S->E, S->mpi, TOHALO);
+	gMul(S->E, -1.);
+	pinc_phase_end(5);
+	S->acc(pop, S->E);
+	pinc_phase_begin(7);
+	pSumKinEnergy(pop);
+	gPotEnergy(S->rho, S->phi, pop);
+	pinc_phase_end(7);
+	check_errors();
+	S->steps++;
+}
+
+static void sim_free(PincSim *S) {
+	if (!S) return;
+	mgFreeSolver(S->solver);
+	gFree(S->E);
+	gFree(S->rho);
+	gFree(S->phi);
+	pFree(S->pop);
+	gFreeMpi(S->mpi);
+	uFree(S->units);
+	iniClose(S->ini);
+	free(S);
+}
+
+/* main.c:50-304 as a run mode of this library */
+void regular(dictionary *ini) {
+	PincSim *S = sim_build(ini, NULL);
+	sim_init(S);
+	sim_fields(S);
+	int nTimeSteps = iniGetInt(ini, "time:nTimeSteps");
+	for (int n = 1; n <= nTimeSteps; n++) {
+		msg(STATUS, "Computing time-step %i", n);
+		sim_step(S);
+		msg(STATUS, "KE %.17g PE %.17g", S->pop->kinEnergy[S->pop->nSpecies], S->pop->potEnergy[S->pop->nSpecies]);
+	}
+	S->ini = NULL; /* owned by the caller */
+	sim_free(S);
+}
+
+/* ======================================================= PincSim API ===== */
+PincSim *pinc_sim_create(const char *iniPath, int nOver, const char **over, const PincSimOpts *opts) {
+	if (g_simActive) {
+		msg(WARNING, "one simulation per process (the device context is global)");
+		return NULL;
+	}
+	char **argv = calloc(nOver + 2, sizeof(char *));
+	argv[0] = "pinc";
+	argv[1] = (char *)iniPath;
+	for (int i = 0; i < nOver; i++) argv[2 + i] = (char *)over[i];
+	dictionary *ini = iniOpen(nOver + 2, argv);
+	free(argv);
+	PincSim *S = sim_build(ini, opts);
+	g_simActive = 1;
+	return S;
+}
+
+void pinc_sim_free(PincSim *S) {
+	sim_free(S);
+	g_simActive = 0;
+}
+
+int pinc_sim_init(PincSim *S) {
+	sim_init(S);
+	sim_fields(S);
+	S->initialised = 1;
+	return 0;
+}
+
+int pinc_sim_step(PincSim *S) {
+	sim_step(S);
+	return 0;
+}
+
+int pinc_sim_op(PincSim *S, const char *op) {
+	if (!strcmp(op, "init_particles")) sim_init(S);
+	else if (!strcmp(op, "init_fields")) sim_fields(S);
+	else if (!strcmp(op, "move")) puMove(S->pop, NULL);
+	else if (!strcmp(op, "extract")) S->extractEmigrants(S->pop, S->mpi);
+	else if (!strcmp(op, "migrate")) puMigrate(S->pop, S->mpi, S->rho);
+	else if (!strcmp(op, "distr_nohalo")) S->distr(S->pop, S->rho);
+	else if (!strcmp(op, "distr")) {
+		S->distr(S->pop, S->rho);
+		gHaloOp((funPtr)addSlice, S->rho, S->mpi, FROMHALO);
+	} else if (!strcmp(op, "solve")) mgSolve(S->solver, S->rho, S->phi, S->mpi);
+	else if (!strcmp(op, "efield")) {
+		gHaloOp((funPtr)setSlice, S->phi, S->mpi, TOHALO);
+		gFinDiff1st(S->phi, S->E);
+		gHaloOp((funPtr)setSlice, S->E, S->mpi, TOHALO);
+		gMul(S->E, -1.);
+	} else if (!strcmp(op, "acc")) S->acc(S->pop, S->E);
+	else if (!strcmp(op, "energy")) {
+		pSumKinEnergy(S->pop);
+		gPotEnergy(S->rho, S->phi, S->pop);
+	} else if (!strcmp(op, "step")) sim_step(S);
+	else {
+		msg(WARNING, "unknown op %s", op);
+		return 1;
+	}
+	pinc_check(pinc_hip_stream_sync(g_pinc.stream), op);
+	return 0;
+}
+
+int pinc_sim_energy(PincSim *S, double *ke, double *pe, double *keSpecies) {
+	int ns = S->pop->nSpecies;
+	double v[PINC_MAX_SPECIES + 2];
+	v[0] = S->pop->kinEnergy[ns];
+	v[1] = S->pop->potEnergy[ns];
+	for (int s = 0; s < ns; s++) v[2 + s] = S->pop->kinEnergy[s];
+	if (g_pinc.nranks > 1) {
+		double *d = PINC_SLOT(96);
+		pinc_check(pinc_hip_h2d(d, v, (ns + 2) * sizeof(double), g_pinc.stream), "energy");
+		pinc_check(pinc_hip_comm_allreduce_sum(g_pinc.comm, d, d, ns + 2, g_pinc.stream), "energy allreduce");
+		pinc_check(pinc_hip_d2h(v, d, (ns + 2) * sizeof(double), g_pinc.stream), "energy");
+	}
+	*ke = v[0];
+	*pe = v[1];
+	if (keSpecies)
+		for (int s = 0; s < ns; s++) keSpecies[s] = v[2 + s];
+	return 0;
+}
+
+long pinc_sim_cycles(const PincSim *S) { return mgCycleCount(S->solver); }
+int pinc_sim_nspecies(const PincSim *S) { return S->pop->nSpecies; }
+int pinc_sim_ndims(const PincSim *S) { return S->pop->nDims; }
+long pinc_sim_pop_count(PincSim *S, int s) { return S->pop->iStop[s] - S->pop->iStart[s]; }
+
+long pinc_sim_total_particles(PincSim *S) {
+	long n = 0;
+	for (int s = 0; s < S->pop->nSpecies; s++) n += S->pop->iStop[s] - S->pop->iStart[s];
+	return n;
+}
+
+int pinc_sim_pop_get(PincSim *S, int s, double *pos, double *vel) {
+	Population *p = S->pop;
+	pSyncToHost(p);
+	long a = p->iStart[s], n = p->iStop[s] - a, nd = p->nDims;
+	if (pos) memcpy(pos, p->pos + a * nd, n * nd * sizeof(double));
+	if (vel) memcpy(vel, p->vel + a * nd, n * nd * sizeof(double));
+	return 0;
+}
+
+int pinc_sim_pop_set(PincSim *S, int s, long n, const double *pos, const double *vel) {
+	Population *p = S->pop;
+	if (n > p->iStart[s + 1] - p->iStart[s]) {
+		msg(WARNING, "pinc_sim_pop_set: capacity exceeded");
+		return 1;
+	}
+	pSyncToHost(p);
+	long a = p->iStart[s], nd = p->nDims;
+	memcpy(p->pos + a * nd, pos, n * nd * sizeof(double));
+	memcpy(p->vel + a * nd, vel, n * nd * sizeof(double));
+	p->iStop[s] = a + n;
+	pSyncToDevice(p);
+	return 0;
+}
+
+static Grid *which_grid(PincSim *S, int which) {
+	return which == 0 ? S->rho : (which == 1 ? S->phi : S->E);
+}
+
+long pinc_sim_grid_shape(PincSim *S, int which, int *size4) {
+	Grid *g = which_grid(S, which);
+	for (int d = 0; d < 4; d++) size4[d] = d < g->rank ? g->size[d] : 1;
+	return g->sizeProd[g->rank];
+}
+
+int pinc_sim_grid_get(PincSim *S, int which, double *out) {
+	Grid *g = which_grid(S, which);
+	gSyncToHost(g);
+	memcpy(out, g->val, g->sizeProd[g->rank] * sizeof(double));
+	return 0;
+}
+
+int pinc_sim_grid_set(PincSim *S, int which, const double *in) {
+	Grid *g = which_grid(S, which);
+	if (!g->val) g->val = calloc(g->sizeProd[g->rank], sizeof(double));
+	memcpy(g->val, in, g->sizeProd[g->rank] * sizeof(double));
+	gSyncToDevice(g);
+	return 0;
+}
+
+int pinc_sim_emigrants(PincSim *S, long *nEmigrants) {
+	memcpy(nEmigrants, S->mpi->nEmigrants, S->mpi->nNeighbors * S->pop->nSpecies * sizeof(long));
+	return 0;
+}
+
+int pinc_sim_species(PincSim *S, double *charge, double *mass) {
+	memcpy(charge, S->pop->charge, S->pop->nSpecies * sizeof(double));
+	memcpy(mass, S->pop->mass, S->pop->nSpecies * sizeof(double));
+	return 0;
+}
+
+int pinc_sim_sync(PincSim *S) {
+	(void)S;
+	return pinc_hip_stream_sync(g_pinc.stream);
+}
+
+int pinc_sim_timers(PincSim *S, double *ms) {
+	(void)S;
+	for (int i = 0; i < PINC_NPHASES; i++) ms[i] = g_pinc.phaseMs[i];
+	return 0;
+}
+
+int pinc_sim_timers_reset(PincSim *S) {
+	(void)S;
+	for (int i = 0; i < PINC_NPHASES; i++) g_pinc.phaseMs[i] = 0;
+	return 0;
+}

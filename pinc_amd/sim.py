@@ -1,0 +1,138 @@
+"""Python handle on one rank of the MI355X PINC simulation (libpinc.so).
+
+This mirrors the reference's run mode regular() (src/main.c:50-304): the
+ini file plus ``key=value`` overrides select the operators, normalise the
+units and size the population and grids; ``init()`` builds the initial state
+and ``step()`` runs one timestep on the GPU.  All computation happens in the
+native library; this wrapper only moves arguments and diagnostics.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import HOST, PincSimOpts
+
+
+class Sim:
+    def __init__(self, ini: str, overrides: Sequence[str] = (), *, literal: bool = False,
+                 perturb: bool = True, maxwell: bool = False, device_init: bool = False,
+                 seed: int = 0, rank: int = 0, nranks: int = 1, device: int = 0,
+                 comm_id: bytes | None = None, timing: bool = False):
+        self._id_buf = None
+        opts = PincSimOpts()
+        opts.literal = int(literal)
+        opts.perturb = int(perturb)
+        opts.maxwell = int(maxwell)
+        opts.deviceInit = int(device_init)
+        opts.seed = seed
+        opts.rank = rank
+        opts.nranks = nranks
+        opts.device = device
+        opts.timing = int(timing)
+        if comm_id is not None:
+            self._id_buf = (C.c_ubyte * len(comm_id)).from_buffer_copy(comm_id)
+            opts.commId = C.cast(self._id_buf, C.c_void_p)
+        arr = (C.c_char_p * max(1, len(overrides)))(*[o.encode() for o in overrides])
+        self._h = HOST.pinc_sim_create(str(ini).encode(), len(overrides), arr, C.byref(opts))
+        if not self._h:
+            raise RuntimeError("pinc_sim_create failed: " + HOST.pinc_last_error().decode())
+        self.nspecies = HOST.pinc_sim_nspecies(self._h)
+        self.ndims = HOST.pinc_sim_ndims(self._h)
+
+    # -- lifecycle ---------------------------------------------------------
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            HOST.pinc_sim_free(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def init(self) -> None:
+        HOST.pinc_sim_init(self._h)
+
+    def step(self, n: int = 1) -> None:
+        for _ in range(n):
+            HOST.pinc_sim_step(self._h)
+
+    def op(self, name: str) -> None:
+        if HOST.pinc_sim_op(self._h, name.encode()):
+            raise ValueError(f"unknown op {name}")
+
+    def sync(self) -> None:
+        HOST.pinc_sim_sync(self._h)
+
+    # -- diagnostics -------------------------------------------------------
+    def energy(self) -> tuple[float, float, np.ndarray]:
+        ke, pe = C.c_double(), C.c_double()
+        kes = (C.c_double * self.nspecies)()
+        HOST.pinc_sim_energy(self._h, C.byref(ke), C.byref(pe), kes)
+        return ke.value, pe.value, np.array(kes)
+
+    @property
+    def cycles(self) -> int:
+        return HOST.pinc_sim_cycles(self._h)
+
+    def count(self, s: int) -> int:
+        return HOST.pinc_sim_pop_count(self._h, s)
+
+    def total_particles(self) -> int:
+        return HOST.pinc_sim_total_particles(self._h)
+
+    def particles(self, s: int) -> tuple[np.ndarray, np.ndarray]:
+        n = self.count(s)
+        pos = np.zeros((n, self.ndims))
+        vel = np.zeros((n, self.ndims))
+        HOST.pinc_sim_pop_get(self._h, s, pos.ctypes.data, vel.ctypes.data)
+        return pos, vel
+
+    def set_particles(self, s: int, pos: np.ndarray, vel: np.ndarray) -> None:
+        pos = np.ascontiguousarray(pos, dtype=np.float64)
+        vel = np.ascontiguousarray(vel, dtype=np.float64)
+        if HOST.pinc_sim_pop_set(self._h, s, pos.shape[0], pos.ctypes.data, vel.ctypes.data):
+            raise RuntimeError("pinc_sim_pop_set failed")
+
+    def grid_shape(self, which: int) -> tuple[int, ...]:
+        size = (C.c_int * 4)()
+        HOST.pinc_sim_grid_shape(self._h, which, size)
+        return tuple(size)
+
+    def grid(self, which: int) -> np.ndarray:
+        """rho (0), phi (1) or E (2) in the reference layout (value-major,
+        ghost layers included), shaped [nz+2, ny+2, nx+2, nValues] for 3-D."""
+        size = self.grid_shape(which)
+        rank = self.ndims + 1
+        out = np.zeros(int(np.prod(size[:rank])))
+        HOST.pinc_sim_grid_get(self._h, which, out.ctypes.data)
+        return out.reshape(tuple(reversed(size[:rank])))
+
+    def set_grid(self, which: int, values: np.ndarray) -> None:
+        v = np.ascontiguousarray(values, dtype=np.float64).ravel()
+        HOST.pinc_sim_grid_set(self._h, which, v.ctypes.data)
+
+    def emigrants(self) -> np.ndarray:
+        n = 3 ** self.ndims * self.nspecies
+        out = np.zeros(n, dtype=np.int64)
+        HOST.pinc_sim_emigrants(self._h, out.ctypes.data)
+        return out.reshape(3 ** self.ndims, self.nspecies)
+
+    def species(self) -> tuple[np.ndarray, np.ndarray]:
+        q = np.zeros(self.nspecies)
+        m = np.zeros(self.nspecies)
+        HOST.pinc_sim_species(self._h, q.ctypes.data, m.ctypes.data)
+        return q, m
+
+    def timers(self) -> dict[str, float]:
+        ms = np.zeros(_lib.NPHASES)
+        HOST.pinc_sim_timers(self._h, ms.ctypes.data)
+        return dict(zip(_lib.PHASES, ms.tolist()))
+
+    def timers_reset(self) -> None:
+        HOST.pinc_sim_timers_reset(self._h)

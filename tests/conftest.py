@@ -1,0 +1,25 @@
+"""pytest configuration: the `gpu` marker and shared fixtures.
+
+CPU tests (-m "not gpu") cover the oracle against the reference's recorded
+outputs, the host logic and the C ABI exports; GPU tests (-m gpu) are the
+parity tests proper and run through the native libraries on an MI355X.
+"""
+import os
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "oracle"))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libpinc_hip)")
+
+
+@pytest.fixture(scope="session")
+def built():
+    from pinc_amd.build import build
+    return build()
