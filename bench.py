@@ -1,0 +1,232 @@
+#!/usr/bin/env python3
+"""bench.py -- PINC per-timestep PIC hot path on MI355X.
+
+Workload (BASELINE.json metric "particle-updates/sec + Poisson-solve
+ms/step, 256^3 grid 64 ppc, 1/2/4/8 MI355X"): the warm 3-D two-species plasma
+of config C4 (warm_big.ini family) on a 256^3 periodic grid
+with 64 particles per cell per species (2.15 G particles), Maxwellian
+velocities (v_th,e = 0.05 cells/step) from the counter RNG, decomposed into
+N slabs along z for N GPUs (strong scaling: the global problem is fixed).
+One step = move + migrate + deposit + multigrid solve (reference algorithm,
+parity mode) + E field + accelerate, i.e. main.c:197-274.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Rank 0 prints one JSON line.  value = particles x K / (max over ranks of the
+K-step wall time).  The roofline object times the dominant kernel's launches
+inside the timed region with HIP events on the library's stream.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+METRIC = "particle-updates/sec + Poisson-solve ms/step, 256³ grid 64 ppc, 1/2/4/8 MI355X"
+
+
+def _cpu_baseline(size: int, ppc: int, steps: int) -> dict:
+    """The oracle (plain-C restatement of the reference, one core) on a
+    bounded sample of the same workload."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import orc  # test/baseline infrastructure only
+    from pinc_amd import configs
+    cfg = configs.config("warm", true_size=(size, size, size), nsub=(1, 1, 1), ppc=ppc, nalloc_pc=ppc + 8)
+    ini = configs.write_ini(cfg)
+    w = orc.World(ini)
+    w.init(perturb=False, maxwell=True, seed=20260101)
+    w.init_fields()
+    n = w.count(0) + w.count(1)
+    c0 = w.cycles
+    t0 = time.perf_counter()
+    w.step(steps)
+    dt = time.perf_counter() - t0
+    cyc = (w.cycles - c0) / steps
+    w.close()
+    os.unlink(ini)
+    return {"value": n * steps / dt, "unit": "particle-updates/s", "cores": 1, "kind": "port",
+            "sample": f"oracle (C restatement, 1 thread) on the same warm 3-D workload at {size}^3, "
+                      f"{ppc} ppc x 2 species ({n} particles), {steps} steps; {cyc:.0f} V-cycles/solve",
+            "seconds": dt}
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--size", type=int, default=256, help="global cells per dimension")
+    ap.add_argument("--ppc", type=int, default=64)
+    ap.add_argument("--probe", default="gs_pass",
+                    choices=["gs_pass", "accelerate", "move_classify", "deposit", "residual_sumsq"])
+    ap.add_argument("--mg-native", action="store_true", help="corrected coarse-grid scaling (not the reference algorithm)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-size", type=int, default=64)
+    ap.add_argument("--cpu-steps", type=int, default=3)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+        return 2
+
+    import torch
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from pinc_amd import configs, _lib
+    from pinc_amd.sim import Sim
+
+    comm_id = None
+    if world > 1:
+        obj = [_lib.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        comm_id = obj[0]
+
+    S = args.size
+    if S % world:
+        raise SystemExit("grid size must divide by the GPU count")
+    cfg = configs.config("warm", true_size=(S, S, S // world), nsub=(1, 1, world), ppc=args.ppc,
+                         nalloc_pc=args.ppc + 8)
+    if args.mg_native:
+        cfg["multigrid"]["native"] = "1"
+    ini = configs.write_ini(cfg)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    def log(msg):
+        print(f"[bench rank {rank}] {msg}", file=sys.stderr, flush=True)
+
+    t_init0 = time.perf_counter()
+    log(f"creating {S}^3 x {args.ppc} ppc on {world} GPU(s)")
+    sim = Sim(ini, rank=rank, nranks=world, device=local, comm_id=comm_id, maxwell=True, perturb=False,
+              device_init=True, seed=20260101, timing=True)
+    sim.init()
+    sim.sync()
+    t_init = time.perf_counter() - t_init0
+    cycles_init = sim.cycles
+    log(f"init {t_init:.1f} s, {sim.total_particles()} particles, {cycles_init} V-cycles")
+
+    for i in range(args.warmup):
+        tw = time.perf_counter()
+        sim.step()
+        sim.sync()
+        log(f"warmup step {i}: {time.perf_counter() - tw:.2f} s, cycles {sim.cycles}")
+    sim.timers_reset()
+    c0 = sim.cycles
+    _lib.probe_start(args.probe, 4096)
+
+    barrier()
+    torch.cuda.synchronize()
+    sim.sync()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        sim.step()
+        log(f"timed step {i} done at {time.perf_counter() - t0:.2f} s")
+    sim.sync()
+    torch.cuda.synchronize()
+    barrier()
+    dt = time.perf_counter() - t0
+
+    probe = _lib.probe_read()
+    phases = sim.timers()
+    cycles = sim.cycles - c0
+    n_local = sim.total_particles()
+    ke, pe, _ = sim.energy()
+
+    dt_max = dt
+    n_total = n_local
+    if dist is not None:
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt_max = float(t.item())
+        c = torch.tensor([n_local], dtype=torch.int64, device="cuda")
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        n_total = int(c.item())
+
+    K = args.steps
+    value = n_total * K / dt_max
+    ms_step = 1000.0 * dt_max / K
+    solve_ms = phases["solve"] / K
+    push_ms = (phases["move"] + phases["extract"] + phases["migrate"] + phases["deposit"] +
+               phases["accelerate"]) / K
+    achieved = probe["mean_bytes"] / (probe["mean_ms"] * 1e-3) / 1e9 if probe["mean_ms"] > 0 else 0.0
+
+    result = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "particle-updates/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": args.warmup,
+        "ms_per_step": ms_step,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (lattice positions, Maxwellian velocities from a seeded counter RNG)",
+        "config": {
+            "workload": f"C4 warm 3-D two-species plasma, {S}^3 grid, {args.ppc} ppc per species "
+                        f"({n_total} particles), 1D slab decomposition 1,1,{world}",
+            "grid": [S, S, S],
+            "ppc_per_species": args.ppc,
+            "species": 2,
+            "particles": n_total,
+            "decomposition": f"1,1,{world}",
+            "poisson": "multigrid mgVRecursive, 5 levels, RB Gauss-Seidel 10/10/10, "
+                       + ("native coarse scaling" if args.mg_native else "reference algorithm (parity mode)"),
+        },
+        "poisson_ms_per_step": solve_ms,
+        "push_deposit_ms_per_step": push_ms,
+        "push_deposit_updates_per_s": n_local / (push_ms * 1e-3) * world if push_ms > 0 else None,
+        "mg_cycles_per_solve": cycles / K,
+        "phase_ms_per_step": {k: v / K for k, v in phases.items()},
+        "init_s": t_init,
+        "init_cycles": cycles_init,
+        "energy": {"KE": ke, "PE": pe},
+        "roofline": {
+            "bound": "hbm",
+            "kernel": args.probe,
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": None,
+            "bytes_per_launch": probe["mean_bytes"],
+            "mean_launch_ms": probe["mean_ms"],
+            "samples": probe["samples"],
+            "launches": probe["launches"],
+        },
+        "cpu_baseline": None,
+    }
+    sim.close()
+    os.unlink(ini)
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = _cpu_baseline(args.cpu_size, args.ppc, args.cpu_steps)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -118,6 +118,7 @@ typedef struct {
 	double maxVel;
 	/* diagnostics */
 	long cycles;        /* V-cycles run so far */
+	int verbose;        /* ORC_VERBOSE=n: MG progress every n cycles (stderr) */
 	long solves;
 	double lastKE, lastPE;
 	double *keSpecies;  /* nSpecies */

@@ -244,6 +244,8 @@ void ow_mg_solve(OWorld *w){
 			double sum = 0;
 			for(int r = 0; r < w->P; r++){ og_square(res[r]); sum += og_sum_true(res[r]); }
 			barRes = sqrt(sum/N);
+			if(w->verbose && w->cycles % w->verbose == 0)
+				fprintf(stderr, "[orc] cycle %ld residual %.3e\n", (long)w->cycles, barRes);
 		}
 	} else {
 		OGrid *rho[256], *phi[256];

@@ -180,6 +180,7 @@ static void select_methods(OWorld *w){
 /* ------------------------------------------------------------- world -- */
 OWorld *ow_create(OIni *ini, int literal){
 	OWorld *w = calloc(1, sizeof(*w));
+	{ const char *ev = getenv("ORC_VERBOSE"); w->verbose = ev ? atoi(ev) : 0; }
 	w->ini = ini;
 	w->literal = literal;
 	select_methods(w);

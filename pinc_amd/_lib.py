@@ -65,7 +65,21 @@ _sigs = {
     "pinc_sim_timers": (C.c_int, [C.c_void_p, C.c_void_p]),
     "pinc_sim_timers_reset": (C.c_int, [C.c_void_p]),
     "pinc_sim_total_particles": (C.c_long, [C.c_void_p]),
+    "pinc_probe_start": (C.c_int, [C.c_int, C.c_int]),
+    "pinc_probe_read": (C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_int),
+                                  C.POINTER(C.c_long)]),
 }
+PROBES = {"gs_pass": 0, "accelerate": 1, "move_classify": 2, "deposit": 3, "residual_sumsq": 4}
+
+
+def probe_start(kernel: str, max_samples: int = 4096) -> None:
+    HOST.pinc_probe_start(PROBES[kernel], max_samples)
+
+
+def probe_read() -> dict:
+    ms, b, n, launches = C.c_double(), C.c_double(), C.c_int(), C.c_long()
+    HOST.pinc_probe_read(C.byref(ms), C.byref(b), C.byref(n), C.byref(launches))
+    return {"mean_ms": ms.value, "mean_bytes": b.value, "samples": n.value, "launches": launches.value}
 for _n, (_r, _a) in _sigs.items():
     _f = getattr(HOST, _n)
     _f.restype = _r
@@ -90,6 +104,7 @@ def header_symbols(header: Path) -> list[str]:
     import re
     text = header.read_text()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    text = "\n".join(l for l in text.splitlines() if not l.lstrip().startswith(("typedef", "#")))
     names = re.findall(r"^[A-Za-z_][\w \*]*?\b(\w+)\s*\(", text, flags=re.M)
-    skip = {"if", "for", "while", "return", "sizeof", "defined"}
+    skip = {"if", "for", "while", "return", "sizeof", "defined", "void", "int", "double", "long", "char"}
     return sorted({n for n in names if n not in skip and not n.startswith("__")})

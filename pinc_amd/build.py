@@ -2,9 +2,9 @@
 
     pinc_amd/lib/libpinc_hip.so   gfx950 kernels + C ABI (include/pinc_hip.h)
     pinc_amd/lib/libpinc.so       host operator surface in C (include/pinc.h)
-    oracle/build/liborc.so        CPU oracle (test infrastructure only)
 
-Run ``python -m pinc_amd.build`` (or ``__graft_entry__.build()``).
+Run ``python -m pinc_amd.build``; ``__graft_entry__.build()`` also builds the
+CPU checker under oracle/ (test infrastructure, not part of this package).
 """
 from __future__ import annotations
 
@@ -71,10 +71,7 @@ def build(verbose: bool = False, jobs: int = 8) -> dict:
               "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"])
         _run(["gcc", "-shared", "-o", str(libhost), *c_objs, f"-L{LIB}", "-lpinc_hip", "-lm",
               "-Wl,-rpath,$ORIGIN"])
-    # oracle (plain C, test infrastructure)
-    _run(["make", "-s", "-C", str(ROOT / "oracle"), "-j4"])
-    out = {"libpinc_hip": str(libhip), "libpinc": str(libhost),
-           "liborc": str(ROOT / "oracle" / "build" / "liborc.so")}
+    out = {"libpinc_hip": str(libhip), "libpinc": str(libhost)}
     if verbose:
         print(out)
     return out

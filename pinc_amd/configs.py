@@ -53,11 +53,11 @@ def _langmuir_nd(nd: int) -> dict:
     }
 
 
-def _cold3d() -> dict:
+def _cold3d(true_size=(32, 16, 16), nsub=(1, 1, 1)) -> dict:
     return {
         "time": {"nTimeSteps": "45", "timeStep": "0.2"},
-        "grid": {"nDims": "3", "nSubdomains": "1,1,1", "nEmigrantsAlloc": "1 pc, 2 pc, 4 pc",
-                 "trueSize": "32,16,16", "stepSize": "0.005", "nGhostLayers": "1", "thresholds": "0.1",
+        "grid": {"nDims": "3", "nSubdomains": ",".join(map(str, nsub)), "nEmigrantsAlloc": "1 pc, 2 pc, 4 pc",
+                 "trueSize": ",".join(map(str, true_size)), "stepSize": "0.005", "nGhostLayers": "1", "thresholds": "0.1",
                  "boundaries": "PERIODIC"},
         "fields": {"BExt": "0,0,0", "EExt": "0,0,0"},
         "population": {"nSpecies": "2", "nParticles": "64 pc", "nAlloc": "96 pc", "charge": "-1,1",
@@ -110,7 +110,7 @@ def config(name: str, **kw) -> dict:
         c["population"]["nAlloc"] = "48 pc"
         return c
     if name == "cold3d":
-        return _cold3d()
+        return _cold3d(**kw)
     if name == "warm":
         return _warm(**kw)
     raise KeyError(name)

@@ -475,6 +475,8 @@ void pinc_ctx_require(void) {
 	pinc_check(pinc_hip_malloc((void **)&g_pinc.dErr, 64), "err word");
 	pinc_check(pinc_hip_memset(g_pinc.dErr, 0, 64, g_pinc.stream), "err word");
 	if (g_pinc.nranks < 1) g_pinc.nranks = 1;
+	g_pinc.probeKernel = -1;
+	g_pinc.verbose = getenv("PINC_VERBOSE") ? atoi(getenv("PINC_VERBOSE")) : 0;
 	for (int i = 0; i < 2 * PINC_NPHASES; i++) pinc_check(pinc_hip_event_create(&g_pinc.ev[i]), "event");
 	g_pinc.initialised = 1;
 }
@@ -492,6 +494,55 @@ void pinc_phase_end(int p) {
 	pinc_check(pinc_hip_event_elapsed(&ms, g_pinc.ev[2 * p], g_pinc.ev[2 * p + 1]), "elapsed");
 	g_pinc.phaseMs[p] += ms;
 	g_pinc.phaseOpen[p] = 0;
+}
+
+/* ------------------------------------------------------------- probe -- */
+int pinc_probe_start(int kernel, int maxSamples) {
+	pinc_ctx_require();
+	if (g_pinc.probeEv) {
+		for (int i = 0; i < 2 * g_pinc.probeMax; i++) pinc_hip_event_destroy(g_pinc.probeEv[i]);
+		free(g_pinc.probeEv);
+		free(g_pinc.probeBytes);
+	}
+	g_pinc.probeKernel = kernel;
+	g_pinc.probeMax = maxSamples;
+	g_pinc.probeN = 0;
+	g_pinc.probeLaunches = 0;
+	g_pinc.probeEv = calloc(2 * maxSamples, sizeof(void *));
+	g_pinc.probeBytes = calloc(maxSamples, sizeof(double));
+	for (int i = 0; i < 2 * maxSamples; i++) pinc_check(pinc_hip_event_create(&g_pinc.probeEv[i]), "probe event");
+	return 0;
+}
+
+int pinc_probe_begin(int k) {
+	if (!g_pinc.probeEv || k != g_pinc.probeKernel) return -1;
+	g_pinc.probeLaunches++;
+	if (g_pinc.probeN >= g_pinc.probeMax) return -1;
+	int slot = g_pinc.probeN++;
+	pinc_check(pinc_hip_event_record(g_pinc.probeEv[2 * slot], g_pinc.stream), "probe");
+	return slot;
+}
+
+void pinc_probe_end(int k, int slot, double bytes) {
+	if (slot < 0 || k != g_pinc.probeKernel) return;
+	pinc_check(pinc_hip_event_record(g_pinc.probeEv[2 * slot + 1], g_pinc.stream), "probe");
+	g_pinc.probeBytes[slot] = bytes;
+}
+
+int pinc_probe_read(double *meanMs, double *meanBytes, int *samples, long *launches) {
+	double t = 0, b = 0;
+	int n = g_pinc.probeN;
+	for (int i = 0; i < n; i++) {
+		float ms = 0;
+		pinc_check(pinc_hip_event_elapsed(&ms, g_pinc.probeEv[2 * i], g_pinc.probeEv[2 * i + 1]), "probe read");
+		t += ms;
+		b += g_pinc.probeBytes[i];
+	}
+	*meanMs = n ? t / n : 0;
+	*meanBytes = n ? b / n : 0;
+	*samples = n;
+	*launches = g_pinc.probeLaunches;
+	return 0;
 }
 
 /* reduce the first nParts partials in the scratch area into slot 0; read it */

@@ -26,11 +26,23 @@ typedef struct {
 	double maxVel;
 	double thr[9];      /* migration thresholds lo[nd], up[nd], assert bound[nd] */
 	int thrSet;
+	int verbose;        /* PINC_VERBOSE=n: progress every n V-cycles */
 	int timing;
 	void *ev[2*PINC_NPHASES];
 	double phaseMs[PINC_NPHASES];
 	int phaseOpen[PINC_NPHASES];
+	/* kernel probe: HIP events around launches of one kernel, read lazily
+	 * (no host synchronisation inside the timed region) */
+	int probeKernel;          /* PINC_PROBE_* or -1 */
+	int probeMax, probeN;     /* capacity, recorded pairs */
+	void **probeEv;           /* 2*probeMax events */
+	double *probeBytes;       /* algorithmic bytes of each recorded launch */
+	long probeLaunches;       /* launches seen (recorded or not) */
 } PincCtx;
+
+/* probe hooks around a launch of kernel k with algorithmic byte count b */
+int pinc_probe_begin(int k);
+void pinc_probe_end(int k, int slot, double bytes);
 
 extern PincCtx g_pinc;
 

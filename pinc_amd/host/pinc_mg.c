@@ -142,9 +142,13 @@ static void smooth(MultigridSolver *S, int q, int nIter, int nd3) {
 	for (int k = 0; k < nPass; k++) {
 		const double *muPrev = k ? PINC_SLOT(MU_SLOT + ((k - 1) & 1)) : NULL;
 		int nb = 0;
+		/* algorithmic bytes of one colour pass: half of a
+		 * red+black iteration's 24 B per point (phi R+W, rho R) */
+		int slot = q == 0 ? pinc_probe_begin(PINC_PROBE_GS) : -1;
 		pinc_check(pinc_hip_gs_pass(S->phi[q], S->rho[q], S->L[q], k & 1, nd3, muPrev, g_pinc.dScratch, &nb,
 		                            g_pinc.stream),
 		           "gs pass");
+		pinc_probe_end(PINC_PROBE_GS, slot, 12.0 * S->N[q]);
 		pinc_check(pinc_hip_reduce(g_pinc.dScratch, nb, (double)S->N[q], PINC_SLOT(MU_SLOT + (k & 1)), g_pinc.stream),
 		           "gs mean");
 	}
@@ -192,13 +196,19 @@ void mgSolve(MultigridSolver *S, Grid *rho, Grid *phi, const MpiInfo *mpiInfo) {
 			vrec(S, 0);
 			S->cycles++;
 			int nb = 0;
+			int slot = pinc_probe_begin(PINC_PROBE_RESIDUAL);
 			pinc_check(pinc_hip_residual_sumsq(S->phi[0], S->rho[0], S->L[0], g_pinc.dScratch, &nb, g_pinc.stream),
 			           "residual norm");
+			pinc_probe_end(PINC_PROBE_RESIDUAL, slot, 16.0 * S->N[0]);
 			pinc_check(pinc_hip_reduce(g_pinc.dScratch, nb, 1.0, PINC_SLOT(TMP_SLOT + 1), g_pinc.stream), "norm");
 			double sum = 0;
 			pinc_check(pinc_hip_d2h(&sum, PINC_SLOT(TMP_SLOT + 1), sizeof(double), g_pinc.stream), "norm");
 			barRes = sqrt(sum / S->N[0]);
 			if (++c > maxCycles || isnan(barRes)) msg(ERROR, "multigrid did not converge (residual %g)", barRes);
+			if (g_pinc.verbose && (c % g_pinc.verbose == 0)) {
+				fprintf(stderr, "[pinc] rank %d solve cycle %ld residual %.3e\n", g_pinc.rank, c, barRes);
+				fflush(stderr);
+			}
 		}
 	} else {
 		for (int c = 0; c < S->mgCycles; c++) {

@@ -92,10 +92,15 @@ static void classify(Population *pop, int doMove) {
 	if (!g_pinc.thrSet) msg(ERROR, "gCreateNeighborhood must run before puMove/extract");
 	PincDevPop *dv = pop->dev;
 	pinc_pop_t p = pinc_devpop(pop);
-	for (int s = 0; s < pop->nSpecies; s++)
+	for (int s = 0; s < pop->nSpecies; s++) {
+		long n = pop->iStop[s] - pop->iStart[s];
+		int slot = doMove ? pinc_probe_begin(PINC_PROBE_MOVE) : -1;
 		pinc_check(pinc_hip_move_classify(p, s, doMove, g_pinc.thr, dv->flags, dv->chunkCount + dv->chunkBase[s],
 		                                  g_pinc.maxVel, g_pinc.dErr, g_pinc.stream),
 		           "move/classify");
+		/* read pos+vel, write pos: 72 B per 3-D particle */
+		pinc_probe_end(PINC_PROBE_MOVE, slot, 24.0 * pop->nDims * n);
+	}
 	dv->flagsValid = 1;
 }
 
@@ -278,7 +283,11 @@ static void distr(const Population *pop, Grid *rho) {
 		if (s > 0)
 			pinc_check(pinc_hip_scale2(g->d, g->n, pop->charge[s - 1], 1.0 / pop->charge[s], g_pinc.stream),
 			           "distr scale");
+		int slot = pinc_probe_begin(PINC_PROBE_DEPOSIT);
 		pinc_check(pinc_hip_deposit(p, s, g->geom, g->d, g_pinc.stream), "deposit");
+		/* read pos (8 B per dim per particle) + write rho (8 B per node) */
+		pinc_probe_end(PINC_PROBE_DEPOSIT, slot,
+		               8.0 * pop->nDims * (pop->iStop[s] - pop->iStart[s]) + 8.0 * g->n);
 	}
 	pinc_check(pinc_hip_scale(g->d, g->n, pop->charge[pop->nSpecies - 1], g_pinc.stream), "distr scale");
 	g->ghostsValid = 0;
@@ -296,9 +305,13 @@ static void acc(Population *pop, Grid *E, int ke) {
 	int ns = pop->nSpecies;
 	for (int s = 0; s < ns; s++) {
 		int nb = 0;
+		int slot = pinc_probe_begin(PINC_PROBE_ACCEL);
 		pinc_check(pinc_hip_accelerate(p, s, E->dev->geom, E->dev->d, dv->qm, dv->mq, 1.0, dv->kePartial, &nb,
 		                               g_pinc.stream),
 		           "accelerate");
+		/* read pos+vel, write vel (72 B per 3-D particle) + read E once */
+		pinc_probe_end(PINC_PROBE_ACCEL, slot,
+		               24.0 * pop->nDims * (pop->iStop[s] - pop->iStart[s]) + 8.0 * E->dev->n);
 		if (nb > 0) pinc_check(pinc_hip_reduce(dv->kePartial, nb, 1.0, PINC_SLOT(16 + s), g_pinc.stream), "ke");
 		else pinc_check(pinc_hip_memset(PINC_SLOT(16 + s), 0, sizeof(double), g_pinc.stream), "ke");
 	}

@@ -21,5 +21,7 @@ def pytest_configure(config):
 
 @pytest.fixture(scope="session")
 def built():
+    import subprocess
     from pinc_amd.build import build
+    subprocess.run(["make", "-s", "-C", str(ROOT / "oracle"), "-j4"], check=True)
     return build()
