@@ -7,15 +7,18 @@ of config C4 (warm_big.ini family) on a 256^3 periodic grid
 with 64 particles per cell per species (2.15 G particles), Maxwellian
 velocities (v_th,e = 0.05 cells/step) from the counter RNG, decomposed into
 N slabs along z for N GPUs (strong scaling: the global problem is fixed).
-One step = move + migrate + deposit + multigrid solve (reference algorithm,
-parity mode) + E field + accelerate, i.e. main.c:197-274.
+One step = move + migrate + deposit + multigrid solve + E field + accelerate,
+i.e. main.c:197-274.  The solve runs in native mode by default: the
+reference's own mgVRecursive does not converge on this grid (DESIGN.md
+section 6; --mg reference runs it anyway).
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 Rank 0 prints one JSON line.  value = particles x K / (max over ranks of the
-K-step wall time).  The roofline object times the dominant kernel's launches
-inside the timed region with HIP events on the library's stream.
+K-step wall time).  Every probed kernel's launches inside the timed region
+are timed with HIP events on the library's stream; `roofline` reports the
+one with the most time per step, `kernels` all of them.
 """
 from __future__ import annotations
 
@@ -31,6 +34,14 @@ sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 METRIC = "particle-updates/sec + Poisson-solve ms/step, 256³ grid 64 ppc, 1/2/4/8 MI355X"
+# kernel names as rocprofv3 --kernel-trace reports them (3-D instantiations)
+ROCPROF_NAMES = {
+    "gs_pass": "k_gs_pass<3, true>",
+    "accelerate": "k_accel<3, true, true>",
+    "move_classify": "k_move_classify<3>",
+    "deposit": "k_deposit_tiled<3, true>",
+    "residual_sumsq": "k_residual_sumsq<3>",
+}
 
 
 def _cpu_baseline(size: int, ppc: int, steps: int) -> dict:
@@ -65,9 +76,10 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--size", type=int, default=256, help="global cells per dimension")
     ap.add_argument("--ppc", type=int, default=64)
-    ap.add_argument("--probe", default="gs_pass",
-                    choices=["gs_pass", "accelerate", "move_classify", "deposit", "residual_sumsq"])
-    ap.add_argument("--mg-native", action="store_true", help="corrected coarse-grid scaling (not the reference algorithm)")
+    ap.add_argument("--mg", default="native", choices=["native", "reference"],
+                    help="native: correction-scheme V-cycle with the coarse h^2 factor (default; the reference "
+                         "algorithm does not converge at 256^3 with 5 levels, DESIGN.md section 6); reference: "
+                         "the reference's mgVRecursive exactly")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-size", type=int, default=64)
     ap.add_argument("--cpu-steps", type=int, default=3)
@@ -102,7 +114,7 @@ def main() -> int:
         raise SystemExit("grid size must divide by the GPU count")
     cfg = configs.config("warm", true_size=(S, S, S // world), nsub=(1, 1, world), ppc=args.ppc,
                          nalloc_pc=args.ppc + 8)
-    if args.mg_native:
+    if args.mg == "native":
         cfg["multigrid"]["native"] = "1"
     ini = configs.write_ini(cfg)
 
@@ -130,7 +142,7 @@ def main() -> int:
         log(f"warmup step {i}: {time.perf_counter() - tw:.2f} s, cycles {sim.cycles}")
     sim.timers_reset()
     c0 = sim.cycles
-    _lib.probe_start(args.probe, 4096)
+    _lib.probe_start("all", 4096)
 
     barrier()
     torch.cuda.synchronize()
@@ -144,7 +156,7 @@ def main() -> int:
     barrier()
     dt = time.perf_counter() - t0
 
-    probe = _lib.probe_read()
+    probes = {k: _lib.probe_read(k) for k in _lib.PROBES}
     phases = sim.timers()
     cycles = sim.cycles - c0
     n_local = sim.total_particles()
@@ -166,7 +178,20 @@ def main() -> int:
     solve_ms = phases["solve"] / K
     push_ms = (phases["move"] + phases["extract"] + phases["migrate"] + phases["deposit"] +
                phases["accelerate"]) / K
-    achieved = probe["mean_bytes"] / (probe["mean_ms"] * 1e-3) / 1e9 if probe["mean_ms"] > 0 else 0.0
+    kernels = {}
+    for k, p in probes.items():
+        if p["samples"] == 0 or p["mean_ms"] <= 0:
+            continue
+        gbs = p["mean_bytes"] / (p["mean_ms"] * 1e-3) / 1e9
+        kernels[k] = {"rocprof_name": ROCPROF_NAMES[k], "mean_launch_ms": p["mean_ms"],
+                      "bytes_per_launch": p["mean_bytes"], "achieved_GBs": gbs, "frac": gbs / HBM_PEAK_GBS,
+                      "launches": p["launches"], "samples": p["samples"],
+                      "est_ms_per_step": p["mean_ms"] * p["launches"] / args.steps}
+    dom = max(kernels, key=lambda k: kernels[k]["est_ms_per_step"])
+    dk = kernels[dom]
+    # push+deposit against SURVEY.md 8(d): 144 B per particle-update (3-D)
+    pd_bytes = 144.0 * n_local + 32.0 * S ** 3 / world
+    pd_gbs = pd_bytes / (push_ms * 1e-3) / 1e9 if push_ms > 0 else 0.0
 
     result = {
         "metric": METRIC,
@@ -190,7 +215,8 @@ def main() -> int:
             "particles": n_total,
             "decomposition": f"1,1,{world}",
             "poisson": "multigrid mgVRecursive, 5 levels, RB Gauss-Seidel 10/10/10, "
-                       + ("native coarse scaling" if args.mg_native else "reference algorithm (parity mode)"),
+                       + ("native mode (correction scheme, coarse h^2 factor)" if args.mg == "native"
+                          else "reference algorithm (parity mode)"),
         },
         "poisson_ms_per_step": solve_ms,
         "push_deposit_ms_per_step": push_ms,
@@ -202,17 +228,22 @@ def main() -> int:
         "energy": {"KE": ke, "PE": pe},
         "roofline": {
             "bound": "hbm",
-            "kernel": args.probe,
-            "achieved": achieved,
+            "kernel": dom,
+            "rocprof_name": dk["rocprof_name"],
+            "achieved": dk["achieved_GBs"],
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS,
+            "frac": dk["frac"],
             "traffic": None,
-            "bytes_per_launch": probe["mean_bytes"],
-            "mean_launch_ms": probe["mean_ms"],
-            "samples": probe["samples"],
-            "launches": probe["launches"],
+            "bytes_per_launch": dk["bytes_per_launch"],
+            "mean_launch_ms": dk["mean_launch_ms"],
+            "samples": dk["samples"],
+            "launches": dk["launches"],
         },
+        "push_deposit_roofline": {"bytes_per_step": pd_bytes, "achieved": pd_gbs, "peak": HBM_PEAK_GBS,
+                                  "unit": "GB/s", "frac": pd_gbs / HBM_PEAK_GBS,
+                                  "basis": "144 B per particle-update + 32 B per cell (SURVEY.md 8(d))"},
+        "kernels": kernels,
         "cpu_baseline": None,
     }
     sim.close()

@@ -232,17 +232,20 @@ int pinc_sim_sync(PincSim *sim);
 #define PINC_NPHASES 8
 int pinc_sim_timers(PincSim *sim, double *ms);
 int pinc_sim_timers_reset(PincSim *sim);
-/* Kernel probe: record HIP events around up to maxSamples launches of one
- * kernel on the library's stream, without host synchronisation; read the
- * mean duration and mean algorithmic bytes per launch afterwards.
- * Algorithmic bytes follow SURVEY.md 8(d) (DESIGN.md "Roofline"). */
+/* Kernel probes: record HIP events around up to maxSamples launches of each
+ * probed kernel on the library's stream, without host synchronisation; read
+ * the mean duration and mean algorithmic bytes per launch afterwards.
+ * Algorithmic bytes follow SURVEY.md 8(d).
+ * pinc_probe_start(PINC_PROBE_ALL, n) probes every kernel below. */
 #define PINC_PROBE_GS 0        /* red-black smoothing pass, finest level */
 #define PINC_PROBE_ACCEL 1     /* gather + accelerate */
 #define PINC_PROBE_MOVE 2      /* move + classify */
 #define PINC_PROBE_DEPOSIT 3   /* charge deposit */
 #define PINC_PROBE_RESIDUAL 4  /* residual norm, finest level */
+#define PINC_NPROBES 5
+#define PINC_PROBE_ALL (-1)
 int pinc_probe_start(int kernel, int maxSamples);
-int pinc_probe_read(double *meanMs, double *meanBytes, int *samples, long *launches);
+int pinc_probe_read(int kernel, double *meanMs, double *meanBytes, int *samples, long *launches);
 long pinc_sim_total_particles(PincSim *sim);
 
 #ifdef __cplusplus

@@ -129,13 +129,18 @@ int pinc_hip_import(pinc_pop_t pop, int s, long dst, const double *buf, long cap
  * reference's 1/q, q rescaling with pinc_hip_scale). */
 int pinc_hip_deposit(pinc_pop_t pop, int s, pinc_geom_t g, double *rhoSlab, void *stream);
 
+/* E as the reference holds it while species s is accelerated: its sequence
+ * of in-place gMul(E, q/m) ... gMul(E, m/q) (pusher.c:192,212) gives
+ * Es = E*pre; for t<s: Es = (Es*qm[t])*mq[t]; Es *= qm[s] (same rounding).
+ * n doubles of the slab E grid; qm/mq are device arrays. */
+int pinc_hip_field_chain(const double *E, double *Es, long n, const double *qm, const double *mq,
+                         double pre, int s, void *stream);
+
 /* puAcc3D1KE / puAccND1KE (pusher.c:178-265) with puInterp3D1/ND1
- * (pusher.c:1089-1162).  E node values are rescaled on the fly exactly as
- * the reference's sequence of in-place gMul(E, q/m), gMul(E, m/q) does:
- * value = E*pre; for t<s: value = (value*qm[t])*mq[t]; value *= qm[s].
- * kePartial receives per-block partial sums of v.(v+dv); nBlocks returned. */
-int pinc_hip_accelerate(pinc_pop_t pop, int s, pinc_geom_t g, const double *Eslab,
-                        const double *qm, const double *mq, double pre,
+ * (pusher.c:1089-1162), gathering from Es (pinc_hip_field_chain).
+ * kePartial receives per-block partial sums of v.(v+dv) (at most
+ * ceil((n+1)/2048) blocks); nBlocks returned. */
+int pinc_hip_accelerate(pinc_pop_t pop, int s, pinc_geom_t g, const double *Es,
                         double *kePartial, int *nBlocks, void *stream);
 
 /* device-side initial conditions (pPosLattice population.c:172-240,

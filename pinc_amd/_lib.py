@@ -66,19 +66,23 @@ _sigs = {
     "pinc_sim_timers_reset": (C.c_int, [C.c_void_p]),
     "pinc_sim_total_particles": (C.c_long, [C.c_void_p]),
     "pinc_probe_start": (C.c_int, [C.c_int, C.c_int]),
-    "pinc_probe_read": (C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_int),
+    "pinc_probe_read": (C.c_int, [C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_int),
                                   C.POINTER(C.c_long)]),
 }
 PROBES = {"gs_pass": 0, "accelerate": 1, "move_classify": 2, "deposit": 3, "residual_sumsq": 4}
 
 
-def probe_start(kernel: str, max_samples: int = 4096) -> None:
-    HOST.pinc_probe_start(PROBES[kernel], max_samples)
+def probe_start(kernel: str = "all", max_samples: int = 4096) -> None:
+    """Start HIP-event probes on one kernel (PROBES key) or on all of them."""
+    k = -1 if kernel == "all" else PROBES[kernel]
+    if HOST.pinc_probe_start(k, max_samples):
+        raise ValueError(f"bad probe {kernel!r}")
 
 
-def probe_read() -> dict:
+def probe_read(kernel: str) -> dict:
+    """Mean duration (ms) and algorithmic bytes per probed launch."""
     ms, b, n, launches = C.c_double(), C.c_double(), C.c_int(), C.c_long()
-    HOST.pinc_probe_read(C.byref(ms), C.byref(b), C.byref(n), C.byref(launches))
+    HOST.pinc_probe_read(PROBES[kernel], C.byref(ms), C.byref(b), C.byref(n), C.byref(launches))
     return {"mean_ms": ms.value, "mean_bytes": b.value, "samples": n.value, "launches": launches.value}
 for _n, (_r, _a) in _sigs.items():
     _f = getattr(HOST, _n)

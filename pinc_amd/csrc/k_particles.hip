@@ -331,14 +331,15 @@ struct Geo {
 };
 
 __device__ __forceinline__ Geo make_geo(const pinc_geom_t &g) {
+	// fully unrolled: no dynamically indexed register arrays (scratch)
 	Geo r;
-	for (int d = 0; d < 3; d++) r.T[d] = g.T[d];
 	r.slab = g.nd - 1;
-	r.T[r.slab] = g.nloc;
 	long s = 1;
-	for (int d = 0; d < g.nd; d++) {
+#pragma unroll
+	for (int d = 0; d < 3; d++) {
+		r.T[d] = (d == r.slab) ? g.nloc : g.T[d];
 		r.stride[d] = s;
-		s *= (d == r.slab) ? (long)(g.nloc + 2) : (long)r.T[d];
+		if (d < g.nd) s *= (d == r.slab) ? (long)(g.nloc + 2) : (long)r.T[d];
 	}
 	return r;
 }
@@ -349,69 +350,279 @@ __device__ __forceinline__ long node_off(const Geo &G, int d, int p) {
 	return (long)s * G.stride[d];
 }
 
+// --------------------------------------------- LDS-privatised deposit -----
+// One workgroup owns a chunk of kDepChunk consecutive particles; each thread
+// owns kDepItems consecutive ones (one 16-B load per pair and component).
+// Particles keep the reference's order, which stays spatially coherent
+// (lattice start, slow drift), so:
+//  * consecutive particles of one thread mostly share a cell: their eight
+//    weights are summed in registers and written once per run of equal
+//    cells, and lanes of one wave hit distinct nodes (no same-address LDS
+//    atomics inside an instruction);
+//  * the chunk covers a small box of nodes, accumulated in LDS (ds_add_f64)
+//    and flushed with one global atomic per touched node.
+// Chunks whose box exceeds the LDS tile use the same run accumulation with
+// global atomics.  Weights are the reference's expressions (pusher.c:550-565,
+// 626-638); only the summation order differs from the serial loop.
+constexpr int kDepItems = 8;
+constexpr int kDepChunk = kThreads * kDepItems;
+constexpr int kDepCap = 4096;  // LDS nodes per workgroup (32 KiB)
+
+__device__ __forceinline__ int wave_min_i(int v) {
+#pragma unroll
+	for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+	return v;
+}
+__device__ __forceinline__ int wave_max_i(int v) {
+#pragma unroll
+	for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+	return v;
+}
+
 template <int ND, bool V3D>
-__global__ __launch_bounds__(kThreads) void k_deposit(const double *__restrict__ x0,
-                                                      const double *__restrict__ x1,
-                                                      const double *__restrict__ x2, long n,
-                                                      pinc_geom_t g, double *__restrict__ rho) {
-	Geo G = make_geo(g);
-	const double *xs[3] = {x0, x1, x2};
-	for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-	     i += (long)gridDim.x * blockDim.x) {
-		double dec[3], comp[3];
-		long o0[3], o1[3];
+__device__ __forceinline__ void cic_weights(const double *dec, const double *comp, double *w) {
+	if (V3D) {
+		double xc = comp[0], yc = comp[1], zc = comp[2];
+		double x = dec[0], y = dec[1], z = dec[2];
+		w[0] = xc * yc * zc;
+		w[1] = x * yc * zc;
+		w[2] = xc * y * zc;
+		w[3] = x * y * zc;
+		w[4] = xc * yc * z;
+		w[5] = x * yc * z;
+		w[6] = xc * y * z;
+		w[7] = x * y * z;
+	} else {
 #pragma unroll
-		for (int d = 0; d < ND; d++) {
-			double p = xs[d][i];
-			int j = (int)p;
-			dec[d] = p - j;
-			comp[d] = 1 - dec[d];
-			o0[d] = node_off(G, d, j);
-			o1[d] = node_off(G, d, j + 1);
-		}
-		if (V3D) {
-			// puDistr3D1: weights (xc*yc)*zc etc. (pusher.c:550-565)
-			double xc = comp[0], yc = comp[1], zc = comp[2];
-			double x = dec[0], y = dec[1], z = dec[2];
-			unsafeAtomicAdd(&rho[o0[0] + o0[1] + o0[2]], xc * yc * zc);
-			unsafeAtomicAdd(&rho[o1[0] + o0[1] + o0[2]], x * yc * zc);
-			unsafeAtomicAdd(&rho[o0[0] + o1[1] + o0[2]], xc * y * zc);
-			unsafeAtomicAdd(&rho[o1[0] + o1[1] + o0[2]], x * y * zc);
-			unsafeAtomicAdd(&rho[o0[0] + o0[1] + o1[2]], xc * yc * z);
-			unsafeAtomicAdd(&rho[o1[0] + o0[1] + o1[2]], x * yc * z);
-			unsafeAtomicAdd(&rho[o0[0] + o1[1] + o1[2]], xc * y * z);
-			unsafeAtomicAdd(&rho[o1[0] + o1[1] + o1[2]], x * y * z);
-		} else {
-			// puDistrND1Inner: factor of the outer dims, then comp/dec of x
-			// (pusher.c:626-638): w = c_x*(c_y*(c_z*1))
+		for (int c = 0; c < (1 << ND); c++) {
+			double f = 1.0;
 #pragma unroll
-			for (int c = 0; c < (1 << ND); c++) {
-				double f = 1.0;
-				long off = 0;
-#pragma unroll
-				for (int d = ND - 1; d >= 1; d--) {
-					int b = (c >> d) & 1;
-					f = (b ? dec[d] : comp[d]) * f;
-					off += b ? o1[d] : o0[d];
-				}
-				int b0 = c & 1;
-				double wgt = (b0 ? dec[0] : comp[0]) * f;
-				off += b0 ? o1[0] : o0[0];
-				unsafeAtomicAdd(&rho[off], wgt);
-			}
+			for (int d = ND - 1; d >= 1; d--) f = (((c >> d) & 1) ? dec[d] : comp[d]) * f;
+			w[c] = ((c & 1) ? dec[0] : comp[0]) * f;
 		}
 	}
 }
 
+// global offset of padded node (j[0]+c0, j[1]+c1, ...) for corner c
+template <int ND>
+__device__ __forceinline__ long corner_off(const Geo &G, const int *j, int c) {
+	long off = 0;
+#pragma unroll
+	for (int d = 0; d < ND; d++) off += node_off(G, d, j[d] + ((c >> d) & 1));
+	return off;
+}
+
+template <int ND, bool V3D>
+__global__ __launch_bounds__(kThreads) void k_deposit_tiled(const double *__restrict__ x0,
+                                                            const double *__restrict__ x1,
+                                                            const double *__restrict__ x2, long b0,
+                                                            long n, pinc_geom_t g,
+                                                            double *__restrict__ rho) {
+	constexpr int NC = 1 << ND;
+	__shared__ double acc[kDepCap];
+	__shared__ int red[2 * 3 * (kThreads / 64)];
+	__shared__ int box[7];
+	Geo G = make_geo(g);
+	const double *xs[3] = {x0, x1, x2};
+	const long end = b0 + n;
+	const long i0 = (b0 & ~1L) + (long)blockIdx.x * kDepChunk + (long)threadIdx.x * kDepItems;
+	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+
+	// load this thread's particles (pairs of 16 B, 16-B aligned by i0)
+	double p[3][kDepItems];
+	unsigned valid = 0;
+#pragma unroll
+	for (int k = 0; k < kDepItems; k++) {
+		long i = i0 + k;
+		valid |= (unsigned)(i >= b0 && i < end) << k;
+	}
+#pragma unroll
+	for (int d = 0; d < ND; d++) {
+#pragma unroll
+		for (int k = 0; k < kDepItems; k += 2) {
+			long i = i0 + k;
+			if (((valid >> k) & 3u) == 3u) {
+				double2 v = *reinterpret_cast<const double2 *>(xs[d] + i);
+				p[d][k] = v.x;
+				p[d][k + 1] = v.y;
+			} else {
+				p[d][k] = ((valid >> k) & 1u) ? xs[d][i] : 0.0;
+				p[d][k + 1] = ((valid >> (k + 1)) & 1u) ? xs[d][i + 1] : 0.0;
+			}
+		}
+	}
+
+	// bounding box of the chunk's cells (j .. j+1 per dimension)
+	int lo[3] = {INT32_MAX, INT32_MAX, INT32_MAX}, hi[3] = {INT32_MIN, INT32_MIN, INT32_MIN};
+#pragma unroll
+	for (int k = 0; k < kDepItems; k++) {
+		if ((valid >> k) & 1u) {
+#pragma unroll
+			for (int d = 0; d < ND; d++) {
+				int j = (int)p[d][k];
+				lo[d] = min(lo[d], j);
+				hi[d] = max(hi[d], j + 1);
+			}
+		}
+	}
+#pragma unroll
+	for (int d = 0; d < ND; d++) {
+		int a = wave_min_i(lo[d]), b = wave_max_i(hi[d]);
+		if (lane == 0) {
+			red[(2 * d) * (kThreads / 64) + wv] = a;
+			red[(2 * d + 1) * (kThreads / 64) + wv] = b;
+		}
+	}
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		long vol = 1;
+		for (int d = 0; d < ND; d++) {
+			int a = INT32_MAX, b = INT32_MIN;
+			for (int w = 0; w < kThreads / 64; w++) {
+				a = min(a, red[(2 * d) * (kThreads / 64) + w]);
+				b = max(b, red[(2 * d + 1) * (kThreads / 64) + w]);
+			}
+			box[d] = a;
+			box[3 + d] = b - a + 1;
+			vol *= (long)(b - a + 1);
+		}
+		box[6] = (vol <= kDepCap && vol > 0) ? (int)vol : 0;
+	}
+	__syncthreads();
+	const int vol = box[6];
+
+	if (vol == 0) {
+		// scattered chunk: runs of equal cells, global atomics
+		int cj[3] = {0, 0, 0};
+		bool have = false;
+		double a[NC];
+#pragma unroll
+		for (int k = 0; k < kDepItems; k++) {
+			if (!((valid >> k) & 1u)) continue;
+			double dec[3], comp[3], w[NC];
+			int j[3];
+			bool same = have;
+#pragma unroll
+			for (int d = 0; d < ND; d++) {
+				j[d] = (int)p[d][k];
+				dec[d] = p[d][k] - j[d];
+				comp[d] = 1 - dec[d];
+				same = same && (j[d] == cj[d]);
+			}
+			cic_weights<ND, V3D>(dec, comp, w);
+			if (same) {
+#pragma unroll
+				for (int c = 0; c < NC; c++) a[c] += w[c];
+			} else {
+				if (have) {
+#pragma unroll
+					for (int c = 0; c < NC; c++) unsafeAtomicAdd(&rho[corner_off<ND>(G, cj, c)], a[c]);
+				}
+#pragma unroll
+				for (int c = 0; c < NC; c++) a[c] = w[c];
+#pragma unroll
+				for (int d = 0; d < ND; d++) cj[d] = j[d];
+				have = true;
+			}
+		}
+		if (have) {
+#pragma unroll
+			for (int c = 0; c < NC; c++) unsafeAtomicAdd(&rho[corner_off<ND>(G, cj, c)], a[c]);
+		}
+		return;
+	}
+
+	int blo[3] = {0, 0, 0}, st[3] = {0, 0, 0}, bn[3] = {1, 1, 1};
+	{
+		int sz = 1;
+#pragma unroll
+		for (int d = 0; d < ND; d++) {
+			blo[d] = box[d];
+			bn[d] = box[3 + d];
+			st[d] = sz;
+			sz *= bn[d];
+		}
+	}
+	int coff[NC];
+#pragma unroll
+	for (int c = 0; c < NC; c++) {
+		coff[c] = 0;
+#pragma unroll
+		for (int d = 0; d < ND; d++) coff[c] += ((c >> d) & 1) ? st[d] : 0;
+	}
+	for (int t = threadIdx.x; t < vol; t += kThreads) acc[t] = 0.0;
+	__syncthreads();
+
+	{
+		int cur = -1;
+		double a[NC];
+#pragma unroll
+		for (int k = 0; k < kDepItems; k++) {
+			if (!((valid >> k) & 1u)) continue;
+			double dec[3], comp[3], w[NC];
+			int l0 = 0;
+#pragma unroll
+			for (int d = 0; d < ND; d++) {
+				int j = (int)p[d][k];
+				dec[d] = p[d][k] - j;
+				comp[d] = 1 - dec[d];
+				l0 += (j - blo[d]) * st[d];
+			}
+			cic_weights<ND, V3D>(dec, comp, w);
+			if (l0 == cur) {
+#pragma unroll
+				for (int c = 0; c < NC; c++) a[c] += w[c];
+			} else {
+				if (cur >= 0) {
+#pragma unroll
+					for (int c = 0; c < NC; c++) atomicAdd(&acc[cur + coff[c]], a[c]);
+				}
+#pragma unroll
+				for (int c = 0; c < NC; c++) a[c] = w[c];
+				cur = l0;
+			}
+		}
+		if (cur >= 0) {
+#pragma unroll
+			for (int c = 0; c < NC; c++) atomicAdd(&acc[cur + coff[c]], a[c]);
+		}
+	}
+	__syncthreads();
+
+	// flush: one global atomic per touched node
+	for (int t = threadIdx.x; t < vol; t += kThreads) {
+		double v = acc[t];
+		if (v == 0.0) continue;
+		int r = t;
+		long off = 0;
+#pragma unroll
+		for (int d = 0; d < ND; d++) {
+			int c = r % bn[d];
+			r /= bn[d];
+			off += node_off(G, d, blo[d] + c);
+		}
+		unsafeAtomicAdd(&rho[off], v);
+	}
+}
+
 // ------------------------------------------------------- accelerate -------
+// puAcc3D1KE / puAccND1KE.  The reference rescales the whole E grid per
+// species (gMul(E,q/m) ... gMul(E,m/q), pusher.c:192,212); k_field_chain
+// materialises E as it stands while species s is pushed (same rounding
+// chain), so the particle kernel gathers plain values.  Each thread owns
+// kAccItems consecutive particles (16-B loads/stores per pair) and reuses the
+// gathered corner values while consecutive particles stay in one cell.
 constexpr int kAccItems = 8;
 constexpr int kAccChunk = kThreads * kAccItems;
 
-__device__ __forceinline__ double chain(double e, double pre, const double *qm, const double *mq,
-                                        int s) {
-	double v = e * pre;
-	for (int t = 0; t < s; t++) v = (v * qm[t]) * mq[t];
-	return v * qm[s];
+__global__ void k_field_chain(const double *__restrict__ E, double *__restrict__ Es, long n,
+                              const double *__restrict__ qm, const double *__restrict__ mq,
+                              double pre, int s) {
+	for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+		double v = E[i] * pre;
+		for (int t = 0; t < s; t++) v = (v * qm[t]) * mq[t];
+		Es[i] = v * qm[s];
+	}
 }
 
 template <int ND, bool V3D, bool KE>
@@ -419,90 +630,119 @@ __global__ __launch_bounds__(kThreads) void k_accel(const double *__restrict__ x
                                                     const double *__restrict__ x1,
                                                     const double *__restrict__ x2,
                                                     double *__restrict__ v0, double *__restrict__ v1,
-                                                    double *__restrict__ v2, long n, pinc_geom_t g,
-                                                    const double *__restrict__ E, int s,
-                                                    const double *__restrict__ qmArr,
-                                                    const double *__restrict__ mqArr, double pre,
+                                                    double *__restrict__ v2, long b0, long n,
+                                                    pinc_geom_t g, const double *__restrict__ E,
                                                     double *__restrict__ kePartial) {
+	constexpr int NC = 1 << ND;
 	__shared__ double red[kThreads / 64];
-	__shared__ double sqm[PINC_MAX_SPECIES], smq[PINC_MAX_SPECIES];
-	if (threadIdx.x < PINC_MAX_SPECIES) {
-		sqm[threadIdx.x] = qmArr[threadIdx.x];
-		smq[threadIdx.x] = mqArr[threadIdx.x];
-	}
-	__syncthreads();
 	Geo G = make_geo(g);
 	const double *xs[3] = {x0, x1, x2};
 	double *vs[3] = {v0, v1, v2};
+	const long end = b0 + n;
+	const long i0 = (b0 & ~1L) + (long)blockIdx.x * kAccChunk + (long)threadIdx.x * kAccItems;
 	double ke = 0.;
-	long base = (long)blockIdx.x * kAccChunk;
-	for (int k = 0; k < kAccItems; k++) {
-		long i = base + k * kThreads + threadIdx.x;
-		if (i >= n) break;
-		double dec[3], comp[3];
-		long o0[3], o1[3];
+	int cj[3] = {INT32_MIN, INT32_MIN, INT32_MIN};
+	double e[NC][ND];  // corner values of the current cell
+#pragma unroll
+	for (int k = 0; k < kAccItems; k += 2) {
+		double p[3][2], v[3][2];
+		bool ok[2];
+		ok[0] = (i0 + k >= b0) && (i0 + k < end);
+		ok[1] = (i0 + k + 1 >= b0) && (i0 + k + 1 < end);
+		if (!ok[0] && !ok[1]) continue;
 #pragma unroll
 		for (int d = 0; d < ND; d++) {
-			double p = xs[d][i];
-			int j = (int)p;
-			dec[d] = p - j;
-			comp[d] = 1 - dec[d];
-			o0[d] = node_off(G, d, j) * ND;
-			o1[d] = node_off(G, d, j + 1) * ND;
-		}
-		double dv[ND];
-		if (V3D) {
-			double x = dec[0], y = dec[1], z = dec[2];
-			double xc = comp[0], yc = comp[1], zc = comp[2];
-			long p000 = o0[0] + o0[1] + o0[2], p100 = o1[0] + o0[1] + o0[2];
-			long p010 = o0[0] + o1[1] + o0[2], p110 = o1[0] + o1[1] + o0[2];
-			long p001 = o0[0] + o0[1] + o1[2], p101 = o1[0] + o0[1] + o1[2];
-			long p011 = o0[0] + o1[1] + o1[2], p111 = o1[0] + o1[1] + o1[2];
-#pragma unroll
-			for (int v = 0; v < ND; v++) {
-				double e000 = chain(E[p000 + v], pre, sqm, smq, s);
-				double e100 = chain(E[p100 + v], pre, sqm, smq, s);
-				double e010 = chain(E[p010 + v], pre, sqm, smq, s);
-				double e110 = chain(E[p110 + v], pre, sqm, smq, s);
-				double e001 = chain(E[p001 + v], pre, sqm, smq, s);
-				double e101 = chain(E[p101 + v], pre, sqm, smq, s);
-				double e011 = chain(E[p011 + v], pre, sqm, smq, s);
-				double e111 = chain(E[p111 + v], pre, sqm, smq, s);
-				dv[v] = zc * (yc * (xc * e000 + x * e100) + y * (xc * e010 + x * e110)) +
-				        z * (yc * (xc * e001 + x * e101) + y * (xc * e011 + x * e111));
-			}
-		} else {
-			// puInterpND1Inner: result accumulated corner by corner in the
-			// recursion order (outer dims first), (c_x*f)*val
-#pragma unroll
-			for (int v = 0; v < ND; v++) dv[v] = 0;
-#pragma unroll
-			for (int c = 0; c < (1 << (ND - 1)); c++) {
-				double f = 1.0;
-				long off = 0;
-#pragma unroll
-				for (int d = ND - 1; d >= 1; d--) {
-					int b = (c >> (d - 1)) & 1;
-					f = (b ? dec[d] : comp[d]) * f;
-					off += b ? o1[d] : o0[d];
-				}
-#pragma unroll
-				for (int v = 0; v < ND; v++) {
-					double ea = chain(E[off + o0[0] + v], pre, sqm, smq, s);
-					double eb = chain(E[off + o1[0] + v], pre, sqm, smq, s);
-					dv[v] += comp[0] * f * ea;
-					dv[v] += dec[0] * f * eb;
-				}
+			if (ok[0] && ok[1]) {
+				double2 a = *reinterpret_cast<const double2 *>(xs[d] + i0 + k);
+				double2 b = *reinterpret_cast<const double2 *>(vs[d] + i0 + k);
+				p[d][0] = a.x;
+				p[d][1] = a.y;
+				v[d][0] = b.x;
+				v[d][1] = b.y;
+			} else {
+				long i = ok[0] ? i0 + k : i0 + k + 1;
+				int h = ok[0] ? 0 : 1;
+				p[d][h] = xs[d][i];
+				v[d][h] = vs[d][i];
+				p[d][1 - h] = p[d][h];
+				v[d][1 - h] = v[d][h];
 			}
 		}
-		double vsq = 0;
+#pragma unroll
+		for (int h = 0; h < 2; h++) {
+			if (!ok[h]) continue;
+			double dec[3], comp[3];
+			int j[3];
+			bool same = true;
+#pragma unroll
+			for (int d = 0; d < ND; d++) {
+				j[d] = (int)p[d][h];
+				dec[d] = p[d][h] - j[d];
+				comp[d] = 1 - dec[d];
+				same = same && (j[d] == cj[d]);
+			}
+			if (!same) {
+#pragma unroll
+				for (int c = 0; c < NC; c++) {
+					long off = 0;
+#pragma unroll
+					for (int d = 0; d < ND; d++) off += node_off(G, d, j[d] + ((c >> d) & 1));
+					off *= ND;
+#pragma unroll
+					for (int q = 0; q < ND; q++) e[c][q] = E[off + q];
+				}
+#pragma unroll
+				for (int d = 0; d < ND; d++) cj[d] = j[d];
+			}
+			double dv[ND];
+			if (V3D) {
+				// puInterp3D1 (pusher.c:1116-1120), corner c = x + 2y + 4z
+				double x = dec[0], y = dec[1], z = dec[2];
+				double xc = comp[0], yc = comp[1], zc = comp[2];
+#pragma unroll
+				for (int q = 0; q < ND; q++)
+					dv[q] = zc * (yc * (xc * e[0][q] + x * e[1][q]) + y * (xc * e[2][q] + x * e[3][q])) +
+					        z * (yc * (xc * e[4][q] + x * e[5][q]) + y * (xc * e[6][q] + x * e[7][q]));
+			} else {
+				// puInterpND1Inner: corner by corner in the recursion order
+				// (outer dims first), (c_x*f)*val
+#pragma unroll
+				for (int q = 0; q < ND; q++) dv[q] = 0;
+#pragma unroll
+				for (int c = 0; c < (1 << (ND - 1)); c++) {
+					double f = 1.0;
+					int cc = 0;
+#pragma unroll
+					for (int d = ND - 1; d >= 1; d--) {
+						int bit = (c >> (d - 1)) & 1;
+						f = (bit ? dec[d] : comp[d]) * f;
+						cc |= bit << d;
+					}
+#pragma unroll
+					for (int q = 0; q < ND; q++) {
+						dv[q] += comp[0] * f * e[cc][q];
+						dv[q] += dec[0] * f * e[cc | 1][q];
+					}
+				}
+			}
+			double vsq = 0;
+#pragma unroll
+			for (int d = 0; d < ND; d++) {
+				double vv = v[d][h];
+				vsq += vv * (vv + dv[d]);
+				v[d][h] = vv + dv[d];
+			}
+			ke += vsq;
+		}
 #pragma unroll
 		for (int d = 0; d < ND; d++) {
-			double v = vs[d][i];
-			vsq += v * (v + dv[d]);
-			vs[d][i] = v + dv[d];
+			if (ok[0] && ok[1]) {
+				*reinterpret_cast<double2 *>(vs[d] + i0 + k) = make_double2(v[d][0], v[d][1]);
+			} else {
+				if (ok[0]) vs[d][i0 + k] = v[d][0];
+				if (ok[1]) vs[d][i0 + k + 1] = v[d][1];
+			}
 		}
-		ke += vsq;
 	}
 	if (KE) {
 		double t = block_sum(ke, red);
@@ -722,46 +962,50 @@ extern "C" int pinc_hip_deposit(pinc_pop_t pop, int s, pinc_geom_t g, double *rh
 	long n = pop.iStop[s] - pop.iStart[s];
 	if (n <= 0) return 0;
 	long b0 = pop.iStart[s];
-	long nb = ceil_div(n, kThreads * 4);
-	if (nb > 65536L * 4) nb = 65536L * 4;
+	// chunks start at the even index at or below b0 (16-B aligned pairs)
+	long nb = ceil_div(n + (b0 & 1L), (long)kDepChunk);
 	hipStream_t st = (hipStream_t)stream;
-	const double *x0 = pop.x[0] + b0;
-	const double *x1 = g.nd > 1 ? pop.x[1] + b0 : nullptr;
-	const double *x2 = g.nd > 2 ? pop.x[2] + b0 : nullptr;
+	const double *x0 = pop.x[0];
+	const double *x1 = g.nd > 1 ? pop.x[1] : nullptr;
+	const double *x2 = g.nd > 2 ? pop.x[2] : nullptr;
 	if (g.nd == 3)
-		hipLaunchKernelGGL((k_deposit<3, true>), dim3(nb), dim3(kThreads), 0, st, x0, x1, x2, n, g, rho);
+		hipLaunchKernelGGL((k_deposit_tiled<3, true>), dim3(nb), dim3(kThreads), 0, st, x0, x1, x2, b0, n, g, rho);
 	else if (g.nd == 2)
-		hipLaunchKernelGGL((k_deposit<2, false>), dim3(nb), dim3(kThreads), 0, st, x0, x1, x2, n, g, rho);
+		hipLaunchKernelGGL((k_deposit_tiled<2, false>), dim3(nb), dim3(kThreads), 0, st, x0, x1, x2, b0, n, g, rho);
 	else
-		hipLaunchKernelGGL((k_deposit<1, false>), dim3(nb), dim3(kThreads), 0, st, x0, x1, x2, n, g, rho);
+		hipLaunchKernelGGL((k_deposit_tiled<1, false>), dim3(nb), dim3(kThreads), 0, st, x0, x1, x2, b0, n, g, rho);
 	return check_launch("deposit");
 }
 
-extern "C" int pinc_hip_accelerate(pinc_pop_t pop, int s, pinc_geom_t g, const double *E,
-                                   const double *qm, const double *mq, double pre,
+extern "C" int pinc_hip_field_chain(const double *E, double *Es, long n, const double *qm,
+                                    const double *mq, double pre, int s, void *stream) {
+	if (n <= 0) return 0;
+	long nb = ceil_div(n, (long)kThreads * 4);
+	if (nb > 8192) nb = 8192;
+	hipLaunchKernelGGL(k_field_chain, dim3(nb), dim3(kThreads), 0, (hipStream_t)stream, E, Es, n, qm, mq, pre, s);
+	return check_launch("field chain");
+}
+
+extern "C" int pinc_hip_accelerate(pinc_pop_t pop, int s, pinc_geom_t g, const double *Es,
                                    double *kePartial, int *nBlocks, void *stream) {
 	long n = pop.iStop[s] - pop.iStart[s];
 	*nBlocks = 0;
 	if (n <= 0) return 0;
 	long b0 = pop.iStart[s];
-	long nb = ceil_div(n, kAccChunk);
+	long nb = ceil_div(n + (b0 & 1L), (long)kAccChunk);
 	*nBlocks = (int)nb;
 	hipStream_t st = (hipStream_t)stream;
-	const double *x0 = pop.x[0] + b0;
-	const double *x1 = g.nd > 1 ? pop.x[1] + b0 : nullptr;
-	const double *x2 = g.nd > 2 ? pop.x[2] + b0 : nullptr;
-	double *v0 = pop.v[0] + b0;
-	double *v1 = g.nd > 1 ? pop.v[1] + b0 : nullptr;
-	double *v2 = g.nd > 2 ? pop.v[2] + b0 : nullptr;
+	double *x0 = pop.x[0], *x1 = pop.x[1], *x2 = pop.x[2];
+	double *v0 = pop.v[0], *v1 = pop.v[1], *v2 = pop.v[2];
 	if (g.nd == 3)
-		hipLaunchKernelGGL((k_accel<3, true, true>), dim3(nb), dim3(kThreads), 0, st, x0, x1, x2, v0,
-		                   v1, v2, n, g, E, s, qm, mq, pre, kePartial);
+		hipLaunchKernelGGL((k_accel<3, true, true>), dim3(nb), dim3(kThreads), 0, st, x0, x1, x2, v0, v1, v2, b0, n,
+		                   g, Es, kePartial);
 	else if (g.nd == 2)
-		hipLaunchKernelGGL((k_accel<2, false, true>), dim3(nb), dim3(kThreads), 0, st, x0, x1, x2,
-		                   v0, v1, v2, n, g, E, s, qm, mq, pre, kePartial);
+		hipLaunchKernelGGL((k_accel<2, false, true>), dim3(nb), dim3(kThreads), 0, st, x0, x1, x2, v0, v1, v2, b0,
+		                   n, g, Es, kePartial);
 	else
-		hipLaunchKernelGGL((k_accel<1, false, true>), dim3(nb), dim3(kThreads), 0, st, x0, x1, x2,
-		                   v0, v1, v2, n, g, E, s, qm, mq, pre, kePartial);
+		hipLaunchKernelGGL((k_accel<1, false, true>), dim3(nb), dim3(kThreads), 0, st, x0, x1, x2, v0, v1, v2, b0,
+		                   n, g, Es, kePartial);
 	return check_launch("accelerate");
 }
 

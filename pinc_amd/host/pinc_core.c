@@ -475,7 +475,6 @@ void pinc_ctx_require(void) {
 	pinc_check(pinc_hip_malloc((void **)&g_pinc.dErr, 64), "err word");
 	pinc_check(pinc_hip_memset(g_pinc.dErr, 0, 64, g_pinc.stream), "err word");
 	if (g_pinc.nranks < 1) g_pinc.nranks = 1;
-	g_pinc.probeKernel = -1;
 	g_pinc.verbose = getenv("PINC_VERBOSE") ? atoi(getenv("PINC_VERBOSE")) : 0;
 	for (int i = 0; i < 2 * PINC_NPHASES; i++) pinc_check(pinc_hip_event_create(&g_pinc.ev[i]), "event");
 	g_pinc.initialised = 1;
@@ -497,51 +496,67 @@ void pinc_phase_end(int p) {
 }
 
 /* ------------------------------------------------------------- probe -- */
+static void probe_release(void) {
+	for (int k = 0; k < PINC_NPROBES; k++) {
+		if (g_pinc.probeEv[k]) {
+			for (int i = 0; i < 2 * g_pinc.probeMax; i++) pinc_hip_event_destroy(g_pinc.probeEv[k][i]);
+			free(g_pinc.probeEv[k]);
+			free(g_pinc.probeBytes[k]);
+		}
+		g_pinc.probeEv[k] = NULL;
+		g_pinc.probeBytes[k] = NULL;
+		g_pinc.probeOn[k] = 0;
+		g_pinc.probeN[k] = 0;
+		g_pinc.probeLaunches[k] = 0;
+	}
+}
+
 int pinc_probe_start(int kernel, int maxSamples) {
 	pinc_ctx_require();
-	if (g_pinc.probeEv) {
-		for (int i = 0; i < 2 * g_pinc.probeMax; i++) pinc_hip_event_destroy(g_pinc.probeEv[i]);
-		free(g_pinc.probeEv);
-		free(g_pinc.probeBytes);
-	}
-	g_pinc.probeKernel = kernel;
+	if (kernel < PINC_PROBE_ALL || kernel >= PINC_NPROBES || maxSamples < 1) return 1;
+	probe_release();
 	g_pinc.probeMax = maxSamples;
-	g_pinc.probeN = 0;
-	g_pinc.probeLaunches = 0;
-	g_pinc.probeEv = calloc(2 * maxSamples, sizeof(void *));
-	g_pinc.probeBytes = calloc(maxSamples, sizeof(double));
-	for (int i = 0; i < 2 * maxSamples; i++) pinc_check(pinc_hip_event_create(&g_pinc.probeEv[i]), "probe event");
+	for (int k = 0; k < PINC_NPROBES; k++) {
+		if (kernel != PINC_PROBE_ALL && kernel != k) continue;
+		g_pinc.probeOn[k] = 1;
+		g_pinc.probeEv[k] = calloc(2 * maxSamples, sizeof(void *));
+		g_pinc.probeBytes[k] = calloc(maxSamples, sizeof(double));
+		for (int i = 0; i < 2 * maxSamples; i++)
+			pinc_check(pinc_hip_event_create(&g_pinc.probeEv[k][i]), "probe event");
+	}
 	return 0;
 }
 
 int pinc_probe_begin(int k) {
-	if (!g_pinc.probeEv || k != g_pinc.probeKernel) return -1;
-	g_pinc.probeLaunches++;
-	if (g_pinc.probeN >= g_pinc.probeMax) return -1;
-	int slot = g_pinc.probeN++;
-	pinc_check(pinc_hip_event_record(g_pinc.probeEv[2 * slot], g_pinc.stream), "probe");
+	if (!g_pinc.probeOn[k]) return -1;
+	g_pinc.probeLaunches[k]++;
+	if (g_pinc.probeN[k] >= g_pinc.probeMax) return -1;
+	int slot = g_pinc.probeN[k]++;
+	pinc_check(pinc_hip_event_record(g_pinc.probeEv[k][2 * slot], g_pinc.stream), "probe");
 	return slot;
 }
 
 void pinc_probe_end(int k, int slot, double bytes) {
-	if (slot < 0 || k != g_pinc.probeKernel) return;
-	pinc_check(pinc_hip_event_record(g_pinc.probeEv[2 * slot + 1], g_pinc.stream), "probe");
-	g_pinc.probeBytes[slot] = bytes;
+	if (slot < 0 || !g_pinc.probeOn[k]) return;
+	pinc_check(pinc_hip_event_record(g_pinc.probeEv[k][2 * slot + 1], g_pinc.stream), "probe");
+	g_pinc.probeBytes[k][slot] = bytes;
 }
 
-int pinc_probe_read(double *meanMs, double *meanBytes, int *samples, long *launches) {
+int pinc_probe_read(int k, double *meanMs, double *meanBytes, int *samples, long *launches) {
+	if (k < 0 || k >= PINC_NPROBES) return 1;
 	double t = 0, b = 0;
-	int n = g_pinc.probeN;
+	int n = g_pinc.probeOn[k] ? g_pinc.probeN[k] : 0;
 	for (int i = 0; i < n; i++) {
 		float ms = 0;
-		pinc_check(pinc_hip_event_elapsed(&ms, g_pinc.probeEv[2 * i], g_pinc.probeEv[2 * i + 1]), "probe read");
+		pinc_check(pinc_hip_event_elapsed(&ms, g_pinc.probeEv[k][2 * i], g_pinc.probeEv[k][2 * i + 1]),
+		           "probe read");
 		t += ms;
-		b += g_pinc.probeBytes[i];
+		b += g_pinc.probeBytes[k][i];
 	}
 	*meanMs = n ? t / n : 0;
 	*meanBytes = n ? b / n : 0;
 	*samples = n;
-	*launches = g_pinc.probeLaunches;
+	*launches = g_pinc.probeLaunches[k];
 	return 0;
 }
 

@@ -150,6 +150,7 @@ void gFree(Grid *g) {
 		if (g->dev->ownsGlobal) pinc_hip_free(g->dev->global);
 		pinc_hip_free(g->dev->recv[0]);
 		pinc_hip_free(g->dev->recv[1]);
+		pinc_hip_free(g->dev->scaled);
 		free(g->dev);
 	}
 	free(g->val);

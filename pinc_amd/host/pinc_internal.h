@@ -33,11 +33,11 @@ typedef struct {
 	int phaseOpen[PINC_NPHASES];
 	/* kernel probe: HIP events around launches of one kernel, read lazily
 	 * (no host synchronisation inside the timed region) */
-	int probeKernel;          /* PINC_PROBE_* or -1 */
-	int probeMax, probeN;     /* capacity, recorded pairs */
-	void **probeEv;           /* 2*probeMax events */
-	double *probeBytes;       /* algorithmic bytes of each recorded launch */
-	long probeLaunches;       /* launches seen (recorded or not) */
+	int probeOn[PINC_NPROBES];      /* kernel probed? */
+	int probeMax, probeN[PINC_NPROBES];  /* capacity, recorded pairs */
+	void **probeEv[PINC_NPROBES];   /* 2*probeMax events per kernel */
+	double *probeBytes[PINC_NPROBES]; /* algorithmic bytes of each recorded launch */
+	long probeLaunches[PINC_NPROBES]; /* launches seen (recorded or not) */
 } PincCtx;
 
 /* probe hooks around a launch of kernel k with algorithmic byte count b */
@@ -77,6 +77,7 @@ struct PincDevGrid {
 	int ownsGlobal;
 	int ghostsValid;    /* slab ghost planes already hold periodic images */
 	double *recv[2];    /* halo receive planes (multi-rank) */
+	double *scaled;     /* E as rescaled for the species being pushed (lazy) */
 };
 
 struct MultigridSolver {

@@ -159,6 +159,9 @@ static void smooth(MultigridSolver *S, int q, int nIter, int nd3) {
 
 static void vrec(MultigridSolver *S, int q) {
 	int bottom = S->nLevels - 1;
+	/* native mode: correction scheme, each coarse visit solves for the
+	 * correction from zero (the reference warm-starts coarse phi) */
+	if (S->native && q > 0) pinc_check(pinc_hip_zero(S->phi[q], S->N[q], g_pinc.stream), "native zero");
 	if (q == bottom) {
 		neutralize(S->rho[q], S->N[q]);
 		smooth(S, q, S->nCoarse, S->coarse3d);
@@ -189,7 +192,11 @@ void mgSolve(MultigridSolver *S, Grid *rho, Grid *phi, const MpiInfo *mpiInfo) {
 		           "gather rho");
 	}
 	if (S->nLevels > 1) {
-		const long maxCycles = 1000000; /* the reference loops forever (multigrid.c:1698) */
+		/* the reference loops until converged (multigrid.c:1698); PINC_MG_MAX_CYCLES
+		 * caps a solve for diagnostics (stops with a warning) */
+		const long maxCycles = 1000000;
+		const char *capEnv = getenv("PINC_MG_MAX_CYCLES");
+		long cap = capEnv ? atol(capEnv) : 0;
 		double barRes = 2.;
 		long c = 0;
 		while (barRes > 1.E-10) {
@@ -208,6 +215,11 @@ void mgSolve(MultigridSolver *S, Grid *rho, Grid *phi, const MpiInfo *mpiInfo) {
 			if (g_pinc.verbose && (c % g_pinc.verbose == 0)) {
 				fprintf(stderr, "[pinc] rank %d solve cycle %ld residual %.3e\n", g_pinc.rank, c, barRes);
 				fflush(stderr);
+			}
+			if (cap > 0 && c >= cap) {
+				fprintf(stderr, "[pinc] rank %d solve stopped at the PINC_MG_MAX_CYCLES cap (%ld), residual %.3e\n",
+				        g_pinc.rank, c, barRes);
+				break;
 			}
 		}
 	} else {

@@ -305,9 +305,13 @@ static void acc(Population *pop, Grid *E, int ke) {
 	int ns = pop->nSpecies;
 	for (int s = 0; s < ns; s++) {
 		int nb = 0;
+		PincDevGrid *eg = E->dev;
+		if (!eg->scaled)
+			pinc_check(pinc_hip_malloc((void **)&eg->scaled, eg->n * sizeof(double)), "E scaled");
+		pinc_check(pinc_hip_field_chain(eg->d, eg->scaled, eg->n, dv->qm, dv->mq, 1.0, s, g_pinc.stream),
+		           "E chain");
 		int slot = pinc_probe_begin(PINC_PROBE_ACCEL);
-		pinc_check(pinc_hip_accelerate(p, s, E->dev->geom, E->dev->d, dv->qm, dv->mq, 1.0, dv->kePartial, &nb,
-		                               g_pinc.stream),
+		pinc_check(pinc_hip_accelerate(p, s, eg->geom, eg->scaled, dv->kePartial, &nb, g_pinc.stream),
 		           "accelerate");
 		/* read pos+vel, write vel (72 B per 3-D particle) + read E once */
 		pinc_probe_end(PINC_PROBE_ACCEL, slot,

@@ -131,3 +131,71 @@ def test_reference_known_values(sim_cls):
         ke, pe, _ = s.energy()
     assert abs(ke - 0.97536794508303382) < 1e-9
     assert abs(pe - 32.140625756280251) < 1e-7
+
+
+@pytest.mark.parametrize("name,kw", [("cold3d", {}), ("warm", {"true_size": (32, 32, 32), "ppc": 8,
+                                                               "nalloc_pc": 16, "levels": 3})])
+def test_native_mg_same_solution(sim_cls, name, kw):
+    """multigrid:native=1 (correction scheme with the coarse h^2 factor; not
+    the reference's algorithm) solves the same discrete problem: phi agrees
+    with the oracle's reference-algorithm solution to within what the
+    1e-10 RMS-residual stop allows, in a handful of V-cycles."""
+    cfg = configs.config(name, **kw)
+    maxwell = name == "warm"
+    ini_p = configs.write_ini(cfg)
+    cfg["multigrid"]["native"] = "1"
+    ini_n = configs.write_ini(cfg)
+    w = orc.World(ini_p)
+    w.init(perturb=not maxwell, maxwell=maxwell, seed=7)
+    w.init_fields()
+    w.step()
+    with sim_cls(ini_n, maxwell=maxwell, perturb=not maxwell, seed=7) as s:
+        s.init()
+        for sp in range(2):
+            po, vo, _ = w.particles(sp)
+            s.set_particles(sp, po, vo)
+        c0 = s.cycles
+        s.op("distr")
+        s.op("solve")
+        pg = s.grid(1)
+        cyc_native = s.cycles - c0
+    c0 = w.cycles
+    w.op("distr")
+    w.op("solve")
+    po = w.grid(1)
+    cyc_ref = w.cycles - c0
+    inner = (slice(1, -1),) * 3
+    err = _rel(pg[inner], po[inner])
+    assert err < 1e-6, err
+    assert cyc_native <= 12, (cyc_native, cyc_ref)
+
+
+@pytest.mark.parametrize("layout", ["sorted", "scattered", "mixed"])
+def test_deposit_layouts(sim_cls, layout):
+    """puDistr3D1 on particle orders that exercise both deposit paths: the
+    LDS-tiled one (spatially coherent chunks) and the global-atomic one
+    (chunks whose node box exceeds the LDS tile)."""
+    ini = _ini("cold3d")
+    w = orc.World(ini)
+    w.init()
+    rng = np.random.default_rng(11)
+    with sim_cls(ini) as s:
+        s.op("init_particles")
+        for sp in range(2):
+            po, vo, _ = w.particles(sp)
+            n = len(po)
+            lo, hi = 1.0, np.array([32.9, 16.9, 16.9])
+            pos = lo + rng.random((n, 3)) * (hi - lo)
+            if layout == "sorted":
+                pos = pos[np.lexsort((pos[:, 0], pos[:, 1], pos[:, 2]))]
+            elif layout == "mixed":
+                pos[: n // 2] = pos[: n // 2][np.lexsort((pos[: n // 2, 0], pos[: n // 2, 1], pos[: n // 2, 2]))]
+            s.set_particles(sp, pos, vo)
+            w.set_particles(sp, pos, vo)
+        s.op("distr")
+        w.op("distr")
+        rg, ro = s.grid(0), w.grid(0)
+        inner = (slice(1, -1),) * 3
+        q, _ = s.species()
+        ppc = s.count(0) / ro[inner].size
+        assert np.max(np.abs(rg[inner] - ro[inner])) < 1e-13 * abs(q[0]) * ppc * 8
