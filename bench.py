@@ -72,17 +72,21 @@ def _cpu_baseline(size: int, ppc: int, steps: int) -> dict:
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=8)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--size", type=int, default=256, help="global cells per dimension")
     ap.add_argument("--ppc", type=int, default=64)
     ap.add_argument("--mg", default="native", choices=["native", "reference"],
                     help="native: correction-scheme V-cycle with the coarse h^2 factor (default; the reference "
                          "algorithm does not converge at 256^3 with 5 levels, DESIGN.md section 6); reference: "
                          "the reference's mgVRecursive exactly")
+    ap.add_argument("--layout", default="tiled", choices=["tiled", "reference"],
+                    help="tiled: particles re-sorted by 4^3-cell tile every --sort-interval moves (default); "
+                         "reference: the reference's particle order (bit-exact indices)")
+    ap.add_argument("--sort-interval", type=int, default=4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-size", type=int, default=64)
-    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--cpu-steps", type=int, default=8)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -116,6 +120,9 @@ def main() -> int:
                          nalloc_pc=args.ppc + 8)
     if args.mg == "native":
         cfg["multigrid"]["native"] = "1"
+    if args.layout == "tiled":
+        cfg["population"]["layout"] = "tiled"
+        cfg["population"]["sortInterval"] = str(args.sort_interval)
     ini = configs.write_ini(cfg)
 
     def barrier():
@@ -214,6 +221,7 @@ def main() -> int:
             "species": 2,
             "particles": n_total,
             "decomposition": f"1,1,{world}",
+            "layout": args.layout + (f" (tile sort every {args.sort_interval} steps)" if args.layout == "tiled" else ""),
             "poisson": "multigrid mgVRecursive, 5 levels, RB Gauss-Seidel 10/10/10, "
                        + ("native mode (correction scheme, coarse h^2 factor)" if args.mg == "native"
                           else "reference algorithm (parity mode)"),

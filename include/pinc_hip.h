@@ -75,11 +75,22 @@ int pinc_hip_mem_info(unsigned long *freeBytes, unsigned long *totalBytes);
 /* puMove (pusher.c:86-119, as compiled: pos += vel) fused with the
  * neighbour classification of puExtractEmigrants3D/ND (pusher.c:782-910):
  * flags[i] = ne in 0..3^nd-1, center = stays.  chunkCount[b] = emigrants of
- * chunk b (PINC_CHUNK particles).  If doMove is 0 only classifies. */
+ * chunk b (PINC_CHUNK particles).  If doMove is 0 only classifies.
+ * thr = [lower(nd), upper(nd), size-1 (nd)] as MpiInfo.thresholds.
+ * wrapMask bit d (tiled layout only): a crossing in dimension d is applied in
+ * place with the import's periodic shift and does not count as emigration;
+ * 0 reproduces the reference exactly. */
 #define PINC_CHUNK 2048
 int pinc_hip_move_classify(pinc_pop_t pop, int s, int doMove, const double *thr,
                            unsigned char *flags, int *chunkCount, double maxVel,
-                           int *errFlag, void *stream);
+                           int *errFlag, int wrapMask, void *stream);
+
+/* Tiled layout (population:layout = tiled, not in the reference): counting
+ * sort of species s by tile of tileWidth^nd cells, from pop into out (same
+ * ranges); the caller swaps the two.  work holds 2*(nTiles+1) ints
+ * (workCap); nTilesOut returns nTiles.  Order within a tile is arbitrary. */
+int pinc_hip_sort_tiles(pinc_pop_t pop, pinc_pop_t out, int s, pinc_geom_t g, int tileWidth,
+                        int *work, long workCap, long *nTilesOut, void *stream);
 
 /* Emigrant extraction with the reference's back-fill order (pusher.c:
  * 782-855): survivors fill holes from the tail, emigrants are listed in the

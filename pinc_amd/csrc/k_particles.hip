@@ -21,6 +21,7 @@ namespace {
 
 struct Thr {
 	double lo[3], up[3], hi[3];
+	int T[3];  // true cells per dimension (local)
 };
 
 constexpr int kThreads = 256;
@@ -37,7 +38,7 @@ __global__ __launch_bounds__(kThreads) void k_move_classify(
 		const double *__restrict__ v0, const double *__restrict__ v1,
 		const double *__restrict__ v2, long n, int doMove, Thr thr, int center,
 		unsigned char *__restrict__ flags, int *__restrict__ chunkCount, double maxVel,
-		int *__restrict__ err) {
+		int *__restrict__ err, int wrapMask) {
 	__shared__ int wcnt[kThreads / 64];
 	double *xs[3] = {x0, x1, x2};
 	const double *vs[3] = {v0, v1, v2};
@@ -63,10 +64,19 @@ __global__ __launch_bounds__(kThreads) void k_move_classify(
 #pragma unroll
 		for (int d = ND - 1; d >= 0; d--) {
 			int dig = 1 - (p[d] < thr.lo[d]) + (p[d] >= thr.up[d]);
-			ne = ne * 3 + dig;
 			// pPosAssertInLocalFrame after the periodic shift (population.c:316-340)
 			double q = p[d] - (double)(dig - 1) * (thr.hi[d] - 1.0);
 			bad |= (q < 0.0 || q > thr.hi[d]) << 1;
+			if ((wrapMask >> d) & 1) {
+				// tiled layout: a crossing of a rank-local periodic boundary is
+				// applied in place with the import's shift (pusher.c:941-964)
+				if (dig != 1) {
+					p[d] = p[d] + (double)((1 - dig) * thr.T[d]);
+					xs[d][i] = p[d];
+				}
+				dig = 1;
+			}
+			ne = ne * 3 + dig;
 		}
 		flags[i] = (unsigned char)ne;
 		cnt += (ne != center);
@@ -351,16 +361,14 @@ __device__ __forceinline__ long node_off(const Geo &G, int d, int p) {
 }
 
 // --------------------------------------------- LDS-privatised deposit -----
-// One workgroup owns a chunk of kDepChunk consecutive particles; each thread
-// owns kDepItems consecutive ones (one 16-B load per pair and component).
-// Particles keep the reference's order, which stays spatially coherent
-// (lattice start, slow drift), so:
-//  * consecutive particles of one thread mostly share a cell: their eight
-//    weights are summed in registers and written once per run of equal
-//    cells, and lanes of one wave hit distinct nodes (no same-address LDS
-//    atomics inside an instruction);
-//  * the chunk covers a small box of nodes, accumulated in LDS (ds_add_f64)
-//    and flushed with one global atomic per touched node.
+// One workgroup owns a chunk of kDepChunk consecutive particles, loaded as
+// lane-contiguous 16-B pairs.  In either layout (the reference's order,
+// spatially coherent from the lattice start, or the tiled layout) a chunk
+// covers a small box of nodes:
+//  * the two particles of a pair often share a cell: their eight weights are
+//    summed in registers first;
+//  * the box is accumulated in LDS (ds_add_f64) and flushed with one global
+//    atomic per touched node.
 // Chunks whose box exceeds the LDS tile use the same run accumulation with
 // global atomics.  Weights are the reference's expressions (pusher.c:550-565,
 // 626-638); only the summation order differs from the serial loop.
@@ -425,22 +433,23 @@ __global__ __launch_bounds__(kThreads) void k_deposit_tiled(const double *__rest
 	Geo G = make_geo(g);
 	const double *xs[3] = {x0, x1, x2};
 	const long end = b0 + n;
-	const long i0 = (b0 & ~1L) + (long)blockIdx.x * kDepChunk + (long)threadIdx.x * kDepItems;
+	// item k of this thread: pair k/2 of the lane-contiguous pairs, so each
+	// 16-B load instruction of a wave covers 1 KiB of contiguous memory
+	const long cb = (b0 & ~1L) + (long)blockIdx.x * kDepChunk + 2L * threadIdx.x;
 	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 
-	// load this thread's particles (pairs of 16 B, 16-B aligned by i0)
 	double p[3][kDepItems];
 	unsigned valid = 0;
 #pragma unroll
 	for (int k = 0; k < kDepItems; k++) {
-		long i = i0 + k;
+		long i = cb + 2L * kThreads * (k >> 1) + (k & 1);
 		valid |= (unsigned)(i >= b0 && i < end) << k;
 	}
 #pragma unroll
 	for (int d = 0; d < ND; d++) {
 #pragma unroll
 		for (int k = 0; k < kDepItems; k += 2) {
-			long i = i0 + k;
+			long i = cb + 2L * kThreads * (k >> 1);
 			if (((valid >> k) & 3u) == 3u) {
 				double2 v = *reinterpret_cast<const double2 *>(xs[d] + i);
 				p[d][k] = v.x;
@@ -609,9 +618,9 @@ __global__ __launch_bounds__(kThreads) void k_deposit_tiled(const double *__rest
 // puAcc3D1KE / puAccND1KE.  The reference rescales the whole E grid per
 // species (gMul(E,q/m) ... gMul(E,m/q), pusher.c:192,212); k_field_chain
 // materialises E as it stands while species s is pushed (same rounding
-// chain), so the particle kernel gathers plain values.  Each thread owns
-// kAccItems consecutive particles (16-B loads/stores per pair) and reuses the
-// gathered corner values while consecutive particles stay in one cell.
+// chain), so the particle kernel gathers plain values.  Particles are loaded
+// and stored as lane-contiguous 16-B pairs; the gathered corner values are
+// reused while a thread's next particle stays in the same cell.
 constexpr int kAccItems = 8;
 constexpr int kAccChunk = kThreads * kAccItems;
 
@@ -639,7 +648,8 @@ __global__ __launch_bounds__(kThreads) void k_accel(const double *__restrict__ x
 	const double *xs[3] = {x0, x1, x2};
 	double *vs[3] = {v0, v1, v2};
 	const long end = b0 + n;
-	const long i0 = (b0 & ~1L) + (long)blockIdx.x * kAccChunk + (long)threadIdx.x * kAccItems;
+	// pair k/2 of the lane-contiguous pairs (1 KiB per wave load instruction)
+	const long cb = (b0 & ~1L) + (long)blockIdx.x * kAccChunk + 2L * threadIdx.x;
 	double ke = 0.;
 	int cj[3] = {INT32_MIN, INT32_MIN, INT32_MIN};
 	double e[NC][ND];  // corner values of the current cell
@@ -647,20 +657,20 @@ __global__ __launch_bounds__(kThreads) void k_accel(const double *__restrict__ x
 	for (int k = 0; k < kAccItems; k += 2) {
 		double p[3][2], v[3][2];
 		bool ok[2];
-		ok[0] = (i0 + k >= b0) && (i0 + k < end);
-		ok[1] = (i0 + k + 1 >= b0) && (i0 + k + 1 < end);
+		ok[0] = (cb + 2L * kThreads * (k >> 1) >= b0) && (cb + 2L * kThreads * (k >> 1) < end);
+		ok[1] = (cb + 2L * kThreads * (k >> 1) + 1 >= b0) && (cb + 2L * kThreads * (k >> 1) + 1 < end);
 		if (!ok[0] && !ok[1]) continue;
 #pragma unroll
 		for (int d = 0; d < ND; d++) {
 			if (ok[0] && ok[1]) {
-				double2 a = *reinterpret_cast<const double2 *>(xs[d] + i0 + k);
-				double2 b = *reinterpret_cast<const double2 *>(vs[d] + i0 + k);
+				double2 a = *reinterpret_cast<const double2 *>(xs[d] + cb + 2L * kThreads * (k >> 1));
+				double2 b = *reinterpret_cast<const double2 *>(vs[d] + cb + 2L * kThreads * (k >> 1));
 				p[d][0] = a.x;
 				p[d][1] = a.y;
 				v[d][0] = b.x;
 				v[d][1] = b.y;
 			} else {
-				long i = ok[0] ? i0 + k : i0 + k + 1;
+				long i = ok[0] ? cb + 2L * kThreads * (k >> 1) : cb + 2L * kThreads * (k >> 1) + 1;
 				int h = ok[0] ? 0 : 1;
 				p[d][h] = xs[d][i];
 				v[d][h] = vs[d][i];
@@ -737,10 +747,10 @@ __global__ __launch_bounds__(kThreads) void k_accel(const double *__restrict__ x
 #pragma unroll
 		for (int d = 0; d < ND; d++) {
 			if (ok[0] && ok[1]) {
-				*reinterpret_cast<double2 *>(vs[d] + i0 + k) = make_double2(v[d][0], v[d][1]);
+				*reinterpret_cast<double2 *>(vs[d] + cb + 2L * kThreads * (k >> 1)) = make_double2(v[d][0], v[d][1]);
 			} else {
-				if (ok[0]) vs[d][i0 + k] = v[d][0];
-				if (ok[1]) vs[d][i0 + k + 1] = v[d][1];
+				if (ok[0]) vs[d][cb + 2L * kThreads * (k >> 1)] = v[d][0];
+				if (ok[1]) vs[d][cb + 2L * kThreads * (k >> 1) + 1] = v[d][1];
 			}
 		}
 	}
@@ -856,12 +866,101 @@ __global__ __launch_bounds__(kThreads) void k_lattice_write(LatticeArgs a, long 
 
 inline long ceil_div(long a, long b) { return (a + b - 1) / b; }
 
+
+// ----------------------------------------------------- tiled layout -------
+// Counting sort of one species by tile (a TW^nd block of cells) for the
+// optional tiled layout (population:layout = tiled).  Particles of a tile
+// become contiguous, so a deposit or gather chunk touches a few hundred
+// nodes instead of whole rows.  Within a tile the order is arbitrary.
+struct TileGeo {
+	int tw;         // cells per tile side
+	int nt[3];      // tiles per dimension (cell index (int)p is in [0, T+1])
+	long ts[3];     // tile index stride per dimension
+	int cmax[3];    // largest admissible cell index
+};
+
+template <int ND>
+__device__ __forceinline__ int tile_key(const TileGeo &tg, const double *p) {
+	long key = 0;
+#pragma unroll
+	for (int d = 0; d < ND; d++) {
+		int c = (int)p[d];
+		c = c < 0 ? 0 : (c > tg.cmax[d] ? tg.cmax[d] : c);
+		key += (long)(c / tg.tw) * tg.ts[d];
+	}
+	return (int)key;
+}
+
+// wave-aggregated atomicAdd of 1 per active lane on ctr[key]; returns the
+// lane's slot (old value + rank among the lanes with the same key)
+__device__ __forceinline__ int agg_add(int *ctr, int key, bool active) {
+	int lane = threadIdx.x & 63;
+	unsigned long long pending = __ballot(active);
+	int mine = 0;
+	while (pending) {
+		int leader = __ffsll((long long)pending) - 1;
+		int lk = __shfl(key, leader, 64);
+		unsigned long long m = __ballot(active && key == lk) & pending;
+		int base = 0;
+		if (lane == leader) base = atomicAdd(&ctr[lk], __popcll(m));
+		base = __shfl(base, leader, 64);
+		if ((m >> lane) & 1ull) mine = base + __popcll(m & lanemask_lt());
+		pending &= ~m;
+	}
+	return mine;
+}
+
+template <int ND>
+__global__ __launch_bounds__(kThreads) void k_sort_count(const double *__restrict__ x0,
+                                                         const double *__restrict__ x1,
+                                                         const double *__restrict__ x2, long n,
+                                                         TileGeo tg, int *__restrict__ counts) {
+	const double *xs[3] = {x0, x1, x2};
+	for (long base = (long)blockIdx.x * blockDim.x; base < n; base += (long)gridDim.x * blockDim.x) {
+		long i = base + threadIdx.x;
+		bool act = i < n;
+		double p[3] = {0, 0, 0};
+		if (act) {
+#pragma unroll
+			for (int d = 0; d < ND; d++) p[d] = xs[d][i];
+		}
+		int key = act ? tile_key<ND>(tg, p) : 0;
+		agg_add(counts, key, act);
+	}
+}
+
+template <int ND>
+__global__ __launch_bounds__(kThreads) void k_sort_scatter(pinc_pop_t in, pinc_pop_t out, long b0, long n,
+                                                           TileGeo tg, int *__restrict__ cursor) {
+	for (long base = (long)blockIdx.x * blockDim.x; base < n; base += (long)gridDim.x * blockDim.x) {
+		long i = base + threadIdx.x;
+		bool act = i < n;
+		double p[3] = {0, 0, 0}, v[3] = {0, 0, 0};
+		if (act) {
+#pragma unroll
+			for (int d = 0; d < ND; d++) {
+				p[d] = in.x[d][b0 + i];
+				v[d] = in.v[d][b0 + i];
+			}
+		}
+		int key = act ? tile_key<ND>(tg, p) : 0;
+		int slot = agg_add(cursor, key, act);
+		if (act) {
+#pragma unroll
+			for (int d = 0; d < ND; d++) {
+				out.x[d][b0 + slot] = p[d];
+				out.v[d][b0 + slot] = v[d];
+			}
+		}
+	}
+}
+
 }  // namespace
 
 // =========================================================== C ABI ========
 extern "C" int pinc_hip_move_classify(pinc_pop_t pop, int s, int doMove, const double *thr,
                                       unsigned char *flags, int *chunkCount, double maxVel,
-                                      int *errFlag, void *stream) {
+                                      int *errFlag, int wrapMask, void *stream) {
 	long n = pop.iStop[s] - pop.iStart[s];
 	if (n <= 0) return 0;
 	long b0 = pop.iStart[s];
@@ -871,6 +970,7 @@ extern "C" int pinc_hip_move_classify(pinc_pop_t pop, int s, int doMove, const d
 		t.lo[d] = d < nd ? thr[d] : 0;
 		t.up[d] = d < nd ? thr[nd + d] : 0;
 		t.hi[d] = d < nd ? thr[2 * nd + d] : 0;
+		t.T[d] = d < nd ? (int)(thr[2 * nd + d] - 1.0 + 0.5) : 1;
 	}
 	int center = 0;
 	for (int d = 0, p = 1; d < nd; d++, p *= 3) center += p;
@@ -881,7 +981,7 @@ extern "C" int pinc_hip_move_classify(pinc_pop_t pop, int s, int doMove, const d
 	                   nd > 1 ? pop.x[1] + b0 : nullptr, nd > 2 ? pop.x[2] + b0 : nullptr,     \
 	                   pop.v[0] + b0, nd > 1 ? pop.v[1] + b0 : nullptr,                        \
 	                   nd > 2 ? pop.v[2] + b0 : nullptr, n, doMove, t, center, flags + b0,     \
-	                   chunkCount, maxVel, errFlag)
+	                   chunkCount, maxVel, errFlag, wrapMask)
 	if (nd == 3) LAUNCH_MC(3);
 	else if (nd == 2) LAUNCH_MC(2);
 	else LAUNCH_MC(1);
@@ -1058,4 +1158,40 @@ extern "C" int pinc_hip_init_species(pinc_pop_t pop, int s, pinc_geom_t g, long 
 	(void)hipFreeAsync(off, st);
 	*nOut = total;
 	return check_launch("init_species");
+}
+
+extern "C" int pinc_hip_sort_tiles(pinc_pop_t pop, pinc_pop_t out, int s, pinc_geom_t g, int tileWidth,
+                                   int *work, long workCap, long *nTilesOut, void *stream) {
+	TileGeo tg;
+	long nt = 1;
+	tg.tw = tileWidth;
+	for (int d = 0; d < 3; d++) {
+		int T = d < g.nd ? (d == g.nd - 1 ? g.nloc : g.T[d]) : 1;
+		tg.cmax[d] = T + 1;
+		tg.nt[d] = d < g.nd ? (T + 1) / tileWidth + 1 : 1;
+		tg.ts[d] = nt;
+		nt *= tg.nt[d];
+	}
+	*nTilesOut = nt;
+	if (2 * (nt + 1) > workCap) return set_error(hipErrorInvalidValue, "sort_tiles: work buffer too small");
+	long n = pop.iStop[s] - pop.iStart[s];
+	if (n <= 0) return 0;
+	if (n > 2147483647L) return set_error(hipErrorInvalidValue, "sort_tiles: species too large for int slots");
+	long b0 = pop.iStart[s];
+	hipStream_t st = (hipStream_t)stream;
+	int *counts = work, *offs = work + (nt + 1);
+	hipError_t e = hipMemsetAsync(counts, 0, (nt + 1) * sizeof(int), st);
+	if (e != hipSuccess) return set_error(e, "sort_tiles: memset");
+	long nb = ceil_div(n, (long)kThreads);
+	if (nb > 65536L * 8) nb = 65536L * 8;
+	int nd = g.nd;
+	const double *x0 = pop.x[0] + b0, *x1 = nd > 1 ? pop.x[1] + b0 : nullptr, *x2 = nd > 2 ? pop.x[2] + b0 : nullptr;
+	if (nd == 3) hipLaunchKernelGGL(k_sort_count<3>, dim3(nb), dim3(kThreads), 0, st, x0, x1, x2, n, tg, counts);
+	else if (nd == 2) hipLaunchKernelGGL(k_sort_count<2>, dim3(nb), dim3(kThreads), 0, st, x0, x1, x2, n, tg, counts);
+	else hipLaunchKernelGGL(k_sort_count<1>, dim3(nb), dim3(kThreads), 0, st, x0, x1, x2, n, tg, counts);
+	hipLaunchKernelGGL(k_scan_single, dim3(1), dim3(1024), 0, st, counts, offs, (int)nt);
+	if (nd == 3) hipLaunchKernelGGL(k_sort_scatter<3>, dim3(nb), dim3(kThreads), 0, st, pop, out, b0, n, tg, offs);
+	else if (nd == 2) hipLaunchKernelGGL(k_sort_scatter<2>, dim3(nb), dim3(kThreads), 0, st, pop, out, b0, n, tg, offs);
+	else hipLaunchKernelGGL(k_sort_scatter<1>, dim3(nb), dim3(kThreads), 0, st, pop, out, b0, n, tg, offs);
+	return check_launch("sort_tiles");
 }

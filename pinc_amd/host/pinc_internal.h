@@ -62,6 +62,13 @@ struct PincDevPop {
 	double *qm, *mq;              /* device q/m and m/q per species */
 	double *kePartial;
 	pinc_geom_t geom;
+	/* tiled layout (population:layout = tiled): particles sorted by tile
+	 * every sortInterval moves into the alternate arrays, then swapped */
+	int tiled, sortInterval, tileWidth;
+	long moves;
+	double *altX[3], *altV[3];
+	int *sortWork;
+	long sortWorkCap;
 	/* multi-rank migration buffers (AoS records: nd pos, nd vel, ne) */
 	double *sendBuf[2], *recvBuf[2];
 	long sendCap, recvCap;

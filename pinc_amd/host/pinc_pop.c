@@ -82,6 +82,21 @@ Population *pAlloc(const dictionary *ini) {
 		pinc_check(pinc_hip_malloc((void **)&dv->p.v[d], cap * sizeof(double)), "pAlloc vel");
 	}
 	pinc_check(pinc_hip_malloc((void **)&dv->flags, cap + 16), "pAlloc flags");
+	if (iniHas(ini, "population:layout")) {
+		char *lay = iniGetStr(ini, "population:layout");
+		if (!strcmp(lay, "tiled")) dv->tiled = 1;
+		else if (strcmp(lay, "reference")) msg(ERROR, "population:layout must be reference or tiled, not %s", lay);
+		free(lay);
+	}
+	if (dv->tiled) {
+		dv->sortInterval = iniHas(ini, "population:sortInterval") ? iniGetInt(ini, "population:sortInterval") : 4;
+		if (dv->sortInterval < 1) msg(ERROR, "population:sortInterval must be >= 1");
+		dv->tileWidth = nd == 3 ? 4 : (nd == 2 ? 8 : 32);
+		for (int d = 0; d < nd; d++) {
+			pinc_check(pinc_hip_malloc((void **)&dv->altX[d], cap * sizeof(double)), "pAlloc pos (tiled)");
+			pinc_check(pinc_hip_malloc((void **)&dv->altV[d], cap * sizeof(double)), "pAlloc vel (tiled)");
+		}
+	}
 	long maxS = 0;
 	dv->chunkBase[0] = 0;
 	for (int s = 0; s < ns; s++) {
@@ -124,6 +139,11 @@ void pFree(Population *p) {
 			pinc_hip_free(dv->p.v[d]);
 		}
 		pinc_hip_free(dv->flags);
+		for (int d = 0; d < 3; d++) {
+			pinc_hip_free(dv->altX[d]);
+			pinc_hip_free(dv->altV[d]);
+		}
+		pinc_hip_free(dv->sortWork);
 		pinc_hip_free(dv->chunkCount);
 		pinc_hip_free(dv->ws[0].chunkOffset);
 		for (int s = 0; s < p->nSpecies; s++) ws_free(&dv->ws[s]);

@@ -88,15 +88,50 @@ int puRankToNeighbor(MpiInfo *m, int rank) {
 }
 
 /* ---------------------------------------------------------------- move -- */
+/* tiled layout: counting sort by tile into the alternate arrays, then swap */
+static void sort_tiles(Population *pop) {
+	PincDevPop *dv = pop->dev;
+	pinc_pop_t p = pinc_devpop(pop), out = p;
+	for (int d = 0; d < pop->nDims; d++) {
+		out.x[d] = dv->altX[d];
+		out.v[d] = dv->altV[d];
+	}
+	for (int s = 0; s < pop->nSpecies; s++) {
+		long nTiles = 0;
+		int rc = pinc_hip_sort_tiles(p, out, s, dv->geom, dv->tileWidth, dv->sortWork, dv->sortWorkCap, &nTiles,
+		                             g_pinc.stream);
+		if (rc && 2 * (nTiles + 1) > dv->sortWorkCap) {
+			pinc_hip_free(dv->sortWork);
+			dv->sortWorkCap = 2 * (nTiles + 1);
+			pinc_check(pinc_hip_malloc((void **)&dv->sortWork, dv->sortWorkCap * sizeof(int)), "sort work");
+			rc = pinc_hip_sort_tiles(p, out, s, dv->geom, dv->tileWidth, dv->sortWork, dv->sortWorkCap, &nTiles,
+			                         g_pinc.stream);
+		}
+		pinc_check(rc, "sort tiles");
+	}
+	for (int d = 0; d < pop->nDims; d++) {
+		double *t = dv->p.x[d];
+		dv->p.x[d] = dv->altX[d];
+		dv->altX[d] = t;
+		t = dv->p.v[d];
+		dv->p.v[d] = dv->altV[d];
+		dv->altV[d] = t;
+	}
+}
+
 static void classify(Population *pop, int doMove) {
 	if (!g_pinc.thrSet) msg(ERROR, "gCreateNeighborhood must run before puMove/extract");
 	PincDevPop *dv = pop->dev;
+	if (doMove && dv->tiled && dv->moves++ % dv->sortInterval == 0) sort_tiles(pop);
+	/* tiled layout: rank-local periodic crossings are wrapped in place */
+	int nd = pop->nDims;
+	int wrapMask = !dv->tiled ? 0 : (g_pinc.nranks == 1 ? (1 << nd) - 1 : (1 << (nd - 1)) - 1);
 	pinc_pop_t p = pinc_devpop(pop);
 	for (int s = 0; s < pop->nSpecies; s++) {
 		long n = pop->iStop[s] - pop->iStart[s];
 		int slot = doMove ? pinc_probe_begin(PINC_PROBE_MOVE) : -1;
 		pinc_check(pinc_hip_move_classify(p, s, doMove, g_pinc.thr, dv->flags, dv->chunkCount + dv->chunkBase[s],
-		                                  g_pinc.maxVel, g_pinc.dErr, g_pinc.stream),
+		                                  g_pinc.maxVel, g_pinc.dErr, wrapMask, g_pinc.stream),
 		           "move/classify");
 		/* read pos+vel, write pos: 72 B per 3-D particle */
 		pinc_probe_end(PINC_PROBE_MOVE, slot, 24.0 * pop->nDims * n);
