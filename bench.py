@@ -186,6 +186,8 @@ def main() -> int:
     push_ms = (phases["move"] + phases["extract"] + phases["migrate"] + phases["deposit"] +
                phases["accelerate"]) / K
     kernels = {}
+    if args.mg == "native":
+        ROCPROF_NAMES["gs_pass"] = "k_gs_sweep"  # one fused red-black iteration per launch
     for k, p in probes.items():
         if p["samples"] == 0 or p["mean_ms"] <= 0:
             continue

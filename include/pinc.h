@@ -248,6 +248,22 @@ int pinc_probe_start(int kernel, int maxSamples);
 int pinc_probe_read(int kernel, double *meanMs, double *meanBytes, int *samples, long *launches);
 long pinc_sim_total_particles(PincSim *sim);
 
+/* Host transport for the multi-rank collectives (testing and CI: several
+ * processes on one GPU, where RCCL refuses duplicate devices).  When set
+ * before pinc_sim_create, no RCCL communicator is made and every exchange,
+ * allgather and allreduce stages device data through host memory and calls
+ * these callbacks (0 = success).  exchange: op i sends sendBytes[i] to
+ * sendPeer[i] and receives recvBytes[i] from recvPeer[i]; the peer's send
+ * op i pairs with this rank's receive op i.  NULL restores RCCL. */
+typedef struct {
+	int (*exchange)(void *user, int nOps, const int *sendPeer, const void *const *sendbuf, const long *sendBytes,
+	                const int *recvPeer, void *const *recvbuf, const long *recvBytes);
+	int (*allgather)(void *user, const double *send, double *recv, long count);
+	int (*allreduce_sum)(void *user, double *buf, long count);
+	void *user;
+} pinc_host_transport_t;
+int pinc_set_host_transport(const pinc_host_transport_t *t);
+
 #ifdef __cplusplus
 }
 #endif

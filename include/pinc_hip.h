@@ -207,6 +207,12 @@ int pinc_hip_gs_pass(double *phi, const double *rho, pinc_lvl_t L, int pass, int
                      const double *muPrev, double *partial, int *nBlocks, void *stream);
 /* phi = (phi - muA) - muB on colour `pass`'s complement and phi - muB on
  * colour `pass` (materialise pending shifts after a smoothing sequence) */
+/* Native mode (multigrid:native): one full red-black iteration of mgGS3D
+ * without the per-colour neutralisation, phiIn -> phiOut (distinct buffers),
+ * in one pass; bit-identical to two pinc_hip_gs_pass calls with muPrev NULL.
+ * Needs a 3-D level with T[0], T[1], T[2] multiples of 16. */
+int pinc_hip_gs_sweep(const double *phiIn, double *phiOut, const double *rho, pinc_lvl_t L,
+                      void *stream);
 int pinc_hip_gs_materialize(double *phi, pinc_lvl_t L, int lastPass, const double *muA,
                             const double *muB, void *stream);
 /* phi -= *mu over all points */

@@ -66,6 +66,7 @@ _sigs = {
     "pinc_sim_timers_reset": (C.c_int, [C.c_void_p]),
     "pinc_sim_total_particles": (C.c_long, [C.c_void_p]),
     "pinc_probe_start": (C.c_int, [C.c_int, C.c_int]),
+    "pinc_set_host_transport": (C.c_int, [C.c_void_p]),
     "pinc_probe_read": (C.c_int, [C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_int),
                                   C.POINTER(C.c_long)]),
 }

@@ -30,7 +30,7 @@ HIP_FLAGS = ["-std=c++17", "-O3", f"--offload-arch={ARCH}", "-ffp-contract=off",
 C_FLAGS = ["-std=c11", "-O2", "-fPIC", "-Wall", "-ffp-contract=off", f"-I{INC}", f"-I{HOST}"]
 
 HIP_SRC = ["runtime.hip", "k_particles.hip", "k_grid.hip", "k_mg.hip"]
-C_SRC = ["pinc_core.c", "pinc_grid.c", "pinc_pop.c", "pinc_pusher.c", "pinc_mg.c", "pinc_regular.c"]
+C_SRC = ["pinc_core.c", "pinc_comm.c", "pinc_grid.c", "pinc_pop.c", "pinc_pusher.c", "pinc_mg.c", "pinc_regular.c"]
 
 
 def _run(cmd: list[str]) -> None:

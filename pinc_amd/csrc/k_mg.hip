@@ -244,6 +244,126 @@ inline unsigned blocks_for(long n) {
 
 inline long npts(const pinc_lvl_t &L) { return (long)L.T[0] * L.T[1] * L.T[2]; }
 
+
+// ------------------------------------------------ fused red-black sweep ---
+// One full red-black Gauss-Seidel iteration of mgGS3D (red = storage
+// (x+y+z) even first, then black; the 1/6 * left-to-right sum of the six
+// neighbours and rho) in a single pass, from phiIn to phiOut, without the
+// per-colour neutralisation (native mode only; multigrid:native).  Each
+// workgroup owns a 16x16 column tile and a chunk of kSwZ planes, marching
+// in z with a 4-plane LDS ring: red of plane z+1 (on the tile plus a one-node
+// halo, recomputed redundantly, from old black values) is formed before
+// black of plane z (from new red).  Every value read from memory is an old
+// one, so the result equals the two-pass iteration bit for bit, and each
+// sweep reads phi and rho and writes phi once (24 B per point) instead of
+// twice per colour.
+constexpr int kSwT = 16;       // tile side (x, y)
+constexpr int kSwH = kSwT + 4; // with the two-node halo
+constexpr int kSwR = kSwT + 2; // red region: tile plus one
+constexpr int kSwZ = 16;       // planes per workgroup
+
+__global__ __launch_bounds__(256) void k_gs_sweep(const double *__restrict__ phiIn,
+                                                  double *__restrict__ phiOut,
+                                                  const double *__restrict__ rho, pinc_lvl_t Lp) {
+	// 5-plane phi ring and 3-plane rho ring: the next planes are prefetched
+	// into registers while the current ones are relaxed, two barriers per plane
+	__shared__ double cur[5][kSwH][kSwH];
+	__shared__ double rh[3][kSwR][kSwR];
+	const int TX = Lp.T[0], TY = Lp.T[1], TZ = Lp.T[2];
+	const long sy = TX, sz = (long)TX * TY;
+	const int ntx = TX / kSwT, nty = TY / kSwT;
+	const int bx = blockIdx.x % ntx, by = (blockIdx.x / ntx) % nty, bz = blockIdx.x / (ntx * nty);
+	const int x0 = bx * kSwT, y0 = by * kSwT, z0 = bz * kSwZ;
+	const int tid = threadIdx.x;
+	auto wrapi = [](int i, int T) { return i < 0 ? i + T : (i >= T ? i - T : i); };
+	auto gidx = [&](int x, int y, int z) {
+		return (long)wrapi(x, TX) + wrapi(y, TY) * sy + (long)wrapi(z, TZ) * sz;
+	};
+	auto ps = [](int z) { return (z + 10) % 5; };
+	auto rs = [](int z) { return (z + 9) % 3; };
+	// this thread's share of a plane: phi items tid, tid+256 (< 400), rho
+	// items tid, tid+256 (< 324)
+	auto fetch_phi = [&](int z, double *f) {
+		for (int k = 0; k < 2; k++) {
+			int i = tid + 256 * k;
+			if (i < kSwH * kSwH) f[k] = phiIn[gidx(x0 + i % kSwH - 2, y0 + i / kSwH - 2, z)];
+		}
+	};
+	auto fetch_rho = [&](int z, double *r) {
+		for (int k = 0; k < 2; k++) {
+			int i = tid + 256 * k;
+			if (i < kSwR * kSwR) r[k] = rho[gidx(x0 + i % kSwR - 1, y0 + i / kSwR - 1, z)];
+		}
+	};
+	auto put = [&](int zf, int zr, const double *f, const double *r, bool withRho) {
+		for (int k = 0; k < 2; k++) {
+			int i = tid + 256 * k;
+			if (i < kSwH * kSwH) cur[ps(zf)][i / kSwH][i % kSwH] = f[k];
+			if (withRho && i < kSwR * kSwR) rh[rs(zr)][i / kSwR][i % kSwR] = r[k];
+		}
+	};
+	// red points of plane z on the tile (+ one-node halo if wide)
+	auto red = [&](int z, bool wide) {
+		double(*c)[kSwH] = cur[ps(z)];
+		double(*cm)[kSwH] = cur[ps(z - 1)];
+		double(*cp)[kSwH] = cur[ps(z + 1)];
+		double(*r)[kSwR] = rh[rs(z)];
+		const int lo = wide ? 0 : 1, w = wide ? kSwR : kSwT;
+		for (int i = tid; i < w * w; i += 256) {
+			int hx = lo + i % w, hy = lo + i / w;  // red-region coordinates
+			int gx = x0 + hx - 1, gy = y0 + hy - 1;
+			if (((gx + gy + z) & 1) != 0) continue;
+			int cx = hx + 1, cy = hy + 1;          // ring coordinates
+			double xp = c[cy][cx + 1], xm = c[cy][cx - 1];
+			double yp = c[cy + 1][cx], ym = c[cy - 1][cx];
+			double zp = cp[cy][cx], zm = cm[cy][cx];
+			c[cy][cx] = (1. / 6.) * (xp + xm + yp + ym + zp + zm + r[hy][hx]);
+		}
+	};
+
+	// prologue: planes z0-2 .. z0+2 and rho z0-1 .. z0+1 in LDS, red of
+	// z0-1 (tile) and z0 (wide)
+	{
+		double f[2], r[2];
+		for (int z = z0 - 2; z <= z0 + 2; z++) {
+			fetch_phi(z, f);
+			if (z >= z0 - 1 && z <= z0 + 1) fetch_rho(z, r);
+			put(z, z, f, r, z >= z0 - 1 && z <= z0 + 1);
+		}
+	}
+	__syncthreads();
+	red(z0 - 1, false);
+	__syncthreads();
+	red(z0, true);
+	__syncthreads();
+	const int tx = tid % kSwT, ty = tid / kSwT;
+	for (int z = z0; z < z0 + kSwZ; z++) {
+		// LDS: phi planes z-2 .. z+2, rho planes z-1 .. z+1
+		double f[2], r[2];
+		fetch_phi(z + 3, f);  // in flight during the relaxation below
+		fetch_rho(z + 2, r);
+		red(z + 1, true);
+		__syncthreads();
+		double(*c)[kSwH] = cur[ps(z)];
+		double(*cm)[kSwH] = cur[ps(z - 1)];
+		double(*cp)[kSwH] = cur[ps(z + 1)];
+		int gx = x0 + tx, gy = y0 + ty;
+		int cx = tx + 2, cy = ty + 2;
+		double v = c[cy][cx];
+		if (((gx + gy + z) & 1) != 0) {
+			double xp = c[cy][cx + 1], xm = c[cy][cx - 1];
+			double yp = c[cy + 1][cx], ym = c[cy - 1][cx];
+			double zp = cp[cy][cx], zm = cm[cy][cx];
+			v = (1. / 6.) * (xp + xm + yp + ym + zp + zm + rh[rs(z)][ty + 1][tx + 1]);
+		}
+		phiOut[gidx(gx, gy, z)] = v;
+		// slot of phi z+3 held z-2 (last read by black z-1), slot of rho z+2
+		// held z-1 (last read by red z-1): both free since the barrier above
+		put(z + 3, z + 2, f, r, true);
+		__syncthreads();
+	}
+}
+
 }  // namespace
 
 extern "C" int pinc_hip_gs_pass(double *phi, const double *rho, pinc_lvl_t L, int pass, int nd3,
@@ -308,4 +428,13 @@ extern "C" int pinc_hip_prolong_add(double *phiF, const double *phiC, pinc_lvl_t
 	else if (Lf.nd == 2) hipLaunchKernelGGL(k_prolong_add<2>, dim3(nb), dim3(kThreads), 0, st, phiF, phiC, Lf);
 	else hipLaunchKernelGGL(k_prolong_add<1>, dim3(nb), dim3(kThreads), 0, st, phiF, phiC, Lf);
 	return check_launch("prolong_add");
+}
+
+extern "C" int pinc_hip_gs_sweep(const double *phiIn, double *phiOut, const double *rho, pinc_lvl_t L,
+                                 void *stream) {
+	if (L.nd != 3 || L.T[0] % kSwT || L.T[1] % kSwT || L.T[2] % kSwZ)
+		return set_error(hipErrorInvalidValue, "gs_sweep: level not a multiple of the 16x16x16 tile");
+	unsigned nb = (unsigned)((L.T[0] / kSwT) * (L.T[1] / kSwT) * (L.T[2] / kSwZ));
+	hipLaunchKernelGGL(k_gs_sweep, dim3(nb), dim3(256), 0, (hipStream_t)stream, phiIn, phiOut, rho, L);
+	return check_launch("gs_sweep");
 }

@@ -1,0 +1,101 @@
+/*
+ * pinc_comm.c -- the three collectives the hot path needs, over RCCL or over
+ * a host transport.
+ *
+ *   exchange        paired point-to-point sends/receives (z-slab halo planes,
+ *                   migrant counts and records; pusher.c:914-1027 and
+ *                   grid.c:392-402 for the reference's MPI_Sendrecv use)
+ *   allgather       rho slabs -> global rho for the replicated solve
+ *   allreduce_sum   neutralisation sums and energies (MPI_Allreduce)
+ *
+ * Default: RCCL over xGMI on the library's stream (device buffers, no host
+ * round trip).  pinc_set_host_transport() installs callbacks that move host
+ * buffers instead; the device data is staged through pinned host memory.
+ * That path exists so the multi-rank code runs with several processes on
+ * one GPU (RCCL refuses duplicate devices) and in CI; it is never the
+ * default and never used by the bench.
+ */
+#include "pinc_internal.h"
+
+static pinc_host_transport_t g_tr;
+static int g_trSet = 0;
+static unsigned char *g_stage = NULL;
+static long g_stageCap = 0;
+
+int pinc_set_host_transport(const pinc_host_transport_t *t) {
+	if (t) {
+		g_tr = *t;
+		g_trSet = 1;
+	} else {
+		memset(&g_tr, 0, sizeof(g_tr));
+		g_trSet = 0;
+	}
+	return 0;
+}
+
+int pinc_comm_host_transport(void) { return g_trSet; }
+
+static unsigned char *stage(long bytes) {
+	if (bytes > g_stageCap) {
+		free(g_stage);
+		g_stageCap = bytes + bytes / 4 + 4096;
+		g_stage = malloc(g_stageCap);
+		if (!g_stage) msg(ERROR, "host transport: out of memory (%ld bytes)", g_stageCap);
+	}
+	return g_stage;
+}
+
+void pinc_comm_exchange(int nOps, const int *sendPeer, void *const *sendbuf, const long *sendBytes,
+                        const int *recvPeer, void *const *recvbuf, const long *recvBytes, const char *what) {
+	if (!g_trSet) {
+		pinc_check(pinc_hip_comm_exchange(g_pinc.comm, nOps, sendPeer, sendbuf, sendBytes, recvPeer, recvbuf,
+		                                  recvBytes, g_pinc.stream),
+		           what);
+		return;
+	}
+	long tot = 0;
+	for (int i = 0; i < nOps; i++) tot += sendBytes[i] + recvBytes[i];
+	unsigned char *h = stage(tot);
+	const void *hs[8];
+	void *hr[8];
+	if (nOps > 8) msg(ERROR, "host transport: too many exchange ops");
+	long off = 0;
+	for (int i = 0; i < nOps; i++) {
+		hs[i] = h + off;
+		if (sendBytes[i]) pinc_check(pinc_hip_d2h(h + off, sendbuf[i], sendBytes[i], g_pinc.stream), what);
+		off += sendBytes[i];
+	}
+	for (int i = 0; i < nOps; i++) {
+		hr[i] = h + off;
+		off += recvBytes[i];
+	}
+	if (g_tr.exchange(g_tr.user, nOps, sendPeer, hs, sendBytes, recvPeer, hr, recvBytes))
+		msg(ERROR, "host transport exchange failed (%s)", what);
+	for (int i = 0; i < nOps; i++)
+		if (recvBytes[i]) pinc_check(pinc_hip_h2d(recvbuf[i], hr[i], recvBytes[i], g_pinc.stream), what);
+}
+
+void pinc_comm_allgather(const double *send, double *recv, long count, const char *what) {
+	if (!g_trSet) {
+		pinc_check(pinc_hip_comm_allgather(g_pinc.comm, send, recv, count, g_pinc.stream), what);
+		return;
+	}
+	long sb = count * (long)sizeof(double);
+	unsigned char *h = stage(sb * (g_pinc.nranks + 1));
+	pinc_check(pinc_hip_d2h(h, send, sb, g_pinc.stream), what);
+	if (g_tr.allgather(g_tr.user, (const double *)h, (double *)(h + sb), count))
+		msg(ERROR, "host transport allgather failed (%s)", what);
+	pinc_check(pinc_hip_h2d(recv, h + sb, sb * g_pinc.nranks, g_pinc.stream), what);
+}
+
+void pinc_comm_allreduce_sum(double *buf, long count, const char *what) {
+	if (!g_trSet) {
+		pinc_check(pinc_hip_comm_allreduce_sum(g_pinc.comm, buf, buf, count, g_pinc.stream), what);
+		return;
+	}
+	long sb = count * (long)sizeof(double);
+	double *h = (double *)stage(sb);
+	pinc_check(pinc_hip_d2h(h, buf, sb, g_pinc.stream), what);
+	if (g_tr.allreduce_sum(g_tr.user, h, count)) msg(ERROR, "host transport allreduce failed (%s)", what);
+	pinc_check(pinc_hip_h2d(buf, h, sb, g_pinc.stream), what);
+}

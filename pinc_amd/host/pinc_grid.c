@@ -241,7 +241,7 @@ static void exchange_planes(Grid *g, int upPlane, int downPlane) {
 	void *sb[2] = {dv->d + (long)upPlane * ps, dv->d + (long)downPlane * ps};
 	void *rb[2] = {dv->recv[0], dv->recv[1]};
 	long nb[2] = {bytes, bytes};
-	pinc_check(pinc_hip_comm_exchange(g_pinc.comm, 2, sp, sb, nb, rp, rb, nb, g_pinc.stream), "halo exchange");
+	pinc_comm_exchange(2, sp, sb, nb, rp, rb, nb, "halo exchange");
 }
 
 void gHaloOp(funPtr sliceOp, Grid *grid, const MpiInfo *mpiInfo, opDirection dir) {
@@ -314,8 +314,7 @@ void gNeutralizeGrid(Grid *grid, const MpiInfo *mpiInfo) {
 	long nTrue = ps * dv->geom.nloc;
 	pinc_check(pinc_hip_sum(dv->d + ps, nTrue, g_pinc.dScratch, PINC_SLOT(1), g_pinc.stream), "neutralize sum");
 	if (g_pinc.nranks > 1)
-		pinc_check(pinc_hip_comm_allreduce_sum(g_pinc.comm, PINC_SLOT(1), PINC_SLOT(1), 1, g_pinc.stream),
-		           "neutralize allreduce");
+		pinc_comm_allreduce_sum(PINC_SLOT(1), 1, "neutralize allreduce");
 	double tot = 0;
 	pinc_check(pinc_hip_d2h(&tot, PINC_SLOT(1), sizeof(double), g_pinc.stream), "neutralize");
 	double avg = tot / ((double)nTrue * g_pinc.nranks);

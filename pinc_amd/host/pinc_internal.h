@@ -98,6 +98,13 @@ struct MultigridSolver {
 	int native;
 };
 
+/* collectives over RCCL or the host transport (pinc_comm.c) */
+void pinc_comm_exchange(int nOps, const int *sendPeer, void *const *sendbuf, const long *sendBytes,
+                        const int *recvPeer, void *const *recvbuf, const long *recvBytes, const char *what);
+void pinc_comm_allgather(const double *send, double *recv, long count, const char *what);
+void pinc_comm_allreduce_sum(double *buf, long count, const char *what);
+int pinc_comm_host_transport(void);
+
 /* helpers shared by the host translation units */
 void pinc_ctx_require(void);
 void pinc_check(int rc, const char *where);

@@ -136,8 +136,40 @@ static void neutralize(double *a, long N) {
 /* nIter red-black iterations, each colour followed by a neutralisation:
  * the mean of pass k is formed from that pass's partial sums and applied
  * lazily by pass k+1 (k_mg.hip), then materialised once at the end. */
+/* native mode: red-black iterations without the per-colour neutralisation;
+ * full sweeps in one pass where the level tiles (pinc_hip_gs_sweep, ping-pong
+ * through res[q], which is free while smoothing), an odd last one in place */
+static void smooth_native(MultigridSolver *S, int q, int nIter, int nd3) {
+	const pinc_lvl_t L = S->L[q];
+	/* the z-marching fused sweep pays off on large levels only (measured at
+	 * 256^3: 128^3 and below are faster, launch-latency bound, as two passes) */
+	int fused = nd3 && L.nd == 3 && L.T[0] % 16 == 0 && L.T[1] % 16 == 0 && L.T[2] % 16 == 0 &&
+	            S->N[q] >= (1L << 23);
+	int k = 0;
+	if (fused) {
+		for (; k + 2 <= nIter; k += 2) {
+			int slot = q == 0 ? pinc_probe_begin(PINC_PROBE_GS) : -1;
+			pinc_check(pinc_hip_gs_sweep(S->phi[q], S->res[q], S->rho[q], L, g_pinc.stream), "gs sweep");
+			/* one full iteration: phi R + W, rho R (24 B per point) */
+			pinc_probe_end(PINC_PROBE_GS, slot, 24.0 * S->N[q]);
+			pinc_check(pinc_hip_gs_sweep(S->res[q], S->phi[q], S->rho[q], L, g_pinc.stream), "gs sweep");
+		}
+	}
+	for (; k < nIter; k++) {
+		for (int pass = 0; pass < 2; pass++) {
+			int nb = 0;
+			pinc_check(pinc_hip_gs_pass(S->phi[q], S->rho[q], L, pass, nd3, NULL, g_pinc.dScratch, &nb, g_pinc.stream),
+			           "gs pass");
+		}
+	}
+}
+
 static void smooth(MultigridSolver *S, int q, int nIter, int nd3) {
 	if (nIter <= 0) return;
+	if (S->native) {
+		smooth_native(S, q, nIter, nd3);
+		return;
+	}
 	int nPass = 2 * nIter;
 	for (int k = 0; k < nPass; k++) {
 		const double *muPrev = k ? PINC_SLOT(MU_SLOT + ((k - 1) & 1)) : NULL;
@@ -187,9 +219,7 @@ void mgSolve(MultigridSolver *S, Grid *rho, Grid *phi, const MpiInfo *mpiInfo) {
 	pinc_phase_begin(4);
 	if (g_pinc.nranks > 1) {
 		long ps = rho->dev->planeSize;
-		pinc_check(pinc_hip_comm_allgather(g_pinc.comm, rho->dev->d + ps, rho->dev->global, ps * rho->dev->geom.nloc,
-		                                   g_pinc.stream),
-		           "gather rho");
+		pinc_comm_allgather(rho->dev->d + ps, rho->dev->global, ps * rho->dev->geom.nloc, "gather rho");
 	}
 	if (S->nLevels > 1) {
 		/* the reference loops until converged (multigrid.c:1698); PINC_MG_MAX_CYCLES

@@ -249,7 +249,7 @@ void puMigrate(Population *pop, MpiInfo *m, Grid *grid) {
 		void *sb[2] = {dc, dc + PINC_MAX_SPECIES};
 		void *rb[2] = {dc + 2 * PINC_MAX_SPECIES, dc + 3 * PINC_MAX_SPECIES};
 		long nb[2] = {ns * sizeof(double), ns * sizeof(double)};
-		pinc_check(pinc_hip_comm_exchange(g_pinc.comm, 2, sp, sb, nb, rp, rb, nb, g_pinc.stream), "count exchange");
+		pinc_comm_exchange(2, sp, sb, nb, rp, rb, nb, "count exchange");
 	}
 	pinc_check(pinc_hip_d2h(cnt, dc, 4 * PINC_MAX_SPECIES * sizeof(double), g_pinc.stream), "counts");
 	long fromDown[PINC_MAX_SPECIES], fromUp[PINC_MAX_SPECIES], totFromDown = 0, totFromUp = 0;
@@ -278,7 +278,7 @@ void puMigrate(Population *pop, MpiInfo *m, Grid *grid) {
 		void *rb[2] = {dv->recvBuf[0], dv->recvBuf[1]};
 		long snb[2] = {totUp * PINC_REC * (long)sizeof(double), totDown * PINC_REC * (long)sizeof(double)};
 		long rnb[2] = {totFromDown * PINC_REC * (long)sizeof(double), totFromUp * PINC_REC * (long)sizeof(double)};
-		pinc_check(pinc_hip_comm_exchange(g_pinc.comm, 2, sp, sb, snb, rp, rb, rnb, g_pinc.stream), "migrant exchange");
+		pinc_comm_exchange(2, sp, sb, snb, rp, rb, rnb, "migrant exchange");
 	}
 	/* import in receive-tag order 26..0: from above, then local, then from below */
 	long offUp = 0, offDown = 0;

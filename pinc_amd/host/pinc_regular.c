@@ -59,7 +59,7 @@ static PincSim *sim_build(dictionary *ini, const PincSimOpts *opts) {
 	g_pinc.nranks = S->opts.nranks;
 	g_pinc.timing = S->opts.timing;
 	pinc_ctx_require();
-	if (S->opts.nranks > 1 && !g_pinc.comm) {
+	if (S->opts.nranks > 1 && !g_pinc.comm && !pinc_comm_host_transport()) {
 		if (!S->opts.commId) msg(ERROR, "multi-rank run without a communicator id");
 		pinc_check(pinc_hip_comm_init(&g_pinc.comm, S->opts.commId, S->opts.nranks, S->opts.rank), "comm init");
 	}
@@ -246,7 +246,7 @@ int pinc_sim_energy(PincSim *S, double *ke, double *pe, double *keSpecies) {
 	if (g_pinc.nranks > 1) {
 		double *d = PINC_SLOT(96);
 		pinc_check(pinc_hip_h2d(d, v, (ns + 2) * sizeof(double), g_pinc.stream), "energy");
-		pinc_check(pinc_hip_comm_allreduce_sum(g_pinc.comm, d, d, ns + 2, g_pinc.stream), "energy allreduce");
+		pinc_comm_allreduce_sum(d, ns + 2, "energy allreduce");
 		pinc_check(pinc_hip_d2h(v, d, (ns + 2) * sizeof(double), g_pinc.stream), "energy");
 	}
 	*ke = v[0];

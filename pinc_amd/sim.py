@@ -21,8 +21,12 @@ class Sim:
     def __init__(self, ini: str, overrides: Sequence[str] = (), *, literal: bool = False,
                  perturb: bool = True, maxwell: bool = False, device_init: bool = False,
                  seed: int = 0, rank: int = 0, nranks: int = 1, device: int = 0,
-                 comm_id: bytes | None = None, timing: bool = False):
+                 comm_id: bytes | None = None, timing: bool = False, transport=None):
+        """transport: a pinc_amd.transport.GlooTransport for multi-rank runs
+        without RCCL (several ranks on one GPU, tests); default RCCL."""
         self._id_buf = None
+        self._transport = transport
+        HOST.pinc_set_host_transport(C.byref(transport.struct) if transport is not None else None)
         opts = PincSimOpts()
         opts.literal = int(literal)
         opts.perturb = int(perturb)
@@ -48,6 +52,8 @@ class Sim:
         if getattr(self, "_h", None):
             HOST.pinc_sim_free(self._h)
             self._h = None
+            if self._transport is not None:
+                HOST.pinc_set_host_transport(None)
 
     def __enter__(self):
         return self
