@@ -86,11 +86,20 @@ int pinc_hip_move_classify(pinc_pop_t pop, int s, int doMove, const double *thr,
                            int *errFlag, int wrapMask, void *stream);
 
 /* Tiled layout (population:layout = tiled, not in the reference): counting
- * sort of species s by tile of tileWidth^nd cells, from pop into out (same
- * ranges); the caller swaps the two.  work holds 2*(nTiles+1) ints
- * (workCap); nTilesOut returns nTiles.  Order within a tile is arbitrary. */
+ * sort of species s by cell, cells grouped in tiles of tileWidth^nd, from
+ * pop into out (same ranges); the caller swaps the two.  nKeysOut returns
+ * the number of keys K (cells incl. the wrap layer); work must hold
+ * 2*(K+1) + 2*ceil(K/4096) + 1 ints (workCap), else an error is returned
+ * with nKeysOut set.  Order within a cell is arbitrary. */
 int pinc_hip_sort_tiles(pinc_pop_t pop, pinc_pop_t out, int s, pinc_geom_t g, int tileWidth,
-                        int *work, long workCap, long *nTilesOut, void *stream);
+                        int *work, long workCap, long *nKeysOut, void *stream);
+/* Cell ranges of the last sort: work + (K+1) holds, after pinc_hip_sort_tiles,
+ * the exclusive end of each cell's particle range.  puDistr over those
+ * ranges: one thread per cell sums its particles' weights in registers;
+ * particles that left their cell since the sort, and particles at index
+ * >= nCell (appended since), are deposited individually. */
+int pinc_hip_deposit_cells(pinc_pop_t pop, int s, pinc_geom_t g, int tileWidth, const int *cellEnds,
+                           long nCell, double *rhoSlab, void *stream);
 
 /* Emigrant extraction with the reference's back-fill order (pusher.c:
  * 782-855): survivors fill holes from the tail, emigrants are listed in the
@@ -213,6 +222,13 @@ int pinc_hip_gs_pass(double *phi, const double *rho, pinc_lvl_t L, int pass, int
  * Needs a 3-D level with T[0], T[1], T[2] multiples of 16. */
 int pinc_hip_gs_sweep(const double *phiIn, double *phiOut, const double *rho, pinc_lvl_t L,
                       void *stream);
+/* Native mode: the whole V-cycle below (and including) a coarse level in one
+ * 1024-thread workgroup, grids in LDS (at most 4800 points over all levels,
+ * 3-D, each level half the previous).  levels[0] is the top coarse level:
+ * its rho is read from `rho`, its correction starts at zero and is written
+ * to `phi`; rho of the levels below is the restricted residual times 4. */
+int pinc_hip_mg_coarse(const double *rho, double *phi, int nLevels, const pinc_lvl_t *levels, int nPre,
+                       int nPost, int nCoarse, int hw3d, void *stream);
 int pinc_hip_gs_materialize(double *phi, pinc_lvl_t L, int lastPass, const double *muA,
                             const double *muB, void *stream);
 /* phi -= *mu over all points */

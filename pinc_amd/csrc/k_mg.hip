@@ -364,6 +364,170 @@ __global__ __launch_bounds__(256) void k_gs_sweep(const double *__restrict__ phi
 	}
 }
 
+
+// ------------------------------------------- coarse levels in one launch ---
+// Native mode: the V-cycle below level qc (every level with at most
+// kCoarseMax points, down to 2^3) runs inside one 1024-thread workgroup with
+// all its grids in LDS, replacing ~100 tiny launches per cycle.  Same
+// operators as the per-level kernels: GS (3-D form), residual, restrict,
+// prolong (prol_low), neutralisation after each smoothing and of rho.
+constexpr int kCoarseMax = 4096;          // points of the top coarse level
+constexpr int kCoarseLds = 4800 * 3;      // doubles: phi, rho, res of all levels
+
+struct CoarseArgs {
+	int nLevels;
+	int T[8][3];
+	int nPre, nPost, nCoarse;
+	int hw3d;
+};
+
+__device__ double blk_sum(double v, double *wred) {
+	v = wave_sum(v);
+	int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+	__syncthreads();
+	if (lane == 0) wred[w] = v;
+	__syncthreads();
+	double t = 0;
+	for (int q = 0; q < (int)(blockDim.x >> 6); q++) t += wred[q];
+	__syncthreads();
+	return t;
+}
+
+__device__ void blk_neutralize(double *a, long n, double *wred) {
+	double t = 0;
+	for (long g = threadIdx.x; g < n; g += blockDim.x) t += a[g];
+	double mu = blk_sum(t, wred) / (double)n;
+	for (long g = threadIdx.x; g < n; g += blockDim.x) a[g] = a[g] - mu;
+	__syncthreads();
+}
+
+__device__ void blk_smooth(double *phi, const double *rho, const Lv &L, int nIter) {
+	long n = (long)L.T[0] * L.T[1] * L.T[2];
+	for (int it = 0; it < nIter; it++) {
+		for (int pass = 0; pass < 2; pass++) {
+			for (long g = threadIdx.x; g < n; g += blockDim.x) {
+				int c[3];
+				c[0] = (int)(g % L.T[0]);
+				long r = g / L.T[0];
+				c[1] = (int)(r % L.T[1]);
+				c[2] = (int)(r / L.T[1]);
+				if (((c[0] + c[1] + c[2]) & 1) != pass) continue;
+				double xp = phi[g + nb_up(L, c, 0)], xm = phi[g + nb_dn(L, c, 0)];
+				double yp = phi[g + nb_up(L, c, 1)], ym = phi[g + nb_dn(L, c, 1)];
+				double zp = phi[g + nb_up(L, c, 2)], zm = phi[g + nb_dn(L, c, 2)];
+				phi[g] = (1. / 6.) * (xp + xm + yp + ym + zp + zm + rho[g]);
+			}
+			__syncthreads();
+		}
+	}
+}
+
+struct CLevel {
+	Lv L;
+	long N;
+	double *phi, *rho, *res;
+};
+
+// level l's grids inside the LDS block (no dynamically indexed arrays:
+// everything is recomputed from the kernel arguments)
+__device__ __forceinline__ CLevel clevel(const CoarseArgs &a, double *lds, int l) {
+	CLevel c;
+	long off = 0;
+	for (int k = 0; k < l; k++) off += 3L * a.T[k][0] * a.T[k][1] * a.T[k][2];
+	pinc_lvl_t lp;
+	lp.nd = 3;
+	lp.T[0] = a.T[l][0];
+	lp.T[1] = a.T[l][1];
+	lp.T[2] = a.T[l][2];
+	c.L = make_lv(lp);
+	c.N = (long)lp.T[0] * lp.T[1] * lp.T[2];
+	c.phi = lds + off;
+	c.rho = lds + off + c.N;
+	c.res = lds + off + 2 * c.N;
+	return c;
+}
+
+__global__ __launch_bounds__(1024) void k_mg_coarse(const double *__restrict__ rhoIn,
+                                                    double *__restrict__ phiOut, CoarseArgs a) {
+	__shared__ double lds[kCoarseLds];
+	__shared__ double wred[16];
+	{
+		CLevel t = clevel(a, lds, 0);
+		for (long g = threadIdx.x; g < t.N; g += blockDim.x) {
+			t.rho[g] = rhoIn[g];
+			t.phi[g] = 0.0;
+		}
+	}
+	__syncthreads();
+	const int B = a.nLevels - 1;
+	for (int l = 0; l < B; l++) {
+		CLevel f = clevel(a, lds, l), c = clevel(a, lds, l + 1);
+		blk_neutralize(f.rho, f.N, wred);
+		blk_smooth(f.phi, f.rho, f.L, a.nPre);
+		for (long g = threadIdx.x; g < f.N; g += blockDim.x) {
+			int q[3];
+			q[0] = (int)(g % f.L.T[0]);
+			long r = g / f.L.T[0];
+			q[1] = (int)(r % f.L.T[1]);
+			q[2] = (int)(r / f.L.T[1]);
+			f.res[g] = residual_at<3>(f.phi, f.rho, f.L, q, g);
+		}
+		__syncthreads();
+		const Lv &F = f.L, &C = c.L;
+		for (long gc = threadIdx.x; gc < c.N; gc += blockDim.x) {
+			int cc[3], cf[3];
+			cc[0] = (int)(gc % C.T[0]);
+			long r = gc / C.T[0];
+			cc[1] = (int)(r % C.T[1]);
+			cc[2] = (int)(r / C.T[1]);
+			long gf = 0;
+#pragma unroll
+			for (int d = 0; d < 3; d++) {
+				cf[d] = 2 * cc[d];
+				gf += (long)cf[d] * F.s[d];
+			}
+			const double *x = f.res;
+			double v;
+			if (a.hw3d) {
+				v = (1. / 12.) * (6 * x[gf] + x[gf + nb_up(F, cf, 0)] + x[gf + nb_dn(F, cf, 0)] +
+				                  x[gf + nb_up(F, cf, 1)] + x[gf + nb_dn(F, cf, 1)] +
+				                  x[gf + nb_up(F, cf, 2)] + x[gf + nb_dn(F, cf, 2)]);
+			} else {
+				v = 6. * x[gf];
+#pragma unroll
+				for (int d = 0; d < 3; d++) v += x[gf + nb_up(F, cf, d)] + x[gf + nb_dn(F, cf, d)];
+				v *= 1. / 12.;
+			}
+			c.rho[gc] = 4.0 * v;  // native: coarse h^2 factor
+			c.phi[gc] = 0.0;      // correction scheme
+		}
+		__syncthreads();
+	}
+	{
+		CLevel b = clevel(a, lds, B);
+		blk_neutralize(b.rho, b.N, wred);
+		blk_smooth(b.phi, b.rho, b.L, a.nCoarse);
+		blk_neutralize(b.phi, b.N, wred);
+	}
+	for (int l = B - 1; l >= 0; l--) {
+		CLevel f = clevel(a, lds, l), c = clevel(a, lds, l + 1);
+		for (long g = threadIdx.x; g < f.N; g += blockDim.x) {
+			int cf[3];
+			cf[0] = (int)(g % f.L.T[0]);
+			long r = g / f.L.T[0];
+			cf[1] = (int)(r % f.L.T[1]);
+			cf[2] = (int)(r / f.L.T[1]);
+			f.phi[g] += prol_low<3, 0>(c.phi, c.L, cf);
+		}
+		__syncthreads();
+		blk_neutralize(f.phi, f.N, wred);
+		blk_smooth(f.phi, f.rho, f.L, a.nPost);
+		blk_neutralize(f.phi, f.N, wred);
+	}
+	CLevel t = clevel(a, lds, 0);
+	for (long g = threadIdx.x; g < t.N; g += blockDim.x) phiOut[g] = t.phi[g];
+}
+
 }  // namespace
 
 extern "C" int pinc_hip_gs_pass(double *phi, const double *rho, pinc_lvl_t L, int pass, int nd3,
@@ -437,4 +601,30 @@ extern "C" int pinc_hip_gs_sweep(const double *phiIn, double *phiOut, const doub
 	unsigned nb = (unsigned)((L.T[0] / kSwT) * (L.T[1] / kSwT) * (L.T[2] / kSwZ));
 	hipLaunchKernelGGL(k_gs_sweep, dim3(nb), dim3(256), 0, (hipStream_t)stream, phiIn, phiOut, rho, L);
 	return check_launch("gs_sweep");
+}
+
+extern "C" int pinc_hip_mg_coarse(const double *rho, double *phi, int nLevels, const pinc_lvl_t *levels, int nPre,
+                                  int nPost, int nCoarse, int hw3d, void *stream) {
+	CoarseArgs a;
+	if (nLevels < 1 || nLevels > 8) return set_error(hipErrorInvalidValue, "mg_coarse: 1..8 levels");
+	long tot = 0;
+	a.nLevels = nLevels;
+	for (int l = 0; l < nLevels; l++) {
+		if (levels[l].nd != 3) return set_error(hipErrorInvalidValue, "mg_coarse: 3-D levels only");
+		long n = 1;
+		for (int d = 0; d < 3; d++) {
+			a.T[l][d] = levels[l].T[d];
+			n *= levels[l].T[d];
+			if (l > 0 && 2 * levels[l].T[d] != levels[l - 1].T[d])
+				return set_error(hipErrorInvalidValue, "mg_coarse: levels must halve");
+		}
+		tot += 3 * n;
+	}
+	if (tot > kCoarseLds) return set_error(hipErrorInvalidValue, "mg_coarse: levels exceed the LDS budget");
+	a.nPre = nPre;
+	a.nPost = nPost;
+	a.nCoarse = nCoarse;
+	a.hw3d = hw3d;
+	hipLaunchKernelGGL(k_mg_coarse, dim3(1), dim3(1024), 0, (hipStream_t)stream, rho, phi, a);
+	return check_launch("mg_coarse");
 }

@@ -361,18 +361,19 @@ __device__ __forceinline__ long node_off(const Geo &G, int d, int p) {
 }
 
 // --------------------------------------------- LDS-privatised deposit -----
-// One workgroup owns a chunk of kDepChunk consecutive particles, loaded as
-// lane-contiguous 16-B pairs.  In either layout (the reference's order,
-// spatially coherent from the lattice start, or the tiled layout) a chunk
-// covers a small box of nodes:
-//  * the two particles of a pair often share a cell: their eight weights are
-//    summed in registers first;
+// One workgroup owns a chunk of kDepChunk consecutive particles; each thread
+// owns kDepItems consecutive ones (loaded 16 B at a time).  In either layout
+// (the reference's order, spatially coherent from the lattice start, or the
+// cell-sorted tiled layout) consecutive particles mostly share a cell and a
+// chunk covers a small box of nodes:
+//  * a thread sums the eight weights of a run of particles in one cell in
+//    registers and adds them once (cell-sorted: once per kDepItems);
 //  * the box is accumulated in LDS (ds_add_f64) and flushed with one global
 //    atomic per touched node.
 // Chunks whose box exceeds the LDS tile use the same run accumulation with
 // global atomics.  Weights are the reference's expressions (pusher.c:550-565,
 // 626-638); only the summation order differs from the serial loop.
-constexpr int kDepItems = 8;
+constexpr int kDepItems = 16;
 constexpr int kDepChunk = kThreads * kDepItems;
 constexpr int kDepCap = 4096;  // LDS nodes per workgroup (32 KiB)
 
@@ -433,44 +434,40 @@ __global__ __launch_bounds__(kThreads) void k_deposit_tiled(const double *__rest
 	Geo G = make_geo(g);
 	const double *xs[3] = {x0, x1, x2};
 	const long end = b0 + n;
-	// item k of this thread: pair k/2 of the lane-contiguous pairs, so each
-	// 16-B load instruction of a wave covers 1 KiB of contiguous memory
-	const long cb = (b0 & ~1L) + (long)blockIdx.x * kDepChunk + 2L * threadIdx.x;
+	// thread's items: i0 .. i0+kDepItems-1, i0 even relative to the 16-B
+	// aligned base below b0
+	const long i0 = (b0 & ~1L) + (long)blockIdx.x * kDepChunk + (long)threadIdx.x * kDepItems;
 	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-
-	double p[3][kDepItems];
+	auto load2 = [&](int d, int k, double &a, double &b) {
+		long i = i0 + k;
+		if (i >= b0 && i + 1 < end) {
+			double2 v = *reinterpret_cast<const double2 *>(xs[d] + i);
+			a = v.x;
+			b = v.y;
+		} else {
+			a = (i >= b0 && i < end) ? xs[d][i] : 0.0;
+			b = (i + 1 >= b0 && i + 1 < end) ? xs[d][i + 1] : 0.0;
+		}
+	};
 	unsigned valid = 0;
 #pragma unroll
-	for (int k = 0; k < kDepItems; k++) {
-		long i = cb + 2L * kThreads * (k >> 1) + (k & 1);
-		valid |= (unsigned)(i >= b0 && i < end) << k;
-	}
+	for (int k = 0; k < kDepItems; k++) valid |= (unsigned)(i0 + k >= b0 && i0 + k < end) << k;
+
+	// pass 1: bounding box of the chunk's cells (j .. j+1 per dimension)
+	int lo[3] = {INT32_MAX, INT32_MAX, INT32_MAX}, hi[3] = {INT32_MIN, INT32_MIN, INT32_MIN};
 #pragma unroll
 	for (int d = 0; d < ND; d++) {
 #pragma unroll
 		for (int k = 0; k < kDepItems; k += 2) {
-			long i = cb + 2L * kThreads * (k >> 1);
-			if (((valid >> k) & 3u) == 3u) {
-				double2 v = *reinterpret_cast<const double2 *>(xs[d] + i);
-				p[d][k] = v.x;
-				p[d][k + 1] = v.y;
-			} else {
-				p[d][k] = ((valid >> k) & 1u) ? xs[d][i] : 0.0;
-				p[d][k + 1] = ((valid >> (k + 1)) & 1u) ? xs[d][i + 1] : 0.0;
+			double a, b;
+			load2(d, k, a, b);
+			if ((valid >> k) & 1u) {
+				lo[d] = min(lo[d], (int)a);
+				hi[d] = max(hi[d], (int)a + 1);
 			}
-		}
-	}
-
-	// bounding box of the chunk's cells (j .. j+1 per dimension)
-	int lo[3] = {INT32_MAX, INT32_MAX, INT32_MAX}, hi[3] = {INT32_MIN, INT32_MIN, INT32_MIN};
-#pragma unroll
-	for (int k = 0; k < kDepItems; k++) {
-		if ((valid >> k) & 1u) {
-#pragma unroll
-			for (int d = 0; d < ND; d++) {
-				int j = (int)p[d][k];
-				lo[d] = min(lo[d], j);
-				hi[d] = max(hi[d], j + 1);
+			if ((valid >> (k + 1)) & 1u) {
+				lo[d] = min(lo[d], (int)b);
+				hi[d] = max(hi[d], (int)b + 1);
 			}
 		}
 	}
@@ -500,49 +497,8 @@ __global__ __launch_bounds__(kThreads) void k_deposit_tiled(const double *__rest
 	__syncthreads();
 	const int vol = box[6];
 
-	if (vol == 0) {
-		// scattered chunk: runs of equal cells, global atomics
-		int cj[3] = {0, 0, 0};
-		bool have = false;
-		double a[NC];
-#pragma unroll
-		for (int k = 0; k < kDepItems; k++) {
-			if (!((valid >> k) & 1u)) continue;
-			double dec[3], comp[3], w[NC];
-			int j[3];
-			bool same = have;
-#pragma unroll
-			for (int d = 0; d < ND; d++) {
-				j[d] = (int)p[d][k];
-				dec[d] = p[d][k] - j[d];
-				comp[d] = 1 - dec[d];
-				same = same && (j[d] == cj[d]);
-			}
-			cic_weights<ND, V3D>(dec, comp, w);
-			if (same) {
-#pragma unroll
-				for (int c = 0; c < NC; c++) a[c] += w[c];
-			} else {
-				if (have) {
-#pragma unroll
-					for (int c = 0; c < NC; c++) unsafeAtomicAdd(&rho[corner_off<ND>(G, cj, c)], a[c]);
-				}
-#pragma unroll
-				for (int c = 0; c < NC; c++) a[c] = w[c];
-#pragma unroll
-				for (int d = 0; d < ND; d++) cj[d] = j[d];
-				have = true;
-			}
-		}
-		if (have) {
-#pragma unroll
-			for (int c = 0; c < NC; c++) unsafeAtomicAdd(&rho[corner_off<ND>(G, cj, c)], a[c]);
-		}
-		return;
-	}
-
 	int blo[3] = {0, 0, 0}, st[3] = {0, 0, 0}, bn[3] = {1, 1, 1};
-	{
+	if (vol) {
 		int sz = 1;
 #pragma unroll
 		for (int d = 0; d < ND; d++) {
@@ -551,6 +507,8 @@ __global__ __launch_bounds__(kThreads) void k_deposit_tiled(const double *__rest
 			st[d] = sz;
 			sz *= bn[d];
 		}
+		for (int t = threadIdx.x; t < vol; t += kThreads) acc[t] = 0.0;
+		__syncthreads();
 	}
 	int coff[NC];
 #pragma unroll
@@ -559,46 +517,61 @@ __global__ __launch_bounds__(kThreads) void k_deposit_tiled(const double *__rest
 #pragma unroll
 		for (int d = 0; d < ND; d++) coff[c] += ((c >> d) & 1) ? st[d] : 0;
 	}
-	for (int t = threadIdx.x; t < vol; t += kThreads) acc[t] = 0.0;
-	__syncthreads();
 
-	{
-		int cur = -1;
-		double a[NC];
+	// pass 2: runs of equal cells summed in registers
+	int cj[3] = {INT32_MIN, 0, 0};
+	double a[NC];
 #pragma unroll
-		for (int k = 0; k < kDepItems; k++) {
-			if (!((valid >> k) & 1u)) continue;
-			double dec[3], comp[3], w[NC];
+	for (int c = 0; c < NC; c++) a[c] = 0.0;
+	auto flush = [&]() {
+		if (cj[0] == INT32_MIN) return;
+		if (vol) {
 			int l0 = 0;
 #pragma unroll
+			for (int d = 0; d < ND; d++) l0 += (cj[d] - blo[d]) * st[d];
+#pragma unroll
+			for (int c = 0; c < NC; c++) atomicAdd(&acc[l0 + coff[c]], a[c]);
+		} else {
+#pragma unroll
+			for (int c = 0; c < NC; c++) unsafeAtomicAdd(&rho[corner_off<ND>(G, cj, c)], a[c]);
+		}
+	};
+#pragma unroll 2
+	for (int k = 0; k < kDepItems; k += 2) {
+		double pp[3][2];
+#pragma unroll
+		for (int d = 0; d < ND; d++) load2(d, k, pp[d][0], pp[d][1]);
+#pragma unroll
+		for (int h = 0; h < 2; h++) {
+			if (!((valid >> (k + h)) & 1u)) continue;
+			double dec[3], comp[3], w[NC];
+			int j[3];
+			bool same = true;
+#pragma unroll
 			for (int d = 0; d < ND; d++) {
-				int j = (int)p[d][k];
-				dec[d] = p[d][k] - j;
+				j[d] = (int)pp[d][h];
+				dec[d] = pp[d][h] - j[d];
 				comp[d] = 1 - dec[d];
-				l0 += (j - blo[d]) * st[d];
+				same = same && (j[d] == cj[d]);
 			}
 			cic_weights<ND, V3D>(dec, comp, w);
-			if (l0 == cur) {
+			if (same) {
 #pragma unroll
 				for (int c = 0; c < NC; c++) a[c] += w[c];
 			} else {
-				if (cur >= 0) {
-#pragma unroll
-					for (int c = 0; c < NC; c++) atomicAdd(&acc[cur + coff[c]], a[c]);
-				}
+				flush();
 #pragma unroll
 				for (int c = 0; c < NC; c++) a[c] = w[c];
-				cur = l0;
+#pragma unroll
+				for (int d = 0; d < ND; d++) cj[d] = j[d];
 			}
 		}
-		if (cur >= 0) {
-#pragma unroll
-			for (int c = 0; c < NC; c++) atomicAdd(&acc[cur + coff[c]], a[c]);
-		}
 	}
+	flush();
+	if (!vol) return;
 	__syncthreads();
 
-	// flush: one global atomic per touched node
+	// flush the tile: one global atomic per touched node
 	for (int t = threadIdx.x; t < vol; t += kThreads) {
 		double v = acc[t];
 		if (v == 0.0) continue;
@@ -879,16 +852,22 @@ struct TileGeo {
 	int cmax[3];    // largest admissible cell index
 };
 
+// sort key: tile index (tiles in x-fastest order) then the cell inside the
+// tile (x fastest), so particles of one cell end up contiguous and cells of
+// one tile adjacent
 template <int ND>
 __device__ __forceinline__ int tile_key(const TileGeo &tg, const double *p) {
-	long key = 0;
+	long tile = 0;
+	int cell = 0, cs = 1;
 #pragma unroll
 	for (int d = 0; d < ND; d++) {
 		int c = (int)p[d];
 		c = c < 0 ? 0 : (c > tg.cmax[d] ? tg.cmax[d] : c);
-		key += (long)(c / tg.tw) * tg.ts[d];
+		tile += (long)(c / tg.tw) * tg.ts[d];
+		cell += (c % tg.tw) * cs;
+		cs *= tg.tw;
 	}
-	return (int)key;
+	return (int)(tile * cs + cell);
 }
 
 // wave-aggregated atomicAdd of 1 per active lane on ctr[key]; returns the
@@ -952,6 +931,201 @@ __global__ __launch_bounds__(kThreads) void k_sort_scatter(pinc_pop_t in, pinc_p
 				out.v[d][b0 + slot] = v[d];
 			}
 		}
+	}
+}
+
+
+// exclusive scan of n ints for large n: block sums, a single-block scan of
+// those, then per-block scans with the block offsets; out[n] = total
+constexpr int kScanItems = 16;
+constexpr int kScanBlock = kThreads * kScanItems;
+
+__global__ __launch_bounds__(kThreads) void k_scan_sums(const int *__restrict__ in, long n,
+                                                        int *__restrict__ sums) {
+	__shared__ int w[kThreads / 64];
+	long b0 = (long)blockIdx.x * kScanBlock;
+	int t = 0;
+	for (int k = 0; k < kScanItems; k++) {
+		long i = b0 + (long)k * kThreads + threadIdx.x;
+		if (i < n) t += in[i];
+	}
+	t = wave_sum(t);
+	if ((threadIdx.x & 63) == 0) w[threadIdx.x >> 6] = t;
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		int s = 0;
+		for (int q = 0; q < kThreads / 64; q++) s += w[q];
+		sums[blockIdx.x] = s;
+	}
+}
+
+__global__ __launch_bounds__(kThreads) void k_scan_apply(const int *__restrict__ in, long n,
+                                                         const int *__restrict__ offs,
+                                                         int *__restrict__ out) {
+	__shared__ int wtot[kThreads / 64];
+	long b0 = (long)blockIdx.x * kScanBlock;
+	// thread owns kScanItems consecutive elements
+	long i0 = b0 + (long)threadIdx.x * kScanItems;
+	int v[kScanItems];
+	int t = 0;
+#pragma unroll
+	for (int k = 0; k < kScanItems; k++) {
+		v[k] = (i0 + k < n) ? in[i0 + k] : 0;
+		t += v[k];
+	}
+	// exclusive scan of t over the block
+	int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+	int x = t;
+#pragma unroll
+	for (int o = 1; o < 64; o <<= 1) {
+		int y = __shfl_up(x, o, 64);
+		if (lane >= o) x += y;
+	}
+	if (lane == 63) wtot[wv] = x;
+	__syncthreads();
+	int before = 0;
+	for (int q = 0; q < wv; q++) before += wtot[q];
+	int run = offs[blockIdx.x] + before + x - t;
+#pragma unroll
+	for (int k = 0; k < kScanItems; k++) {
+		if (i0 + k < n) out[i0 + k] = run;
+		run += v[k];
+	}
+	if (i0 + kScanItems >= n && i0 < n) out[n] = run;
+}
+
+
+// ------------------------------------------ deposit over sorted cell ranges --
+// Tiled layout after a sort: offs is the sort's cursor array after the
+// scatter, i.e. the exclusive end of each key's range, so [offs[key-1],
+// offs[key]) holds the particles that were in cell `key` at the last sort.  One thread per cell
+// sums the eight CIC weights of its particles in registers (no atomics per
+// particle); particles that have since moved to another cell are added
+// individually (LDS box with a one-cell margin, else global atomics).  A
+// workgroup covers 256 consecutive keys (4 tiles in 3-D), accumulated in LDS
+// and flushed once.
+template <int ND, bool V3D>
+__global__ __launch_bounds__(kThreads) void k_deposit_cells(const double *__restrict__ x0,
+                                                            const double *__restrict__ x1,
+                                                            const double *__restrict__ x2, long nCell,
+                                                            const int *__restrict__ offs, long nKeys,
+                                                            TileGeo tg, pinc_geom_t g,
+                                                            double *__restrict__ rho) {
+	constexpr int NC = 1 << ND;
+	__shared__ double acc[kDepCap];
+	Geo G = make_geo(g);
+	const double *xs[3] = {x0, x1, x2};
+	int cpt = 1;
+#pragma unroll
+	for (int d = 0; d < ND; d++) cpt *= tg.tw;
+	const long k0 = (long)blockIdx.x * kThreads;
+	const long k1 = min(k0 + kThreads, nKeys) - 1;
+	// node box of the block's tiles plus a one-cell margin
+	long t0 = k0 / cpt, t1 = k1 / cpt;
+	int tlo[3], thi[3];
+	bool boxOk = true;
+#pragma unroll
+	for (int d = ND - 1; d >= 0; d--) {
+		tlo[d] = (int)(t0 / tg.ts[d]);
+		thi[d] = (int)(t1 / tg.ts[d]);
+		t0 -= (long)tlo[d] * tg.ts[d];
+		t1 -= (long)thi[d] * tg.ts[d];
+		if (d > 0 && tlo[d] != thi[d]) boxOk = false;
+	}
+	int blo[3] = {0, 0, 0}, bn[3] = {1, 1, 1}, st[3] = {0, 0, 0};
+	int vol = 1;
+#pragma unroll
+	for (int d = 0; d < ND; d++) {
+		int clo = tlo[d] * tg.tw, chi = min(thi[d] * tg.tw + tg.tw - 1, tg.cmax[d]);
+		blo[d] = clo - 1;
+		bn[d] = chi - clo + 4;  // nodes clo-1 .. chi+2
+		st[d] = vol;
+		vol *= bn[d];
+	}
+	if (!boxOk || vol > kDepCap) vol = 0;
+	for (int t = threadIdx.x; t < vol; t += kThreads) acc[t] = 0.0;
+	__syncthreads();
+
+	auto add8 = [&](const int *j, const double *w) {
+		bool inBox = vol > 0;
+#pragma unroll
+		for (int d = 0; d < ND; d++) inBox = inBox && j[d] >= blo[d] && j[d] + 1 < blo[d] + bn[d];
+		if (inBox) {
+			int l0 = 0;
+#pragma unroll
+			for (int d = 0; d < ND; d++) l0 += (j[d] - blo[d]) * st[d];
+#pragma unroll
+			for (int c = 0; c < NC; c++) {
+				int off = l0;
+#pragma unroll
+				for (int d = 0; d < ND; d++) off += ((c >> d) & 1) ? st[d] : 0;
+				atomicAdd(&acc[off], w[c]);
+			}
+		} else {
+#pragma unroll
+			for (int c = 0; c < NC; c++) unsafeAtomicAdd(&rho[corner_off<ND>(G, j, c)], w[c]);
+		}
+	};
+
+	const long key = k0 + threadIdx.x;
+	if (key < nKeys) {
+		// this thread's cell
+		long tile = key / cpt;
+		int cin = (int)(key - tile * cpt);
+		int cell[3] = {0, 0, 0};
+#pragma unroll
+		for (int d = ND - 1; d >= 0; d--) {
+			int tc = (int)(tile / tg.ts[d]);
+			tile -= (long)tc * tg.ts[d];
+			cell[d] = tc * tg.tw;
+		}
+#pragma unroll
+		for (int d = 0; d < ND; d++) {
+			cell[d] += cin % tg.tw;
+			cin /= tg.tw;
+		}
+		long a = key > 0 ? (long)offs[key - 1] : 0, b = min((long)offs[key], nCell);
+		double sum[NC];
+#pragma unroll
+		for (int c = 0; c < NC; c++) sum[c] = 0.0;
+		bool any = false;
+		for (long i = a; i < b; i++) {
+			double dec[3], comp[3], w[NC];
+			int j[3];
+			bool own = true;
+#pragma unroll
+			for (int d = 0; d < ND; d++) {
+				double p = xs[d][i];
+				j[d] = (int)p;
+				dec[d] = p - j[d];
+				comp[d] = 1 - dec[d];
+				own = own && j[d] == cell[d];
+			}
+			cic_weights<ND, V3D>(dec, comp, w);
+			if (own) {
+#pragma unroll
+				for (int c = 0; c < NC; c++) sum[c] += w[c];
+				any = true;
+			} else {
+				add8(j, w);
+			}
+		}
+		if (any) add8(cell, sum);
+	}
+	if (!vol) return;
+	__syncthreads();
+	for (int t = threadIdx.x; t < vol; t += kThreads) {
+		double v = acc[t];
+		if (v == 0.0) continue;
+		int r = t;
+		long off = 0;
+#pragma unroll
+		for (int d = 0; d < ND; d++) {
+			int c = r % bn[d];
+			r /= bn[d];
+			off += node_off(G, d, blo[d] + c);
+		}
+		unsafeAtomicAdd(&rho[off], v);
 	}
 }
 
@@ -1062,7 +1236,6 @@ extern "C" int pinc_hip_deposit(pinc_pop_t pop, int s, pinc_geom_t g, double *rh
 	long n = pop.iStop[s] - pop.iStart[s];
 	if (n <= 0) return 0;
 	long b0 = pop.iStart[s];
-	// chunks start at the even index at or below b0 (16-B aligned pairs)
 	long nb = ceil_div(n + (b0 & 1L), (long)kDepChunk);
 	hipStream_t st = (hipStream_t)stream;
 	const double *x0 = pop.x[0];
@@ -1160,10 +1333,9 @@ extern "C" int pinc_hip_init_species(pinc_pop_t pop, int s, pinc_geom_t g, long 
 	return check_launch("init_species");
 }
 
-extern "C" int pinc_hip_sort_tiles(pinc_pop_t pop, pinc_pop_t out, int s, pinc_geom_t g, int tileWidth,
-                                   int *work, long workCap, long *nTilesOut, void *stream) {
+static TileGeo make_tile_geo(pinc_geom_t g, int tileWidth, long *nKeys) {
 	TileGeo tg;
-	long nt = 1;
+	long nt = 1, cpt = 1;
 	tg.tw = tileWidth;
 	for (int d = 0; d < 3; d++) {
 		int T = d < g.nd ? (d == g.nd - 1 ? g.nloc : g.T[d]) : 1;
@@ -1171,16 +1343,28 @@ extern "C" int pinc_hip_sort_tiles(pinc_pop_t pop, pinc_pop_t out, int s, pinc_g
 		tg.nt[d] = d < g.nd ? (T + 1) / tileWidth + 1 : 1;
 		tg.ts[d] = nt;
 		nt *= tg.nt[d];
+		if (d < g.nd) cpt *= tileWidth;
 	}
-	*nTilesOut = nt;
-	if (2 * (nt + 1) > workCap) return set_error(hipErrorInvalidValue, "sort_tiles: work buffer too small");
+	*nKeys = nt * cpt;
+	return tg;
+}
+
+extern "C" int pinc_hip_sort_tiles(pinc_pop_t pop, pinc_pop_t out, int s, pinc_geom_t g, int tileWidth,
+                                   int *work, long workCap, long *nKeysOut, void *stream) {
+	long nk = 0;
+	TileGeo tg = make_tile_geo(g, tileWidth, &nk);
+	long nsb = ceil_div(nk, (long)kScanBlock);
+	*nKeysOut = nk;
+	// work: counts[nk+1] | offsets[nk+1] | block sums[nsb] | block offsets[nsb+1]
+	long need = 2 * (nk + 1) + 2 * nsb + 1;
+	if (need > workCap || nk > 2147483647L) return set_error(hipErrorInvalidValue, "sort_tiles: work buffer too small");
 	long n = pop.iStop[s] - pop.iStart[s];
 	if (n <= 0) return 0;
 	if (n > 2147483647L) return set_error(hipErrorInvalidValue, "sort_tiles: species too large for int slots");
 	long b0 = pop.iStart[s];
 	hipStream_t st = (hipStream_t)stream;
-	int *counts = work, *offs = work + (nt + 1);
-	hipError_t e = hipMemsetAsync(counts, 0, (nt + 1) * sizeof(int), st);
+	int *counts = work, *offs = work + (nk + 1), *bsum = offs + (nk + 1), *boff = bsum + nsb;
+	hipError_t e = hipMemsetAsync(counts, 0, (nk + 1) * sizeof(int), st);
 	if (e != hipSuccess) return set_error(e, "sort_tiles: memset");
 	long nb = ceil_div(n, (long)kThreads);
 	if (nb > 65536L * 8) nb = 65536L * 8;
@@ -1189,9 +1373,41 @@ extern "C" int pinc_hip_sort_tiles(pinc_pop_t pop, pinc_pop_t out, int s, pinc_g
 	if (nd == 3) hipLaunchKernelGGL(k_sort_count<3>, dim3(nb), dim3(kThreads), 0, st, x0, x1, x2, n, tg, counts);
 	else if (nd == 2) hipLaunchKernelGGL(k_sort_count<2>, dim3(nb), dim3(kThreads), 0, st, x0, x1, x2, n, tg, counts);
 	else hipLaunchKernelGGL(k_sort_count<1>, dim3(nb), dim3(kThreads), 0, st, x0, x1, x2, n, tg, counts);
-	hipLaunchKernelGGL(k_scan_single, dim3(1), dim3(1024), 0, st, counts, offs, (int)nt);
+	hipLaunchKernelGGL(k_scan_sums, dim3((unsigned)nsb), dim3(kThreads), 0, st, counts, nk, bsum);
+	hipLaunchKernelGGL(k_scan_single, dim3(1), dim3(1024), 0, st, bsum, boff, (int)nsb);
+	hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)nsb), dim3(kThreads), 0, st, counts, nk, boff, offs);
 	if (nd == 3) hipLaunchKernelGGL(k_sort_scatter<3>, dim3(nb), dim3(kThreads), 0, st, pop, out, b0, n, tg, offs);
 	else if (nd == 2) hipLaunchKernelGGL(k_sort_scatter<2>, dim3(nb), dim3(kThreads), 0, st, pop, out, b0, n, tg, offs);
 	else hipLaunchKernelGGL(k_sort_scatter<1>, dim3(nb), dim3(kThreads), 0, st, pop, out, b0, n, tg, offs);
 	return check_launch("sort_tiles");
+}
+
+extern "C" int pinc_hip_deposit_cells(pinc_pop_t pop, int s, pinc_geom_t g, int tileWidth, const int *offs,
+                                      long nCell, double *rho, void *stream) {
+	long n = pop.iStop[s] - pop.iStart[s];
+	if (n <= 0) return 0;
+	long nKeys = 0;
+	TileGeo tg = make_tile_geo(g, tileWidth, &nKeys);
+	long b0 = pop.iStart[s];
+	if (nCell > n) nCell = n;
+	hipStream_t st = (hipStream_t)stream;
+	const double *x0 = pop.x[0] + b0;
+	const double *x1 = g.nd > 1 ? pop.x[1] + b0 : nullptr;
+	const double *x2 = g.nd > 2 ? pop.x[2] + b0 : nullptr;
+	unsigned nb = (unsigned)ceil_div(nKeys, (long)kThreads);
+	if (g.nd == 3)
+		hipLaunchKernelGGL((k_deposit_cells<3, true>), dim3(nb), dim3(kThreads), 0, st, x0, x1, x2, nCell, offs, nKeys,
+		                   tg, g, rho);
+	else if (g.nd == 2)
+		hipLaunchKernelGGL((k_deposit_cells<2, false>), dim3(nb), dim3(kThreads), 0, st, x0, x1, x2, nCell, offs,
+		                   nKeys, tg, g, rho);
+	else
+		hipLaunchKernelGGL((k_deposit_cells<1, false>), dim3(nb), dim3(kThreads), 0, st, x0, x1, x2, nCell, offs,
+		                   nKeys, tg, g, rho);
+	int rc = check_launch("deposit_cells");
+	if (rc || nCell >= n) return rc;
+	// particles appended since the sort (immigrants): generic deposit
+	pinc_pop_t tail = pop;
+	tail.iStart[s] = b0 + nCell;
+	return pinc_hip_deposit(tail, s, g, rho, stream);
 }

@@ -67,8 +67,10 @@ struct PincDevPop {
 	int tiled, sortInterval, tileWidth;
 	long moves;
 	double *altX[3], *altV[3];
-	int *sortWork;
-	long sortWorkCap;
+	int *sortWork[PINC_MAX_SPECIES];    /* per species: counts | cell ends | scan scratch */
+	long sortWorkCap[PINC_MAX_SPECIES];
+	long sortKeys;                      /* cells (keys) of the sort */
+	long cellValid[PINC_MAX_SPECIES];   /* particles still in sorted order (-1: no sort yet) */
 	/* multi-rank migration buffers (AoS records: nd pos, nd vel, ne) */
 	double *sendBuf[2], *recvBuf[2];
 	long sendCap, recvCap;

@@ -79,6 +79,19 @@ MultigridSolver *mgAllocSolver(const dictionary *ini, Grid *rho, Grid *phi) {
 		if (rho->trueSize[d] % (1 << S->nLevels))
 			msg(ERROR, "All elements in grid:trueSize must be a multiple of 2^mgLevels=%d", 1 << S->nLevels);
 	pinc_geom_t g = rho->dev->geom;
+	if (S->native) {
+		/* native mode coarsens on down to 2 points per dimension, so the
+		 * bottom solve is exact enough not to limit the cycle's convergence */
+		for (;;) {
+			int ok = S->nLevels < PINC_MAX_LEVELS;
+			for (int d = 0; d < nd && ok; d++) {
+				int t = g.T[d] >> (S->nLevels - 1);
+				ok = (t % 2 == 0) && t / 2 >= 2;
+			}
+			if (!ok) break;
+			S->nLevels++;
+		}
+	}
 	for (int q = 0; q < S->nLevels; q++) {
 		S->L[q].nd = nd;
 		S->N[q] = 1;
@@ -189,8 +202,29 @@ static void smooth(MultigridSolver *S, int q, int nIter, int nd3) {
 	           "gs materialize");
 }
 
+/* native mode, 3-D: first level from which the rest of the V-cycle fits the
+ * single-workgroup LDS kernel (pinc_hip_mg_coarse), or -1 */
+static int coarse_start(const MultigridSolver *S) {
+	if (!S->native || S->L[0].nd != 3 || !S->pre3d || !S->post3d || !S->coarse3d) return -1;
+	for (int q = 1; q < S->nLevels; q++) {
+		if (S->N[q] > 4096) continue;
+		long tot = 0;
+		for (int k = q; k < S->nLevels; k++) tot += 3 * S->N[k];
+		if (tot <= 14400 && S->nLevels - q <= 8) return q;
+	}
+	return -1;
+}
+
 static void vrec(MultigridSolver *S, int q) {
 	int bottom = S->nLevels - 1;
+	int qc = coarse_start(S);
+	if (qc > 0 && q == qc) {
+		pinc_check(pinc_hip_mg_coarse(S->rho[q], S->phi[q], S->nLevels - q, &S->L[q], S->nPre, S->nPost, S->nCoarse,
+		                              S->restr3d, g_pinc.stream),
+		           "mg coarse");
+		pinc_check(pinc_hip_prolong_add(S->phi[q - 1], S->phi[q], S->L[q - 1], g_pinc.stream), "prolong");
+		return;
+	}
 	/* native mode: correction scheme, each coarse visit solves for the
 	 * correction from zero (the reference warm-starts coarse phi) */
 	if (S->native && q > 0) pinc_check(pinc_hip_zero(S->phi[q], S->N[q], g_pinc.stream), "native zero");

@@ -92,6 +92,7 @@ Population *pAlloc(const dictionary *ini) {
 		dv->sortInterval = iniHas(ini, "population:sortInterval") ? iniGetInt(ini, "population:sortInterval") : 4;
 		if (dv->sortInterval < 1) msg(ERROR, "population:sortInterval must be >= 1");
 		dv->tileWidth = nd == 3 ? 4 : (nd == 2 ? 8 : 32);
+		for (int s = 0; s < PINC_MAX_SPECIES; s++) dv->cellValid[s] = -1;
 		for (int d = 0; d < nd; d++) {
 			pinc_check(pinc_hip_malloc((void **)&dv->altX[d], cap * sizeof(double)), "pAlloc pos (tiled)");
 			pinc_check(pinc_hip_malloc((void **)&dv->altV[d], cap * sizeof(double)), "pAlloc vel (tiled)");
@@ -143,7 +144,7 @@ void pFree(Population *p) {
 			pinc_hip_free(dv->altX[d]);
 			pinc_hip_free(dv->altV[d]);
 		}
-		pinc_hip_free(dv->sortWork);
+		for (int s = 0; s < PINC_MAX_SPECIES; s++) pinc_hip_free(dv->sortWork[s]);
 		pinc_hip_free(dv->chunkCount);
 		pinc_hip_free(dv->ws[0].chunkOffset);
 		for (int s = 0; s < p->nSpecies; s++) ws_free(&dv->ws[s]);
@@ -328,6 +329,8 @@ void pSyncToDevice(Population *p) {
 	if (!p->pos) msg(ERROR, "pSyncToDevice without host particles");
 	int nd = p->nDims;
 	PincDevPop *dv = p->dev;
+	/* new particle order: the cell ranges of the last tile sort no longer apply */
+	for (int s = 0; s < PINC_MAX_SPECIES; s++) dv->cellValid[s] = -1;
 	for (int s = 0; s < p->nSpecies; s++) {
 		long a = p->iStart[s], n = p->iStop[s] - a;
 		if (n <= 0) continue;

@@ -97,17 +97,20 @@ static void sort_tiles(Population *pop) {
 		out.v[d] = dv->altV[d];
 	}
 	for (int s = 0; s < pop->nSpecies; s++) {
-		long nTiles = 0;
-		int rc = pinc_hip_sort_tiles(p, out, s, dv->geom, dv->tileWidth, dv->sortWork, dv->sortWorkCap, &nTiles,
+		long nKeys = 0;
+		int rc = pinc_hip_sort_tiles(p, out, s, dv->geom, dv->tileWidth, dv->sortWork[s], dv->sortWorkCap[s], &nKeys,
 		                             g_pinc.stream);
-		if (rc && 2 * (nTiles + 1) > dv->sortWorkCap) {
-			pinc_hip_free(dv->sortWork);
-			dv->sortWorkCap = 2 * (nTiles + 1);
-			pinc_check(pinc_hip_malloc((void **)&dv->sortWork, dv->sortWorkCap * sizeof(int)), "sort work");
-			rc = pinc_hip_sort_tiles(p, out, s, dv->geom, dv->tileWidth, dv->sortWork, dv->sortWorkCap, &nTiles,
+		long need = 2 * (nKeys + 1) + 2 * (nKeys / 4096 + 1) + 1;
+		if (rc && need > dv->sortWorkCap[s]) {
+			pinc_hip_free(dv->sortWork[s]);
+			dv->sortWorkCap[s] = need;
+			pinc_check(pinc_hip_malloc((void **)&dv->sortWork[s], need * sizeof(int)), "sort work");
+			rc = pinc_hip_sort_tiles(p, out, s, dv->geom, dv->tileWidth, dv->sortWork[s], dv->sortWorkCap[s], &nKeys,
 			                         g_pinc.stream);
 		}
 		pinc_check(rc, "sort tiles");
+		dv->sortKeys = nKeys;
+		dv->cellValid[s] = pop->iStop[s] - pop->iStart[s];
 	}
 	for (int d = 0; d < pop->nDims; d++) {
 		double *t = dv->p.x[d];
@@ -168,6 +171,8 @@ static void extract(Population *pop, MpiInfo *m) {
 			break;
 		}
 		pop->iStop[s] -= dv->nEmig[s];
+		if (dv->tiled && dv->cellValid[s] > pop->iStop[s] - pop->iStart[s])
+			dv->cellValid[s] = pop->iStop[s] - pop->iStart[s];
 		for (int ne = 0; ne < nN; ne++) m->nEmigrants[ne * ns + s] = dv->neCount[s][ne];
 	}
 	dv->flagsValid = 0;
@@ -319,7 +324,13 @@ static void distr(const Population *pop, Grid *rho) {
 			pinc_check(pinc_hip_scale2(g->d, g->n, pop->charge[s - 1], 1.0 / pop->charge[s], g_pinc.stream),
 			           "distr scale");
 		int slot = pinc_probe_begin(PINC_PROBE_DEPOSIT);
-		pinc_check(pinc_hip_deposit(p, s, g->geom, g->d, g_pinc.stream), "deposit");
+		PincDevPop *dv = pop->dev;
+		if (dv->tiled && dv->cellValid[s] >= 0)
+			pinc_check(pinc_hip_deposit_cells(p, s, g->geom, dv->tileWidth, dv->sortWork[s] + (dv->sortKeys + 1),
+			                                  dv->cellValid[s], g->d, g_pinc.stream),
+			           "deposit (cells)");
+		else
+			pinc_check(pinc_hip_deposit(p, s, g->geom, g->d, g_pinc.stream), "deposit");
 		/* read pos (8 B per dim per particle) + write rho (8 B per node) */
 		pinc_probe_end(PINC_PROBE_DEPOSIT, slot,
 		               8.0 * pop->nDims * (pop->iStop[s] - pop->iStart[s]) + 8.0 * g->n);

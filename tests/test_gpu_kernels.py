@@ -62,3 +62,55 @@ def test_fused_sweep_equals_two_passes(hip, shape):
 def test_fused_sweep_rejects_untiled_level(hip):
     L = Lvl(3, (C.c_int * 3)(24, 16, 16))
     assert hip.pinc_hip_gs_sweep(None, None, None, L, None) != 0
+
+
+class Geom(C.Structure):
+    _fields_ = [("nd", C.c_int), ("T", C.c_int * 3), ("nloc", C.c_int), ("off", C.c_int), ("nranks", C.c_int)]
+
+
+class Pop(C.Structure):
+    _fields_ = [("x", C.c_void_p * 3), ("v", C.c_void_p * 3), ("nSpecies", C.c_int), ("nd", C.c_int),
+                ("iStart", C.c_long * 9), ("iStop", C.c_long * 8)]
+
+
+@pytest.mark.parametrize("n,T,start", [(100_000, (16, 16, 16), 0), (77_777, (32, 16, 8), 13), (5, (8, 8, 8), 1)])
+def test_cell_sort(hip, n, T, start):
+    """pinc_hip_sort_tiles: a permutation of the particles, ordered by the
+    tile-major cell key, with pos and vel moved together."""
+    import torch
+    rng = np.random.default_rng(n)
+    cap = start + n + 3
+    pos = [torch.zeros(cap, dtype=torch.float64) for _ in range(3)]
+    vel = [torch.zeros(cap, dtype=torch.float64) for _ in range(3)]
+    for d in range(3):
+        pos[d][start:start + n] = torch.from_numpy(0.1 + rng.random(n) * (T[d] + 0.8))
+        vel[d][start:start + n] = torch.from_numpy(rng.standard_normal(n))
+    pos = [p.cuda() for p in pos]
+    vel = [v.cuda() for v in vel]
+    out_p = [torch.zeros_like(p) for p in pos]
+    out_v = [torch.zeros_like(v) for v in vel]
+    pop = Pop((C.c_void_p * 3)(*[p.data_ptr() for p in pos]), (C.c_void_p * 3)(*[v.data_ptr() for v in vel]),
+              1, 3, (C.c_long * 9)(start, start + n + 3), (C.c_long * 8)(start + n))
+    out = Pop((C.c_void_p * 3)(*[p.data_ptr() for p in out_p]), (C.c_void_p * 3)(*[v.data_ptr() for v in out_v]),
+              1, 3, (C.c_long * 9)(start, start + n + 3), (C.c_long * 8)(start + n))
+    g = Geom(3, (C.c_int * 3)(*T), T[2], 0, 1)
+    hip.pinc_hip_sort_tiles.argtypes = [Pop, Pop, C.c_int, Geom, C.c_int, C.c_void_p, C.c_long,
+                                        C.POINTER(C.c_long), C.c_void_p]
+    nk = C.c_long()
+    assert hip.pinc_hip_sort_tiles(pop, out, 0, g, 4, None, 0, C.byref(nk), None) != 0
+    need = 2 * (nk.value + 1) + 2 * (nk.value // 4096 + 1) + 1
+    work = torch.zeros(need, dtype=torch.int32, device="cuda")
+    assert hip.pinc_hip_sort_tiles(pop, out, 0, g, 4, work.data_ptr(), need, C.byref(nk), None) == 0
+    torch.cuda.synchronize()
+    P = np.stack([p.cpu().numpy()[start:start + n] for p in out_p], 1)
+    V = np.stack([v.cpu().numpy()[start:start + n] for v in out_v], 1)
+    P0 = np.stack([p.cpu().numpy()[start:start + n] for p in pos], 1)
+    V0 = np.stack([v.cpu().numpy()[start:start + n] for v in vel], 1)
+    c = P.astype(int)
+    nt = [(t + 1) // 4 + 1 for t in T]
+    tile = (c[:, 0] // 4) + nt[0] * ((c[:, 1] // 4) + nt[1] * (c[:, 2] // 4))
+    key = tile * 64 + (c[:, 0] % 4) + 4 * ((c[:, 1] % 4) + 4 * (c[:, 2] % 4))
+    assert np.all(np.diff(key) >= 0)
+    a = np.concatenate([P, V], 1)
+    b = np.concatenate([P0, V0], 1)
+    np.testing.assert_array_equal(a[np.lexsort(a.T[::-1])], b[np.lexsort(b.T[::-1])])
