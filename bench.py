@@ -74,8 +74,11 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--size", type=int, default=256, help="global cells per dimension")
-    ap.add_argument("--ppc", type=int, default=64)
+    ap.add_argument("--workload", default="c4", choices=["c4", "c3"],
+                    help="c4: warm 3-D plasma, 256^3, 64 ppc, multigrid (BASELINE.json metric, default); "
+                         "c3: Maxwellian 128^3, 32 ppc, spectral (rocFFT) Poisson solve")
+    ap.add_argument("--size", type=int, default=None, help="global cells per dimension (c4: 256, c3: 128)")
+    ap.add_argument("--ppc", type=int, default=None, help="particles per cell per species (c4: 64, c3: 32)")
     ap.add_argument("--mg", default="native", choices=["native", "reference"],
                     help="native: correction-scheme V-cycle with the coarse h^2 factor (default; the reference "
                          "algorithm does not converge at 256^3 with 5 levels, DESIGN.md section 6); reference: "
@@ -113,10 +116,15 @@ def main() -> int:
         dist.broadcast_object_list(obj, src=0)
         comm_id = obj[0]
 
+    c3 = args.workload == "c3"
+    if args.size is None:
+        args.size = 128 if c3 else 256
+    if args.ppc is None:
+        args.ppc = 32 if c3 else 64
     S = args.size
     if S % world:
         raise SystemExit("grid size must divide by the GPU count")
-    cfg = configs.config("warm", true_size=(S, S, S // world), nsub=(1, 1, world), ppc=args.ppc,
+    cfg = configs.config("c3" if c3 else "warm", true_size=(S, S, S // world), nsub=(1, 1, world), ppc=args.ppc,
                          nalloc_pc=args.ppc + 8)
     if args.mg == "native":
         cfg["multigrid"]["native"] = "1"
@@ -186,6 +194,7 @@ def main() -> int:
     push_ms = (phases["move"] + phases["extract"] + phases["migrate"] + phases["deposit"] +
                phases["accelerate"]) / K
     kernels = {}
+    ROCPROF_NAMES["spectral"] = "k_spectral_scale + rocFFT r2c/c2r kernels"
     if args.mg == "native":
         ROCPROF_NAMES["gs_pass"] = "k_gs_sweep"  # one fused red-black iteration per launch
     for k, p in probes.items():
@@ -216,7 +225,8 @@ def main() -> int:
         "dtype": "f64",
         "data": "synthetic (lattice positions, Maxwellian velocities from a seeded counter RNG)",
         "config": {
-            "workload": f"C4 warm 3-D two-species plasma, {S}^3 grid, {args.ppc} ppc per species "
+            "workload": (f"C3 Maxwellian 3-D two-species plasma" if c3 else "C4 warm 3-D two-species plasma")
+                        + f", {S}^3 grid, {args.ppc} ppc per species "
                         f"({n_total} particles), 1D slab decomposition 1,1,{world}",
             "grid": [S, S, S],
             "ppc_per_species": args.ppc,
@@ -224,9 +234,10 @@ def main() -> int:
             "particles": n_total,
             "decomposition": f"1,1,{world}",
             "layout": args.layout + (f" (tile sort every {args.sort_interval} steps)" if args.layout == "tiled" else ""),
-            "poisson": "multigrid mgVRecursive, 5 levels, RB Gauss-Seidel 10/10/10, "
-                       + ("native mode (correction scheme, coarse h^2 factor)" if args.mg == "native"
-                          else "reference algorithm (parity mode)"),
+            "poisson": ("spectral (sSolver, rocFFT r2c/c2r, global grid)" if c3 else
+                        "multigrid mgVRecursive, 5 levels, RB Gauss-Seidel 10/10/10, "
+                        + ("native mode (correction scheme, coarse h^2 factor)" if args.mg == "native"
+                           else "reference algorithm (parity mode)")),
         },
         "poisson_ms_per_step": solve_ms,
         "push_deposit_ms_per_step": push_ms,

@@ -186,6 +186,16 @@ void mgFreeSolver(MultigridSolver *solver);
 void mgSolve(MultigridSolver *solver, Grid *rho, Grid *phi, const MpiInfo *mpiInfo);
 long mgCycleCount(const MultigridSolver *solver);
 
+/* ---------------------------------------------------------- spectral -- */
+/* spectral.c:14-115; N-D extension of the reference's 1-D solver on rocFFT */
+typedef struct SpectralSolver SpectralSolver;
+void sSolver(void (**solve)(), void *(**solverAlloc)(), void (**solverFree)());
+funPtr sSolver_set(dictionary *ini);
+SpectralSolver *sAlloc(const dictionary *ini, Grid *rho, Grid *phi);
+void sFree(SpectralSolver *solver);
+void sSolve(SpectralSolver *solver, Grid *rho, Grid *phi, const MpiInfo *mpiInfo);
+long sSolveCount(const SpectralSolver *solver);
+
 /* ---------------------------------------------------------- run mode -- */
 void regular(dictionary *ini);
 funPtr regular_set(dictionary *ini);
@@ -242,7 +252,8 @@ int pinc_sim_timers_reset(PincSim *sim);
 #define PINC_PROBE_MOVE 2      /* move + classify */
 #define PINC_PROBE_DEPOSIT 3   /* charge deposit */
 #define PINC_PROBE_RESIDUAL 4  /* residual norm, finest level */
-#define PINC_NPROBES 5
+#define PINC_PROBE_SPECTRAL 5  /* spectral solve (r2c + scale + c2r) */
+#define PINC_NPROBES 6
 #define PINC_PROBE_ALL (-1)
 int pinc_probe_start(int kernel, int maxSamples);
 int pinc_probe_read(int kernel, double *meanMs, double *meanBytes, int *samples, long *launches);

@@ -244,6 +244,17 @@ int pinc_hip_restrict(const double *fine, double *coarse, pinc_lvl_t Lc, int nd3
 /* mgBilinProl3D/ND + gAddTo (multigrid.c:1024-1238, 1535): phi_f += P(phi_c) */
 int pinc_hip_prolong_add(double *phiFine, const double *phiCoarse, pinc_lvl_t Lf, void *stream);
 
+/* ---------------------------------------------------------- spectral -- */
+/* Spectral Poisson solve on rocFFT, replacing sAlloc/sSolve/sFree
+ * (spectral.c:14-52, 92-115).  T is the global true size (x fastest, x
+ * even).  pinc_hip_fft_poisson reads the global rho [Tz][Ty][Tx] (left
+ * unchanged) and writes the global phi: r2c, DC := 0, multiply by
+ * (N/(2 pi n))^2/N in 1-D (spectral.c:29-37) or 1/|k|^2/N in 2-D/3-D, c2r. */
+typedef struct pinc_fft_s pinc_fft_t;
+int pinc_hip_fft_create(pinc_fft_t **plan, int nd, const int *T, void *stream);
+int pinc_hip_fft_poisson(pinc_fft_t *plan, const double *rhoGlobal, double *phiGlobal, void *stream);
+void pinc_hip_fft_destroy(pinc_fft_t *plan);
+
 /* ------------------------------------------------------------ comm -- */
 /* RCCL communicator over xGMI (one process per GPU).  id is the 128-byte
  * ncclUniqueId produced by pinc_hip_comm_unique_id on rank 0 and

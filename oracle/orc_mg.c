@@ -262,7 +262,10 @@ void ow_mg_solve(OWorld *w){
 /* 1-D spectral Poisson solve by direct DFT (N is small in the 1-D configs).
  * FFTW's r2c/c2r are unnormalised; the factor (N/2 pi n)^2/N carries the
  * 1/N.  c2r ignores the imaginary part of the DC and Nyquist bins. */
+static void ow_spectral_solve_nd(OWorld *w);
+
 void ow_spectral_solve(OWorld *w){
+	if(w->nDims != 1 || w->P != 1){ ow_spectral_solve_nd(w); return; }
 	OGrid *rho = &w->r[0].rho, *phi = &w->r[0].phi;
 	int N = rho->trueSize[1];
 	int M = N/2 + 1;
@@ -287,6 +290,107 @@ void ow_spectral_solve(OWorld *w){
 			if(2*n == N) v += term; else v += 2*term;
 		}
 		phi->val[g+x] = v;
+	}
+	free(re); free(im);
+	w->solves++;
+}
+
+/* N-D extension of sSolve (the reference is 1-D only, spectral.c:80-89):
+ * phi = IDFT(DFT(rho) * f(k)), f = 1/|k|^2/N with k_d = 2 pi n_d/N_d over the
+ * signed frequencies, f(0) = 0, on the global periodic grid gathered from
+ * every emulated rank's true nodes.  The full complex spectrum is used, one
+ * naive DFT along each dimension (separable), which in exact arithmetic
+ * equals the r2c/c2r pair of the build.  Ghosts are left to the TOHALO that
+ * follows every solve (main.c:240). */
+static void dft_axis(double *re, double *im, const int *L, int axis, int sign){
+	long stride = 1;
+	for(int d = 0; d < axis; d++) stride *= L[d];
+	int n = L[axis];
+	long outer = 1;
+	for(int d = 0; d < 3; d++) if(d != axis) outer *= L[d];
+	double *cr = malloc(n*sizeof(double)), *ci = malloc(n*sizeof(double));
+	double *tr = malloc(n*sizeof(double)), *ti = malloc(n*sizeof(double));
+	for(int k = 0; k < n; k++){
+		cr[k] = cos(2.0*M_PI*k/n);
+		ci[k] = sign*sin(2.0*M_PI*k/n);
+	}
+	for(long o = 0; o < outer; o++){
+		/* base index of the line: decompose o over the other axes */
+		long base = 0, r = o, s = 1;
+		for(int d = 0; d < 3; d++){
+			if(d == axis){ s *= L[d]; continue; }
+			base += (r % L[d])*s;
+			r /= L[d];
+			s *= L[d];
+		}
+		for(int k = 0; k < n; k++){
+			double a = 0, b = 0;
+			for(int x = 0; x < n; x++){
+				int t = (int)(((long)k*x) % n);
+				double vr = re[base + x*stride], vi = im[base + x*stride];
+				a += vr*cr[t] - vi*ci[t];
+				b += vr*ci[t] + vi*cr[t];
+			}
+			tr[k] = a; ti[k] = b;
+		}
+		for(int k = 0; k < n; k++){ re[base + k*stride] = tr[k]; im[base + k*stride] = ti[k]; }
+	}
+	free(cr); free(ci); free(tr); free(ti);
+}
+
+/* global index <-> rank-local padded index (x fastest, ghosts g per side) */
+static long local_index(const OGrid *g, const int *p){
+	long i = 0;
+	for(int d = 0; d < g->rank - 1; d++) i += (long)(p[d] + g->nGhost[d+1])*g->sizeProd[d+1];
+	return i;
+}
+
+static void ow_spectral_solve_nd(OWorld *w){
+	int nd = w->nDims;
+	int L[3] = {1, 1, 1};
+	const OMpi *m0 = &w->r[0].mpi;
+	for(int d = 0; d < nd; d++) L[d] = w->r[0].rho.trueSize[d+1]*m0->nSubdomains[d];
+	long N = (long)L[0]*L[1]*L[2];
+	double *re = calloc(N, sizeof(double)), *im = calloc(N, sizeof(double));
+	for(int r = 0; r < w->P; r++){
+		const OGrid *rho = &w->r[r].rho;
+		const OMpi *m = &w->r[r].mpi;
+		int t[3] = {1, 1, 1};
+		for(int d = 0; d < nd; d++) t[d] = rho->trueSize[d+1];
+		for(int z = 0; z < t[2]; z++) for(int y = 0; y < t[1]; y++) for(int x = 0; x < t[0]; x++){
+			int p[3] = {x, y, z};
+			long gi = 0, s = 1;
+			for(int d = 0; d < nd; d++){ gi += (long)(m->subdomain[d]*t[d] + p[d])*s; s *= L[d]; }
+			re[gi] = rho->val[local_index(rho, p)];
+		}
+	}
+	for(int d = 0; d < nd; d++) dft_axis(re, im, L, d, -1);
+	for(long i = 0; i < N; i++){
+		long r = i;
+		double k2 = 0;
+		for(int d = 0; d < nd; d++){
+			int n = (int)(r % L[d]);
+			r /= L[d];
+			if(n > L[d]/2) n -= L[d];
+			double k = 2*M_PI*n/L[d];
+			k2 += k*k;
+		}
+		double f = 0;
+		if(i){ f = 1.0/k2; f /= N; }
+		re[i] *= f; im[i] *= f;
+	}
+	for(int d = 0; d < nd; d++) dft_axis(re, im, L, d, +1);
+	for(int r = 0; r < w->P; r++){
+		OGrid *phi = &w->r[r].phi;
+		const OMpi *m = &w->r[r].mpi;
+		int t[3] = {1, 1, 1};
+		for(int d = 0; d < nd; d++) t[d] = phi->trueSize[d+1];
+		for(int z = 0; z < t[2]; z++) for(int y = 0; y < t[1]; y++) for(int x = 0; x < t[0]; x++){
+			int p[3] = {x, y, z};
+			long gi = 0, s = 1;
+			for(int d = 0; d < nd; d++){ gi += (long)(m->subdomain[d]*t[d] + p[d])*s; s *= L[d]; }
+			phi->val[local_index(phi, p)] = re[gi];
+		}
 	}
 	free(re); free(im);
 	w->solves++;

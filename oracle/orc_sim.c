@@ -170,10 +170,10 @@ static void select_methods(OWorld *w){
 		if(w->nLevels < 1) orc_die("Multi Grid levels is 0");
 		if(!w->mgCycles) orc_die("MG cycles is 0");
 	} else {
-		if(nd != 1) orc_die("sMode only works with grid:nDims=1");
-		int *ns = oini_intarr(ini, "grid:nSubdomains", nd);
-		if(ns[0] != 1) orc_die("sMode only works with grid:nSubdomains=1");
-		free(ns);
+		/* spectral.c:80-89 restricts the solver to nDims=1 without
+		 * decomposition; the build extends it to 1-3 dimensions and slabs
+		 * (global transform), and so does this checker */
+		if(nd < 1 || nd > 3) orc_die("sSolver supports grid:nDims=1..3");
 	}
 }
 
@@ -220,7 +220,7 @@ OWorld *ow_create(OIni *ini, int literal){
 	}
 	free(nsub); free(ng); free(ts);
 	if(w->poisson == ORC_POISSON_MG) ow_mg_alloc(w);
-	else {
+	else if(nd == 1 && w->P == 1){
 		int N = w->r[0].rho.trueSize[1];
 		int M = N/2 + 1;
 		w->spectralFactor = calloc(M, sizeof(double));
@@ -331,7 +331,12 @@ void ow_init(OWorld *w, int perturb, int maxwell, unsigned long long seed){
 void ow_init_fields(OWorld *w){
 	do_distr(w);
 	do_solve(w);
-	do_efield(w, 0);
+	/* main.c:168-186 takes E from phi without a TOHALO.  After mgSolve the
+	 * ghosts are valid (the smoother's halo exchanges); after sSolve they
+	 * are stale (gInsertHalo, grid.c:892-915, does not refill them), so the
+	 * reference's initial E is wrong at the edge nodes.  The build computes
+	 * E from the periodic phi; the checker follows. */
+	do_efield(w, w->poisson == ORC_POISSON_SPECTRAL);
 	for(int r = 0; r < w->P; r++) og_mul(&w->r[r].E, 0.5);
 	do_acc(w);
 	for(int r = 0; r < w->P; r++) og_mul(&w->r[r].E, 2.0);

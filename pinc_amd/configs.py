@@ -10,6 +10,9 @@ the values of the reference inputs and the overrides of SURVEY.md 8(d):
   cold3d       langmuirCold.ini (3-D 32x16x16 per subdomain, 64 ppc)
   warm         warm_big.ini family: 3-D warm Maxwellian plasma, 64 ppc
                (config C4 at 256^3; bench.py sizes it per GPU count)
+  c3           input/maxwellian.ini family (config C3): 3-D Maxwellian,
+               128^3, 32 ppc, v_th,e = 0.05 cells/step, spectral Poisson
+               solve (methods:poisson = sSolver, spectral.c)
 """
 from __future__ import annotations
 
@@ -113,6 +116,13 @@ def config(name: str, **kw) -> dict:
         return _cold3d(**kw)
     if name == "warm":
         return _warm(**kw)
+    if name == "c3":
+        kw.setdefault("true_size", (128, 128, 128))
+        kw.setdefault("ppc", 32)
+        kw.setdefault("nalloc_pc", kw["ppc"] + 8)
+        c = _warm(**kw)
+        c["methods"]["poisson"] = "sSolver"
+        return c
     raise KeyError(name)
 
 

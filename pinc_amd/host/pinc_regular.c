@@ -27,7 +27,10 @@ struct PincSim {
 	MpiInfo *mpi;
 	Population *pop;
 	Grid *E, *rho, *phi;
-	MultigridSolver *solver;
+	void *solver;
+	void (*solve)(void *, Grid *, Grid *, const MpiInfo *);
+	void (*solverFree)(void *);
+	int spectral;
 	void (*acc)(Population *, Grid *);
 	void (*distr)(const Population *, Grid *);
 	void (*extractEmigrants)(Population *, MpiInfo *);
@@ -69,7 +72,7 @@ static PincSim *sim_build(dictionary *ini, const PincSimOpts *opts) {
 	S->distr = (void (*)(const Population *, Grid *))select(ini, "methods:distr", puDistr3D1_set, puDistrND1_set);
 	S->extractEmigrants = (void (*)(Population *, MpiInfo *))select(ini, "methods:migrate", puExtractEmigrants3D_set,
 	                                                                puExtractEmigrantsND_set);
-	void (*solverInterface)() = select(ini, "methods:poisson", mgSolver_set);
+	void (*solverInterface)() = select(ini, "methods:poisson", mgSolver_set, sSolver_set);
 	void (*solve)() = NULL;
 	void *(*solverAlloc)() = NULL;
 	void (*solverFree)() = NULL;
@@ -82,7 +85,10 @@ static PincSim *sim_build(dictionary *ini, const PincSimOpts *opts) {
 	S->E = gAlloc(ini, VECTOR);
 	S->rho = gAlloc(ini, SCALAR);
 	S->phi = gAlloc(ini, SCALAR);
-	S->solver = (MultigridSolver *)((void *(*)(const dictionary *, Grid *, Grid *))solverAlloc)(ini, S->rho, S->phi);
+	S->solver = ((void *(*)(const dictionary *, Grid *, Grid *))solverAlloc)(ini, S->rho, S->phi);
+	S->solve = (void (*)(void *, Grid *, Grid *, const MpiInfo *))solve;
+	S->solverFree = (void (*)(void *))solverFree;
+	S->spectral = solve == (void (*)())sSolve;
 	gCreateNeighborhood(ini, S->mpi, S->rho);
 	gSetBndSlices(S->phi, S->mpi);
 	g_pinc.maxVel = iniHas(ini, "population:maxVel") ? iniGetDouble(ini, "population:maxVel") : INFINITY;
@@ -108,7 +114,7 @@ static void sim_fields(PincSim *S) {
 	/* main.c:168-186 */
 	S->distr(S->pop, S->rho);
 	gHaloOp((funPtr)addSlice, S->rho, S->mpi, FROMHALO);
-	mgSolve(S->solver, S->rho, S->phi, S->mpi);
+	S->solve(S->solver, S->rho, S->phi, S->mpi);
 	pinc_phase_begin(5);
 	gFinDiff1st(S->phi, S->E);
 	gHaloOp((funPtr)setSlice, S->E, S->mpi, TOHALO);
@@ -128,9 +134,9 @@ static void sim_step(PincSim *S) {
 	gHaloOp((funPtr)addSlice, S->rho, S->mpi, FROMHALO);
 	if (S->opts.literal) {
 		gHaloOp((funPtr)addSlice, S->rho, S->mpi, FROMHALO);
-		mgSolve(S->solver, S->rho, S->phi, S->mpi);
+		S->solve(S->solver, S->rho, S->phi, S->mpi);
 	}
-	mgSolve(S->solver, S->rho, S->phi, S->mpi);
+	S->solve(S->solver, S->rho, S->phi, S->mpi);
 	pinc_phase_begin(5);
 	gHaloOp((funPtr)setSlice, S->phi, S->mpi, TOHALO);
 	gFinDiff1st(S->phi, S->E);
@@ -148,7 +154,7 @@ static void sim_step(PincSim *S) {
 
 static void sim_free(PincSim *S) {
 	if (!S) return;
-	mgFreeSolver(S->solver);
+	if (S->solverFree) S->solverFree(S->solver);
 	gFree(S->E);
 	gFree(S->rho);
 	gFree(S->phi);
@@ -218,7 +224,7 @@ int pinc_sim_op(PincSim *S, const char *op) {
 	else if (!strcmp(op, "distr")) {
 		S->distr(S->pop, S->rho);
 		gHaloOp((funPtr)addSlice, S->rho, S->mpi, FROMHALO);
-	} else if (!strcmp(op, "solve")) mgSolve(S->solver, S->rho, S->phi, S->mpi);
+	} else if (!strcmp(op, "solve")) S->solve(S->solver, S->rho, S->phi, S->mpi);
 	else if (!strcmp(op, "efield")) {
 		gHaloOp((funPtr)setSlice, S->phi, S->mpi, TOHALO);
 		gFinDiff1st(S->phi, S->E);
@@ -256,7 +262,10 @@ int pinc_sim_energy(PincSim *S, double *ke, double *pe, double *keSpecies) {
 	return 0;
 }
 
-long pinc_sim_cycles(const PincSim *S) { return mgCycleCount(S->solver); }
+/* V-cycles run so far (multigrid) or solves (spectral) */
+long pinc_sim_cycles(const PincSim *S) {
+	return S->spectral ? sSolveCount(S->solver) : mgCycleCount(S->solver);
+}
 int pinc_sim_nspecies(const PincSim *S) { return S->pop->nSpecies; }
 int pinc_sim_ndims(const PincSim *S) { return S->pop->nDims; }
 long pinc_sim_pop_count(PincSim *S, int s) { return S->pop->iStop[s] - S->pop->iStart[s]; }

@@ -33,10 +33,12 @@ def _sorted_rows(a):
     return a[np.lexsort(a.T[::-1])]
 
 
-@pytest.mark.parametrize("layout", ["reference", "tiled"])
-def test_two_ranks_one_gpu(built, tmp_path, layout):
+@pytest.mark.parametrize("layout,poisson", [("reference", "mgSolver"), ("tiled", "mgSolver"),
+                                            ("reference", "sSolver")])
+def test_two_ranks_one_gpu(built, tmp_path, layout, poisson):
     cfg = configs.config("cold3d", true_size=(16, 16, 8), nsub=(1, 1, 2))
     cfg["multigrid"]["mgLevels"] = "3"
+    cfg["methods"]["poisson"] = poisson
     ini_ref = configs.write_ini(cfg)
     if layout == "tiled":
         cfg["population"]["layout"] = "tiled"
