@@ -195,6 +195,7 @@ def main() -> int:
                phases["accelerate"]) / K
     kernels = {}
     ROCPROF_NAMES["spectral"] = "k_spectral_scale + rocFFT r2c/c2r kernels"
+    ROCPROF_NAMES["push"] = "k_push<3, true, true>"
     if args.mg == "native":
         ROCPROF_NAMES["gs_pass"] = "k_gs_sweep"  # one fused red-black iteration per launch
     for k, p in probes.items():

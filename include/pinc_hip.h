@@ -85,6 +85,22 @@ int pinc_hip_move_classify(pinc_pop_t pop, int s, int doMove, const double *thr,
                            unsigned char *flags, int *chunkCount, double maxVel,
                            int *errFlag, int wrapMask, void *stream);
 
+/* Fused push of species s: optionally puAcc's kick
+ * (kick=1: gather from Es as pinc_hip_accelerate, v += dv, KE partials per
+ * PINC_CHUNK block in kePartial, *nBlocks of them), then puMove's drift,
+ * the classification of pinc_hip_move_classify (flags, chunkCount, errFlag,
+ * wrapMask) and the CIC deposit (puDistr3D1/ND1 weights) of every particle
+ * that stays into the species accumulator rhoS (slab layout, not zeroed
+ * here).  New positions go to xout[d] (may be pop.x[d]). */
+int pinc_hip_push(pinc_pop_t pop, int s, double *const *xout, int kick, pinc_geom_t g, const double *Es,
+                  double *rhoS, const double *thr, unsigned char *flags, int *chunkCount, double maxVel,
+                  int *errFlag, int wrapMask, double *kePartial, int *nBlocks, void *stream);
+/* rho = the reference's per-species chain (gZero; gMul(1/q_s); add species
+ * s; gMul(q_s); pusher.c:512-572) applied to per-species sums acc[s], over
+ * n slab elements */
+int pinc_hip_rho_combine(double *rho, const double *const *acc, const double *charge, int ns, long n,
+                         void *stream);
+
 /* Tiled layout (population:layout = tiled, not in the reference): counting
  * sort of species s by cell, cells grouped in tiles of tileWidth^nd, from
  * pop into out (same ranges); the caller swaps the two.  nKeysOut returns

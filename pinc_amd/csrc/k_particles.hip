@@ -1129,6 +1129,437 @@ __global__ __launch_bounds__(kThreads) void k_deposit_cells(const double *__rest
 	}
 }
 
+// ------------------------------------------------------- fused push -------
+// One pass over a species: [kick: puAcc gather + v += dv + KE (pusher.c:
+// 178-265, 1089-1162)] then drift: puMove (pusher.c:86-119) + the neighbour
+// test of puExtractEmigrants (pusher.c:782-910) + puDistr of every particle
+// that stays (pusher.c:512-638).  Particles that emigrate are deposited after
+// their import (distr's immigrant pass), so the charge is the reference's.
+//
+// Thread t of block b owns particles b*2048 + k*256 + t (k = 0..7): every
+// wave load and store is one contiguous 512-B run.  In a cell-ordered layout
+// the 64 particles of a wave share one or two cells, so the deposit first
+// reduces each large same-cell group across the wave (a transposed butterfly
+// that leaves corner c's sum in lane 8c) and adds it once; the other lanes
+// (particles that changed cell, sparse groups) add their own eight weights.
+// Adds go to an LDS box of the block's cells (ds_add_f64), flushed with one
+// global atomic per touched node; a block whose box exceeds the LDS tile adds
+// to global memory directly.  Only the summation order differs from the
+// serial loop.
+struct PushArgs {
+	const double *xi[3];
+	double *xo[3];       // may alias xi
+	double *v[3];
+	long n;              // particles of the species; pointers start at it
+	pinc_geom_t g;
+	const double *Es;    // kick: E as rescaled for the species (k_field_chain)
+	double *rho;         // species charge accumulator (slab layout)
+	Thr thr;
+	int center, wrapMask;
+	double maxVel;
+	unsigned char *flags;
+	int *chunkCount;
+	int *err;
+	double *kePartial;
+};
+
+// same-cell groups of at least kPushGroupMin lanes (at most kPushGroups of
+// them per wave and item) are summed across the wave before the LDS add
+constexpr int kPushGroupMin = 2;
+constexpr int kPushGroups = 4;
+// 8 waves x 4 particles per thread per PINC_CHUNK block: fewer live VGPRs
+// (px) than 4 waves x 8, so more waves per SIMD hide the gather latency
+constexpr int kPushThreads = 512;
+constexpr int kPushItems = PINC_CHUNK / kPushThreads;
+
+// double-precision lane exchange helpers on the two 32-bit halves
+__device__ __forceinline__ void permlane32_swap(double &a, double &b) {
+	// v_permlane32_swap_b32: lanes 32..63 of a <-> lanes 0..31 of b
+	unsigned long long ua = __double_as_longlong(a), ub = __double_as_longlong(b);
+	auto lo = __builtin_amdgcn_permlane32_swap((unsigned)ua, (unsigned)ub, false, false);
+	auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(ua >> 32), (unsigned)(ub >> 32), false, false);
+	a = __longlong_as_double((long long)(((unsigned long long)hi[0] << 32) | lo[0]));
+	b = __longlong_as_double((long long)(((unsigned long long)hi[1] << 32) | lo[1]));
+}
+__device__ __forceinline__ void permlane16_swap(double &a, double &b) {
+	// v_permlane16_swap_b32: odd rows of a <-> even rows of b (rows of 16 lanes)
+	unsigned long long ua = __double_as_longlong(a), ub = __double_as_longlong(b);
+	auto lo = __builtin_amdgcn_permlane16_swap((unsigned)ua, (unsigned)ub, false, false);
+	auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(ua >> 32), (unsigned)(ub >> 32), false, false);
+	a = __longlong_as_double((long long)(((unsigned long long)hi[0] << 32) | lo[0]));
+	b = __longlong_as_double((long long)(((unsigned long long)hi[1] << 32) | lo[1]));
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp(double v) {
+	unsigned long long u = __double_as_longlong(v);
+	unsigned lo = __builtin_amdgcn_update_dpp(0u, (unsigned)u, CTRL, 0xf, 0xf, false);
+	unsigned hi = __builtin_amdgcn_update_dpp(0u, (unsigned)(u >> 32), CTRL, 0xf, 0xf, false);
+	return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+constexpr int kDppRowRor8 = 0x128, kDppHalfMirror = 0x141, kDppQuadXor2 = 0x4e, kDppQuadXor1 = 0xb1;
+
+// sum of r[0..7] over the 64 lanes, transposed: afterwards lane l holds the
+// total of corner 4*b5 + 2*b4 + b3 (b = bits of l) in lanes with (l & 7) == 0
+__device__ __forceinline__ double wave_reduce8(double *r) {
+	const int lane = threadIdx.x & 63;
+	// lanes 0..31 gather corners 0..3, lanes 32..63 corners 4..7
+	double a[4];
+#pragma unroll
+	for (int i = 0; i < 4; i++) {
+		double x = r[i], y = r[i + 4];
+		permlane32_swap(x, y);
+		a[i] = x + y;
+	}
+	// rows 0,2 gather a[0..1], rows 1,3 a[2..3]
+	double b[2];
+#pragma unroll
+	for (int i = 0; i < 2; i++) {
+		double x = a[i], y = a[i + 2];
+		permlane16_swap(x, y);
+		b[i] = x + y;
+	}
+	// half rows: lanes with bit 3 clear keep b[0], set keep b[1]
+	const bool h3 = lane & 8;
+	double send = h3 ? b[0] : b[1];
+	double keep = h3 ? b[1] : b[0];
+	double c = keep + dpp<kDppRowRor8>(send);
+	// total over the 8 lanes of each group
+	c += dpp<kDppHalfMirror>(c);
+	c += dpp<kDppQuadXor2>(c);
+	c += dpp<kDppQuadXor1>(c);
+	return c;
+}
+
+// storage offsets (in nodes, 32-bit) of padded node coordinates j and j+1
+// along dimension d of the slab (periodic x/y stored without ghosts)
+struct Geo32 {
+	int T[3];
+	int stride[3];
+	int slab;
+};
+__device__ __forceinline__ Geo32 make_geo32(const pinc_geom_t &g) {
+	Geo32 r;
+	r.slab = g.nd - 1;
+	int s = 1;
+#pragma unroll
+	for (int d = 0; d < 3; d++) {
+		r.T[d] = (d == r.slab) ? g.nloc : g.T[d];
+		r.stride[d] = s;
+		if (d < g.nd) s *= (d == r.slab) ? (g.nloc + 2) : r.T[d];
+	}
+	return r;
+}
+// (node coordinates and strides are < 2^24: 24-bit multiplies, full rate)
+__device__ __forceinline__ int mul24(int a, int b) { return (int)__umul24((unsigned)a, (unsigned)b); }
+__device__ __forceinline__ void node_pair(const Geo32 &G, int d, int j, int &o0, int &o1) {
+	if (d == G.slab) {
+		o0 = d ? mul24(j, G.stride[d]) : j;
+		o1 = o0 + G.stride[d];
+	} else {
+		// wrap_pad of j and j+1 (padded coordinates 0..T+1)
+		int s0 = j - 1, s1 = j;
+		s0 = s0 < 0 ? s0 + G.T[d] : (s0 >= G.T[d] ? s0 - G.T[d] : s0);
+		s1 = s1 >= G.T[d] ? s1 - G.T[d] : s1;
+		o0 = d ? mul24(s0, G.stride[d]) : s0;
+		o1 = d ? mul24(s1, G.stride[d]) : s1;
+	}
+}
+
+template <int ND, bool V3D, bool KICK>
+__global__ __launch_bounds__(kPushThreads) void k_push(PushArgs a) {
+	constexpr int NC = 1 << ND;
+	__shared__ double acc[kDepCap];
+	__shared__ int red[2 * 3 * (kPushThreads / 64)];
+	__shared__ int box[7];
+	__shared__ double kered[kPushThreads / 64];
+	__shared__ int wcnt[kPushThreads / 64];
+	const Geo32 G = make_geo32(a.g);
+	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+	const long base = (long)blockIdx.x * PINC_CHUNK;
+
+	double px[kPushItems][ND];  // post-move positions of the particles that stay
+	unsigned dep = 0;
+	int lo[3] = {INT32_MAX, INT32_MAX, INT32_MAX}, hi[3] = {INT32_MIN, INT32_MIN, INT32_MIN};
+	double ke = 0.0;
+	int cnt = 0, bad = 0;
+
+	// ---- phase 1: kick, drift, classify, store (unrolled: px stays in VGPRs)
+#pragma unroll
+	for (int k = 0; k < kPushItems; k++) {
+		const long i = base + k * kPushThreads + threadIdx.x;
+		if (i >= a.n) continue;
+		double p[ND], vv[ND];
+#pragma unroll
+		for (int d = 0; d < ND; d++) {
+			p[d] = a.xi[d][i];
+			vv[d] = a.v[d][i];
+		}
+		if (KICK) {
+			double dec[3], comp[3];
+			int o[3][2];
+#pragma unroll
+			for (int d = 0; d < ND; d++) {
+				int j = (int)p[d];
+				dec[d] = p[d] - j;
+				comp[d] = 1 - dec[d];
+				node_pair(G, d, j, o[d][0], o[d][1]);
+			}
+			double e[NC][ND];
+#pragma unroll
+			for (int c = 0; c < NC; c++) {
+				int off = 0;
+#pragma unroll
+				for (int d = 0; d < ND; d++) off += o[d][(c >> d) & 1];
+				const double *ep = a.Es + (unsigned)(off * ND);
+#pragma unroll
+				for (int q = 0; q < ND; q++) e[c][q] = ep[q];
+			}
+			double dv[ND];
+			if (V3D) {
+				// puInterp3D1 (pusher.c:1116-1120), corner c = x + 2y + 4z
+				double x = dec[0], y = dec[1], z = dec[2];
+				double xc = comp[0], yc = comp[1], zc = comp[2];
+#pragma unroll
+				for (int q = 0; q < ND; q++)
+					dv[q] = zc * (yc * (xc * e[0][q] + x * e[1][q]) + y * (xc * e[2][q] + x * e[3][q])) +
+					        z * (yc * (xc * e[4][q] + x * e[5][q]) + y * (xc * e[6][q] + x * e[7][q]));
+			} else {
+				// puInterpND1Inner: corner by corner in the recursion order
+#pragma unroll
+				for (int q = 0; q < ND; q++) dv[q] = 0;
+#pragma unroll
+				for (int c = 0; c < (1 << (ND - 1)); c++) {
+					double f = 1.0;
+					int cc = 0;
+#pragma unroll
+					for (int d = ND - 1; d >= 1; d--) {
+						int bit = (c >> (d - 1)) & 1;
+						f = (bit ? dec[d] : comp[d]) * f;
+						cc |= bit << d;
+					}
+#pragma unroll
+					for (int q = 0; q < ND; q++) {
+						dv[q] += comp[0] * f * e[cc][q];
+						dv[q] += dec[0] * f * e[cc | 1][q];
+					}
+				}
+			}
+			double vsq = 0;
+#pragma unroll
+			for (int d = 0; d < ND; d++) {
+				vsq += vv[d] * (vv[d] + dv[d]);
+				vv[d] = vv[d] + dv[d];
+				a.v[d][i] = vv[d];
+			}
+			ke += vsq;
+		}
+		// drift + pVelAssertMax (population.c:342-365)
+#pragma unroll
+		for (int d = 0; d < ND; d++) {
+			bad |= (vv[d] > a.maxVel);
+			p[d] += vv[d];
+		}
+		// neighbour digit per dimension, as k_move_classify
+		int ne = 0;
+#pragma unroll
+		for (int d = ND - 1; d >= 0; d--) {
+			int dig = 1 - (p[d] < a.thr.lo[d]) + (p[d] >= a.thr.up[d]);
+			double q = p[d] - (double)(dig - 1) * (a.thr.hi[d] - 1.0);
+			bad |= (q < 0.0 || q > a.thr.hi[d]) << 1;
+			if ((a.wrapMask >> d) & 1) {
+				if (dig != 1) p[d] = p[d] + (double)((1 - dig) * a.thr.T[d]);
+				dig = 1;
+			}
+			ne = ne * 3 + dig;
+		}
+#pragma unroll
+		for (int d = 0; d < ND; d++) a.xo[d][i] = p[d];
+		a.flags[i] = (unsigned char)ne;
+		if (ne != a.center) {
+			cnt++;
+		} else {
+			dep |= 1u << k;
+#pragma unroll
+			for (int d = 0; d < ND; d++) {
+				px[k][d] = p[d];
+				int jj = (int)p[d];
+				lo[d] = min(lo[d], jj);
+				hi[d] = max(hi[d], jj + 1);
+			}
+		}
+	}
+	if (bad) atomicOr(a.err, bad);
+
+	// ---- phase 2: node box of the block's deposits
+#pragma unroll
+	for (int d = 0; d < ND; d++) {
+		int x = wave_min_i(lo[d]), y = wave_max_i(hi[d]);
+		if (lane == 0) {
+			red[(2 * d) * (kPushThreads / 64) + wv] = x;
+			red[(2 * d + 1) * (kPushThreads / 64) + wv] = y;
+		}
+	}
+	int wc = wave_sum(cnt);
+	if (lane == 0) wcnt[wv] = wc;
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		long vol = 1;
+		bool any = true;
+		for (int d = 0; d < ND; d++) {
+			int x = INT32_MAX, y = INT32_MIN;
+			for (int w = 0; w < kPushThreads / 64; w++) {
+				x = min(x, red[(2 * d) * (kPushThreads / 64) + w]);
+				y = max(y, red[(2 * d + 1) * (kPushThreads / 64) + w]);
+			}
+			any = any && x <= y;
+			box[d] = x;
+			box[3 + d] = y - x + 1;
+			vol *= any ? (long)(y - x + 1) : 0;
+		}
+		box[6] = (any && vol <= kDepCap) ? (int)vol : 0;
+		int t = 0;
+		for (int w = 0; w < kPushThreads / 64; w++) t += wcnt[w];
+		a.chunkCount[blockIdx.x] = t;
+	}
+	__syncthreads();
+	const int vol = box[6];
+	int blo[3] = {0, 0, 0}, bn[3] = {1, 1, 1}, st[3] = {0, 0, 0};
+	if (vol) {
+		int sz = 1;
+#pragma unroll
+		for (int d = 0; d < ND; d++) {
+			blo[d] = box[d];
+			bn[d] = box[3 + d];
+			st[d] = sz;
+			sz *= bn[d];
+		}
+		for (int t = threadIdx.x; t < vol; t += kPushThreads) acc[t] = 0.0;
+		__syncthreads();
+	}
+	// per-dimension offsets of the cell's two node layers: LDS box slots, or
+	// global node offsets when the box does not fit
+	auto layer_offsets = [&](const int *j, int o[3][2]) {
+#pragma unroll
+		for (int d = 0; d < ND; d++) {
+			if (vol) {
+				o[d][0] = d ? mul24(j[d] - blo[d], st[d]) : j[d] - blo[d];
+				o[d][1] = o[d][0] + st[d];
+			} else {
+				node_pair(G, d, j[d], o[d][0], o[d][1]);
+			}
+		}
+	};
+	auto add_at = [&](int off, double w) {
+		if (vol) atomicAdd(&acc[off], w);
+		else unsafeAtomicAdd(&a.rho[(unsigned)off], w);
+	};
+
+	// ---- phase 3: deposit
+	int keyMul[3] = {1, G.T[0] + 2, (G.T[0] + 2) * (G.T[1] + 2)};  // unique cell key
+#pragma unroll
+	for (int k = 0; k < kPushItems; k++) {
+		const bool mine = (dep >> k) & 1u;
+		int j[3] = {0, 0, 0};
+		double w[8];
+#pragma unroll
+		for (int c = 0; c < 8; c++) w[c] = 0.0;
+		int key = -1;
+		if (mine) {
+			double dec[3], comp[3];
+			int kk = 0;
+#pragma unroll
+			for (int d = 0; d < ND; d++) {
+				j[d] = (int)px[k][d];
+				dec[d] = px[k][d] - j[d];
+				comp[d] = 1 - dec[d];
+				kk += d ? mul24(j[d], keyMul[d]) : j[d];
+			}
+			key = kk;
+			cic_weights<ND, V3D>(dec, comp, w);
+		}
+		unsigned long long pend = __ballot(mine);
+		unsigned long long indiv = 0;
+#pragma unroll 1
+		for (int grp = 0; grp < kPushGroups && pend; grp++) {
+			int leader = (grp & 1) ? 63 - __clzll((long long)pend) : __ffsll((long long)pend) - 1;
+			int lk = __shfl(key, leader, 64);
+			unsigned long long m = __ballot(key == lk) & pend;
+			pend &= ~m;
+			if (__popcll(m) < kPushGroupMin) {
+				indiv |= m;
+				continue;
+			}
+			double r[8];
+			const bool in = (m >> lane) & 1ull;
+#pragma unroll
+			for (int c = 0; c < 8; c++) r[c] = in ? w[c] : 0.0;
+			double sum = wave_reduce8(r);
+			const int corner = lane >> 3;
+			int jl[3] = {0, 0, 0};  // leader's cell (read with every lane active)
+#pragma unroll
+			for (int d = 0; d < ND; d++) jl[d] = __shfl(j[d], leader, 64);
+			if ((lane & 7) == 0 && corner < NC) {
+				int o[3][2];
+				layer_offsets(jl, o);
+				int off = 0;
+#pragma unroll
+				for (int d = 0; d < ND; d++) off += o[d][(corner >> d) & 1];
+				add_at(off, sum);
+			}
+		}
+		indiv |= pend;
+		if ((indiv >> lane) & 1ull) {
+			int o[3][2];
+			layer_offsets(j, o);
+#pragma unroll
+			for (int c = 0; c < NC; c++) {
+				int off = 0;
+#pragma unroll
+				for (int d = 0; d < ND; d++) off += o[d][(c >> d) & 1];
+				add_at(off, w[c]);
+			}
+		}
+	}
+
+	if (KICK) {
+		double t = block_sum(ke, kered);
+		if (threadIdx.x == 0) a.kePartial[blockIdx.x] = t;
+	}
+	if (!vol) return;
+	__syncthreads();
+	for (int t = threadIdx.x; t < vol; t += kPushThreads) {
+		double v = acc[t];
+		if (v == 0.0) continue;
+		int r = t;
+		int off = 0;
+#pragma unroll
+		for (int d = 0; d < ND; d++) {
+			int c = r % bn[d];
+			r /= bn[d];
+			int o0, o1;
+			node_pair(G, d, blo[d] + c, o0, o1);
+			off += o0;
+		}
+		unsafeAtomicAdd(&a.rho[(unsigned)off], v);
+	}
+}
+
+// rho = chain of the species accumulators with the reference's rescaling
+// (gZero; per species gMul(1/q), add, gMul(q); pusher.c:512-572)
+struct CombineArgs {
+	const double *acc[PINC_MAX_SPECIES];
+	double q[PINC_MAX_SPECIES];
+	int ns;
+};
+
+__global__ void k_rho_combine(double *__restrict__ rho, CombineArgs c, long n) {
+	for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+		double r = c.acc[0][i];
+		for (int s = 1; s < c.ns; s++) r = (r * c.q[s - 1]) * (1.0 / c.q[s]) + c.acc[s][i];
+		rho[i] = r * c.q[c.ns - 1];
+	}
+}
+
 }  // namespace
 
 // =========================================================== C ABI ========
@@ -1410,4 +1841,66 @@ extern "C" int pinc_hip_deposit_cells(pinc_pop_t pop, int s, pinc_geom_t g, int 
 	pinc_pop_t tail = pop;
 	tail.iStart[s] = b0 + nCell;
 	return pinc_hip_deposit(tail, s, g, rho, stream);
+}
+
+extern "C" int pinc_hip_push(pinc_pop_t pop, int s, double *const *xout, int kick, pinc_geom_t g,
+                             const double *Es, double *rhoS, const double *thr, unsigned char *flags,
+                             int *chunkCount, double maxVel, int *errFlag, int wrapMask, double *kePartial,
+                             int *nBlocks, void *stream) {
+	long n = pop.iStop[s] - pop.iStart[s];
+	*nBlocks = 0;
+	if (n <= 0) return 0;
+	long b0 = pop.iStart[s];
+	int nd = pop.nd;
+	if (nd != g.nd) return set_error(hipErrorInvalidValue, "push: population and grid dimensions differ");
+	PushArgs a;
+	for (int d = 0; d < 3; d++) {
+		a.xi[d] = d < nd ? pop.x[d] + b0 : nullptr;
+		a.xo[d] = d < nd ? xout[d] + b0 : nullptr;
+		a.v[d] = d < nd ? pop.v[d] + b0 : nullptr;
+		a.thr.lo[d] = d < nd ? thr[d] : 0;
+		a.thr.up[d] = d < nd ? thr[nd + d] : 0;
+		a.thr.hi[d] = d < nd ? thr[2 * nd + d] : 0;
+		a.thr.T[d] = d < nd ? (int)(thr[2 * nd + d] - 1.0 + 0.5) : 1;
+	}
+	a.n = n;
+	a.g = g;
+	a.Es = Es;
+	a.rho = rhoS;
+	a.center = 0;
+	for (int d = 0, p = 1; d < nd; d++, p *= 3) a.center += p;
+	a.wrapMask = wrapMask;
+	a.maxVel = maxVel;
+	a.flags = flags + b0;
+	a.chunkCount = chunkCount;
+	a.err = errFlag;
+	a.kePartial = kePartial;
+	unsigned nb = (unsigned)ceil_div(n, PINC_CHUNK);
+	*nBlocks = (int)nb;
+	hipStream_t st = (hipStream_t)stream;
+#define LAUNCH_PUSH(ND, V3D)                                                                          \
+	do {                                                                                              \
+		if (kick) hipLaunchKernelGGL((k_push<ND, V3D, true>), dim3(nb), dim3(kPushThreads), 0, st, a); \
+		else hipLaunchKernelGGL((k_push<ND, V3D, false>), dim3(nb), dim3(kPushThreads), 0, st, a);     \
+	} while (0)
+	if (nd == 3) LAUNCH_PUSH(3, true);
+	else if (nd == 2) LAUNCH_PUSH(2, false);
+	else LAUNCH_PUSH(1, false);
+#undef LAUNCH_PUSH
+	return check_launch("push");
+}
+
+extern "C" int pinc_hip_rho_combine(double *rho, const double *const *acc, const double *charge, int ns, long n,
+                                    void *stream) {
+	if (ns < 1 || ns > PINC_MAX_SPECIES) return set_error(hipErrorInvalidValue, "rho_combine: species");
+	CombineArgs c;
+	c.ns = ns;
+	for (int s = 0; s < PINC_MAX_SPECIES; s++) {
+		c.acc[s] = s < ns ? acc[s] : nullptr;
+		c.q[s] = s < ns ? charge[s] : 1.0;
+	}
+	long nb = ceil_div(n, (long)kThreads * 4);
+	if (nb > 8192) nb = 8192;
+	hipLaunchKernelGGL(k_rho_combine, dim3((unsigned)nb), dim3(kThreads), 0, (hipStream_t)stream, rho, c, n);
+	return check_launch("rho_combine");
 }

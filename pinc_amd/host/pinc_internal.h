@@ -71,6 +71,18 @@ struct PincDevPop {
 	long sortWorkCap[PINC_MAX_SPECIES];
 	long sortKeys;                      /* cells (keys) of the sort */
 	long cellValid[PINC_MAX_SPECIES];   /* particles still in sorted order (-1: no sort yet) */
+	/* fused push (population:fused, default 1): puAcc
+	 * runs kick + drift + classify + deposit in one pass and leaves the moved
+	 * positions in altX until the next puMove swaps them in; the charge of
+	 * the particles that stayed is kept per species in rhoS until puDistr
+	 * adds the immigrants and combines */
+	int fused;
+	int pending;                        /* altX holds the positions after the next move */
+	int depValid;                       /* rhoS holds the last move's deposits */
+	int depExtracted;                   /* ... and extract ran since (depEnd valid) */
+	long depEnd[PINC_MAX_SPECIES];      /* particles [iStart, depEnd) are in rhoS */
+	double *rhoS[PINC_MAX_SPECIES];
+	long rhoN;
 	/* multi-rank migration buffers (AoS records: nd pos, nd vel, ne) */
 	double *sendBuf[2], *recvBuf[2];
 	long sendCap, recvCap;

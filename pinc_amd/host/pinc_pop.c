@@ -88,11 +88,14 @@ Population *pAlloc(const dictionary *ini) {
 		else if (strcmp(lay, "reference")) msg(ERROR, "population:layout must be reference or tiled, not %s", lay);
 		free(lay);
 	}
+	dv->fused = iniHas(ini, "population:fused") ? iniGetInt(ini, "population:fused") : 1;
 	if (dv->tiled) {
 		dv->sortInterval = iniHas(ini, "population:sortInterval") ? iniGetInt(ini, "population:sortInterval") : 4;
 		if (dv->sortInterval < 1) msg(ERROR, "population:sortInterval must be >= 1");
 		dv->tileWidth = nd == 3 ? 4 : (nd == 2 ? 8 : 32);
 		for (int s = 0; s < PINC_MAX_SPECIES; s++) dv->cellValid[s] = -1;
+	}
+	if (dv->tiled || dv->fused) {
 		for (int d = 0; d < nd; d++) {
 			pinc_check(pinc_hip_malloc((void **)&dv->altX[d], cap * sizeof(double)), "pAlloc pos (tiled)");
 			pinc_check(pinc_hip_malloc((void **)&dv->altV[d], cap * sizeof(double)), "pAlloc vel (tiled)");
@@ -144,6 +147,7 @@ void pFree(Population *p) {
 			pinc_hip_free(dv->altX[d]);
 			pinc_hip_free(dv->altV[d]);
 		}
+		for (int s = 0; s < PINC_MAX_SPECIES; s++) pinc_hip_free(dv->rhoS[s]);
 		for (int s = 0; s < PINC_MAX_SPECIES; s++) pinc_hip_free(dv->sortWork[s]);
 		pinc_hip_free(dv->chunkCount);
 		pinc_hip_free(dv->ws[0].chunkOffset);
@@ -329,6 +333,8 @@ void pSyncToDevice(Population *p) {
 	if (!p->pos) msg(ERROR, "pSyncToDevice without host particles");
 	int nd = p->nDims;
 	PincDevPop *dv = p->dev;
+	/* new particles: a pending fused move and its deposits no longer apply */
+	dv->pending = dv->depValid = dv->depExtracted = 0;
 	/* new particle order: the cell ranges of the last tile sort no longer apply */
 	for (int s = 0; s < PINC_MAX_SPECIES; s++) dv->cellValid[s] = -1;
 	for (int s = 0; s < p->nSpecies; s++) {

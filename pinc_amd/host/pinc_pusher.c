@@ -122,13 +122,95 @@ static void sort_tiles(Population *pop) {
 	}
 }
 
+/* tiled layout: re-sort every sortInterval moves (before moving) */
+static void maybe_sort(Population *pop) {
+	PincDevPop *dv = pop->dev;
+	if (dv->tiled && dv->moves++ % dv->sortInterval == 0) sort_tiles(pop);
+}
+
+/* tiled layout: rank-local periodic crossings are wrapped in place */
+static int wrap_mask(const Population *pop) {
+	int nd = pop->nDims;
+	return !pop->dev->tiled ? 0 : (g_pinc.nranks == 1 ? (1 << nd) - 1 : (1 << (nd - 1)) - 1);
+}
+
+/* fused push of every species (pinc_hip_push): kick from E (or none), drift
+ * into xout, classification, deposit of the particles that stay into rhoS */
+static void push_all(Population *pop, Grid *E, double *const *xout) {
+	PincDevPop *dv = pop->dev;
+	pinc_geom_t g = dv->geom;
+	long n = 1;
+	for (int d = 0; d < g.nd; d++) n *= d == g.nd - 1 ? (long)g.nloc + 2 : (long)g.T[d];
+	if (dv->rhoN != n) {
+		for (int s = 0; s < PINC_MAX_SPECIES; s++) {
+			pinc_hip_free(dv->rhoS[s]);
+			dv->rhoS[s] = NULL;
+		}
+		for (int s = 0; s < pop->nSpecies; s++)
+			pinc_check(pinc_hip_malloc((void **)&dv->rhoS[s], n * sizeof(double)), "species charge");
+		dv->rhoN = n;
+	}
+	int nd = pop->nDims;
+	for (int s = 0; s < pop->nSpecies; s++) {
+		pinc_check(pinc_hip_zero(dv->rhoS[s], n, g_pinc.stream), "species charge zero");
+		const double *Es = NULL;
+		if (E) {
+			PincDevGrid *eg = E->dev;
+			if (!eg->scaled) pinc_check(pinc_hip_malloc((void **)&eg->scaled, eg->n * sizeof(double)), "E scaled");
+			pinc_check(pinc_hip_field_chain(eg->d, eg->scaled, eg->n, dv->qm, dv->mq, 1.0, s, g_pinc.stream),
+			           "E chain");
+			Es = eg->scaled;
+		}
+		pinc_pop_t p = pinc_devpop(pop);
+		long np = pop->iStop[s] - pop->iStart[s];
+		int nb = 0;
+		int slot = E ? pinc_probe_begin(PINC_PROBE_PUSH) : -1;
+		pinc_check(pinc_hip_push(p, s, xout, E != NULL, g, Es, dv->rhoS[s], g_pinc.thr, dv->flags,
+		                         dv->chunkCount + dv->chunkBase[s], g_pinc.maxVel, g_pinc.dErr, wrap_mask(pop),
+		                         dv->kePartial, &nb, g_pinc.stream),
+		           "push");
+		/* pos R+W, vel R+W (32 B per dim per particle) + E R (8 B per value
+		 * per node) + rho flush (8 B per node) */
+		if (E) pinc_probe_end(PINC_PROBE_PUSH, slot, 32.0 * nd * np + 8.0 * (nd + 1) * (double)n);
+		if (E) {
+			if (nb > 0) pinc_check(pinc_hip_reduce(dv->kePartial, nb, 1.0, PINC_SLOT(16 + s), g_pinc.stream), "ke");
+			else pinc_check(pinc_hip_memset(PINC_SLOT(16 + s), 0, sizeof(double), g_pinc.stream), "ke");
+		}
+	}
+	dv->depValid = 1;
+	dv->depExtracted = 0;
+}
+
+static void swap_pos(PincDevPop *dv, int nd) {
+	for (int d = 0; d < nd; d++) {
+		double *t = dv->p.x[d];
+		dv->p.x[d] = dv->altX[d];
+		dv->altX[d] = t;
+	}
+}
+
 static void classify(Population *pop, int doMove) {
 	if (!g_pinc.thrSet) msg(ERROR, "gCreateNeighborhood must run before puMove/extract");
 	PincDevPop *dv = pop->dev;
-	if (doMove && dv->tiled && dv->moves++ % dv->sortInterval == 0) sort_tiles(pop);
-	/* tiled layout: rank-local periodic crossings are wrapped in place */
 	int nd = pop->nDims;
-	int wrapMask = !dv->tiled ? 0 : (g_pinc.nranks == 1 ? (1 << nd) - 1 : (1 << (nd - 1)) - 1);
+	if (!doMove) dv->pending = 0; /* flags recomputed for the current positions */
+	if (doMove && dv->pending) {
+		/* the fused puAcc already moved, classified and deposited */
+		swap_pos(dv, nd);
+		dv->pending = 0;
+		dv->flagsValid = 1;
+		dv->depValid = 1;
+		dv->depExtracted = 0;
+		return;
+	}
+	if (doMove) maybe_sort(pop);
+	if (doMove && dv->fused) {
+		push_all(pop, NULL, dv->p.x);
+		dv->flagsValid = 1;
+		return;
+	}
+	dv->depValid = 0;
+	int wrapMask = wrap_mask(pop);
 	pinc_pop_t p = pinc_devpop(pop);
 	for (int s = 0; s < pop->nSpecies; s++) {
 		long n = pop->iStop[s] - pop->iStart[s];
@@ -171,11 +253,13 @@ static void extract(Population *pop, MpiInfo *m) {
 			break;
 		}
 		pop->iStop[s] -= dv->nEmig[s];
+		if (dv->depValid) dv->depEnd[s] = pop->iStop[s];
 		if (dv->tiled && dv->cellValid[s] > pop->iStop[s] - pop->iStart[s])
 			dv->cellValid[s] = pop->iStop[s] - pop->iStart[s];
 		for (int ne = 0; ne < nN; ne++) m->nEmigrants[ne * ns + s] = dv->neCount[s][ne];
 	}
 	dv->flagsValid = 0;
+	if (dv->depValid) dv->depExtracted = 1;
 	pinc_phase_end(1);
 }
 
@@ -317,6 +401,24 @@ void puMigrate(Population *pop, MpiInfo *m, Grid *grid) {
 static void distr(const Population *pop, Grid *rho) {
 	pinc_phase_begin(3);
 	PincDevGrid *g = rho->dev;
+	PincDevPop *dvp = pop->dev;
+	if (dvp->depValid && dvp->depExtracted && dvp->rhoN == g->n) {
+		/* fused push: the particles that stayed are in rhoS; add the ones
+		 * imported since (the tail of each species), then combine */
+		for (int s = 0; s < pop->nSpecies; s++) {
+			if (pop->iStop[s] <= dvp->depEnd[s]) continue;
+			pinc_pop_t t = pinc_devpop(pop);
+			t.iStart[s] = dvp->depEnd[s];
+			pinc_check(pinc_hip_deposit(t, s, g->geom, dvp->rhoS[s], g_pinc.stream), "deposit (immigrants)");
+		}
+		pinc_check(pinc_hip_rho_combine(g->d, (const double *const *)dvp->rhoS, pop->charge, pop->nSpecies, g->n,
+		                                g_pinc.stream),
+		           "rho combine");
+		dvp->depValid = dvp->depExtracted = 0;
+		g->ghostsValid = 0;
+		pinc_phase_end(3);
+		return;
+	}
 	pinc_check(pinc_hip_zero(g->d, g->n, g_pinc.stream), "distr zero");
 	pinc_pop_t p = pinc_devpop(pop);
 	for (int s = 0; s < pop->nSpecies; s++) {
@@ -347,6 +449,22 @@ void puDistrND1(const Population *pop, Grid *rho) { distr(pop, rho); }
 static void acc(Population *pop, Grid *E, int ke) {
 	pinc_phase_begin(6);
 	PincDevPop *dv = pop->dev;
+	if (dv->fused) {
+		/* kick now; the drift of the next puMove, its classification and its
+		 * deposit ride along (positions to altX, swapped in by puMove) */
+		maybe_sort(pop);
+		dv->pending = 0;
+		push_all(pop, E, dv->altX);
+		dv->pending = 1;
+		dv->flagsValid = 0;
+		if (ke) {
+			double sums[PINC_MAX_SPECIES];
+			pinc_check(pinc_hip_d2h(sums, PINC_SLOT(16), pop->nSpecies * sizeof(double), g_pinc.stream), "ke readback");
+			for (int s = 0; s < pop->nSpecies; s++) pop->kinEnergy[s] = sums[s] * (0.5 * pop->mass[s]);
+		}
+		pinc_phase_end(6);
+		return;
+	}
 	pinc_pop_t p = pinc_devpop(pop);
 	int ns = pop->nSpecies;
 	for (int s = 0; s < ns; s++) {

@@ -252,3 +252,37 @@ def test_tiled_layout(sim_cls, name, kw, maxwell):
             assert abs(pe - pe_o) <= 1e-8 * abs(pe_o), (n, pe, pe_o)
             for sp in range(2):
                 assert s.count(sp) == w.count(sp)
+
+
+@pytest.mark.parametrize("name,kw,maxwell", [("cold3d", {}, False),
+                                             ("warm", {"true_size": (32, 32, 32), "ppc": 8, "nalloc_pc": 16}, True),
+                                             ("langmuir2d", {}, False), ("langmuir1d", {}, False)])
+def test_fused_push_equals_separate_operators(sim_cls, name, kw, maxwell):
+    """population:fused=1 (default: puAcc's kick, the next puMove's drift,
+    the classification and the deposit of the particles that stay in one
+    pass) against fused=0 (one kernel per reference operator), 3 steps.
+    Each run's deposit sums in a different order (atomics), so the field and
+    through it the particles differ by rounding only: same counts, same
+    order, positions to 1e-13 of the grid size, velocities to 1e-10 of
+    max|v|, rho to 1e-12 of one species' charge scale (|q| ppc 8, as
+    test_deposit_layouts: the net charge cancels), energies to 1e-9."""
+    cfg = configs.config(name, **kw)
+    out = {}
+    for fused in ("0", "1"):
+        cfg["population"]["fused"] = fused
+        ini = configs.write_ini(cfg)
+        with sim_cls(ini, maxwell=maxwell, perturb=not maxwell, seed=7) as s:
+            s.init()
+            s.step(3)
+            out[fused] = {"parts": [s.particles(sp) for sp in range(2)], "rho": s.grid(0), "e": s.energy()[:2]}
+            q, _ = s.species()
+            rho_scale = abs(q[0]) * s.count(0) / np.prod(out[fused]["rho"].shape[:-1]) * 8
+    L = max(int(t) for t in cfg["grid"]["trueSize"].split(","))
+    for sp in range(2):
+        (p1, v1), (p0, v0) = out["1"]["parts"][sp], out["0"]["parts"][sp]
+        assert p1.shape == p0.shape
+        assert np.abs(p1 - p0).max() <= 1e-13 * L
+        assert np.abs(v1 - v0).max() <= 1e-10 * max(np.abs(v0).max(), 1e-300)
+    assert np.abs(out["1"]["rho"] - out["0"]["rho"]).max() <= 1e-12 * rho_scale
+    for a, b in zip(out["1"]["e"], out["0"]["e"]):
+        assert abs(a - b) <= 1e-9 * abs(b)
