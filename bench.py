@@ -87,6 +87,8 @@ def main() -> int:
                     help="tiled: particles re-sorted by 4^3-cell tile every --sort-interval moves (default); "
                          "reference: the reference's particle order (bit-exact indices)")
     ap.add_argument("--sort-interval", type=int, default=4)
+    ap.add_argument("--sort-in-push", type=int, default=1,
+                    help="1: the tile sort rides in every sort-interval-th push (default); 0: separate sort pass")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-size", type=int, default=64)
     ap.add_argument("--cpu-steps", type=int, default=8)
@@ -131,6 +133,7 @@ def main() -> int:
     if args.layout == "tiled":
         cfg["population"]["layout"] = "tiled"
         cfg["population"]["sortInterval"] = str(args.sort_interval)
+        cfg["population"]["sortInPush"] = str(args.sort_in_push)
     ini = configs.write_ini(cfg)
 
     def barrier():

@@ -38,6 +38,9 @@ typedef struct {
 	int nloc;      /* true cells of this rank along the slab dimension */
 	int off;       /* first true cell of this rank along the slab dim */
 	int nranks;    /* slabs along the slab dimension */
+	int literal;   /* main.c's double rho FROMHALO (literal loop): deposits on
+	                  periodic ghost nodes of the non-slab dims count twice per
+	                  ghost coordinate */
 } pinc_geom_t;
 
 /* a population on the device (by value; pointers are device pointers) */
@@ -86,15 +89,49 @@ int pinc_hip_move_classify(pinc_pop_t pop, int s, int doMove, const double *thr,
                            int *errFlag, int wrapMask, void *stream);
 
 /* Fused push of species s: optionally puAcc's kick
- * (kick=1: gather from Es as pinc_hip_accelerate, v += dv, KE partials per
- * PINC_CHUNK block in kePartial, *nBlocks of them), then puMove's drift,
- * the classification of pinc_hip_move_classify (flags, chunkCount, errFlag,
- * wrapMask) and the CIC deposit (puDistr3D1/ND1 weights) of every particle
- * that stays into the species accumulator rhoS (slab layout, not zeroed
- * here).  New positions go to xout[d] (may be pop.x[d]). */
-int pinc_hip_push(pinc_pop_t pop, int s, double *const *xout, int kick, pinc_geom_t g, const double *Es,
-                  double *rhoS, const double *thr, unsigned char *flags, int *chunkCount, double maxVel,
-                  int *errFlag, int wrapMask, double *kePartial, int *nBlocks, void *stream);
+ * (kick=1: gather from Es as pinc_hip_accelerate, v += dv, KE partials of
+ * blocks of PINC_CHUNK/2 particles in kePartial, *nBlocks of them), then
+ * puMove's drift, the classification of pinc_hip_move_classify (flags,
+ * chunkCount -- zeroed by the caller -- errFlag, wrapMask) and the CIC
+ * deposit (puDistr3D1/ND1 weights) of every particle that stays into the
+ * species accumulator rhoS (slab layout, not zeroed here).
+ *   cursor == NULL: particle i stays at i; new positions go to xout (may be
+ *     pop.x), velocities to vout (may be pop.v).
+ *   cursor != NULL (tiled layout, sorted output): particle i goes to slot
+ *     cursor[key(x_i)]++ (cursor = exclusive scan of the key counts of the
+ *     current positions, pinc_hip_count_keys + pinc_hip_scan_keys), its
+ *     moved state to xout/vout at that slot (must not alias pop), flags at
+ *     that slot, perm[i] = slot; chunkCount counts emigrants per
+ *     destination chunk; the keys of the moved particles that
+ *     stay are counted into cntNext (zeroed by the caller). */
+typedef struct {
+	double *xout[3];
+	double *vout[3];
+	int kick;
+	const double *Es;
+	double *rhoS;
+	const double *thr;
+	unsigned char *flags;
+	int *chunkCount;
+	double maxVel;
+	int *errFlag;
+	int wrapMask;
+	double *kePartial;
+	int tileWidth;
+	int *cursor;
+	int *cntNext;
+	int *perm;
+} pinc_push_t;
+int pinc_hip_push(pinc_pop_t pop, int s, pinc_geom_t g, const pinc_push_t *args, int *nBlocks, void *stream);
+/* number of sort keys (cells incl. the wrap layer) of the tiled layout */
+long pinc_hip_tile_keys(pinc_geom_t g, int tileWidth);
+/* counts[key(x_i)] += 1 for particles iStart[s]+first .. iStop[s]-1 */
+int pinc_hip_count_keys(pinc_pop_t pop, int s, long first, pinc_geom_t g, int tileWidth, int *counts, void *stream);
+/* exclusive scan of nKeys counts (offsets[nKeys] = total); work holds
+ * 2*ceil(nKeys/4096)+1 ints */
+int pinc_hip_scan_keys(const int *counts, long nKeys, int *offsets, int *work, void *stream);
+/* dst[i] = src[perm[i]] (velocities of a sorted push in the old order) */
+int pinc_hip_gather_perm(const double *src, const int *perm, long n, double *dst, void *stream);
 /* rho = the reference's per-species chain (gZero; gMul(1/q_s); add species
  * s; gMul(q_s); pusher.c:512-572) applied to per-species sums acc[s], over
  * n slab elements */

@@ -412,6 +412,28 @@ __device__ __forceinline__ void cic_weights(const double *dec, const double *com
 	}
 }
 
+// main.c's literal loop adds rho's ghost layers twice (main.c:226,232): a
+// weight that lands on a periodic ghost node counts 2^g times, g = its ghost
+// coordinates (checked against grid.c:340-406 applied twice).  Slab ghost
+// planes are kept on the device and folded twice by the caller; here the
+// non-slab dimensions, which are wrapped at deposit, get their factor.
+template <int ND>
+__device__ __forceinline__ void literal_ghost_weights(const pinc_geom_t &g, const int *j, double *w) {
+	if (!g.literal) return;
+	const int slab = g.nd - 1;
+#pragma unroll
+	for (int c = 0; c < (1 << ND); c++) {
+		double m = 1.0;
+#pragma unroll
+		for (int d = 0; d < ND; d++) {
+			if (d == slab) continue;
+			int p = j[d] + ((c >> d) & 1);
+			if (p == 0 || p == g.T[d] + 1) m *= 2.0;
+		}
+		w[c] *= m;
+	}
+}
+
 // global offset of padded node (j[0]+c0, j[1]+c1, ...) for corner c
 template <int ND>
 __device__ __forceinline__ long corner_off(const Geo &G, const int *j, int c) {
@@ -555,6 +577,7 @@ __global__ __launch_bounds__(kThreads) void k_deposit_tiled(const double *__rest
 				same = same && (j[d] == cj[d]);
 			}
 			cic_weights<ND, V3D>(dec, comp, w);
+			literal_ghost_weights<ND>(g, j, w);
 			if (same) {
 #pragma unroll
 				for (int c = 0; c < NC; c++) a[c] += w[c];
@@ -1102,6 +1125,7 @@ __global__ __launch_bounds__(kThreads) void k_deposit_cells(const double *__rest
 				own = own && j[d] == cell[d];
 			}
 			cic_weights<ND, V3D>(dec, comp, w);
+			literal_ghost_weights<ND>(g, j, w);
 			if (own) {
 #pragma unroll
 				for (int c = 0; c < NC; c++) sum[c] += w[c];
@@ -1148,8 +1172,9 @@ __global__ __launch_bounds__(kThreads) void k_deposit_cells(const double *__rest
 // serial loop.
 struct PushArgs {
 	const double *xi[3];
-	double *xo[3];       // may alias xi
-	double *v[3];
+	double *xo[3];       // may alias xi (unsorted)
+	const double *vi[3];
+	double *vo[3];       // may alias vi (unsorted)
 	long n;              // particles of the species; pointers start at it
 	pinc_geom_t g;
 	const double *Es;    // kick: E as rescaled for the species (k_field_chain)
@@ -1161,6 +1186,12 @@ struct PushArgs {
 	int *chunkCount;
 	int *err;
 	double *kePartial;
+	// sorted output (tiled layout): particle i goes to cursor[key(x_i)]++,
+	// the keys of the moved particles are counted in cntNext for the next push
+	TileGeo tg;
+	int *cursor;
+	int *cntNext;
+	int *perm;           // perm[i] = destination of particle i
 };
 
 // same-cell groups of at least kPushGroupMin lanes (at most kPushGroups of
@@ -1169,8 +1200,9 @@ constexpr int kPushGroupMin = 2;
 constexpr int kPushGroups = 4;
 // 8 waves x 4 particles per thread per PINC_CHUNK block: fewer live VGPRs
 // (px) than 4 waves x 8, so more waves per SIMD hide the gather latency
-constexpr int kPushThreads = 512;
-constexpr int kPushItems = PINC_CHUNK / kPushThreads;
+constexpr int kPushThreads = 256;
+constexpr int kPushItems = 4;
+constexpr int kPushChunk = kPushThreads * kPushItems;  // particles per block (PINC_CHUNK / 2)
 
 // double-precision lane exchange helpers on the two 32-bit halves
 __device__ __forceinline__ void permlane32_swap(double &a, double &b) {
@@ -1265,54 +1297,273 @@ __device__ __forceinline__ void node_pair(const Geo32 &G, int d, int j, int &o0,
 	}
 }
 
-template <int ND, bool V3D, bool KICK>
-__global__ __launch_bounds__(kPushThreads) void k_push(PushArgs a) {
+// LDS capacities of the push: E nodes (pre-move cells + 1), charge nodes
+// (post-move cells + 1), input cells and output cells of the sort counters
+constexpr int kEBoxCap = 384;
+constexpr int kRhoBoxCap = 1024;
+constexpr int kInCellCap = 256;
+constexpr int kOutCellCap = 512;
+
+// box of integer coordinates: origin, extents, volume, linear index
+struct Box {
+	int lo[3], n[3];
+	int vol;
+	__device__ __forceinline__ int index(const int *c, int nd) const {
+		int l = 0, s = 1;
+		for (int d = 0; d < nd; d++) {
+			l += mul24(c[d] - lo[d], s);
+			s *= n[d];
+		}
+		return l;
+	}
+	__device__ __forceinline__ bool inside(const int *c, int nd) const {
+		bool ok = vol > 0;
+		for (int d = 0; d < nd; d++) ok = ok && c[d] >= lo[d] && c[d] < lo[d] + n[d];
+		return ok;
+	}
+	__device__ __forceinline__ void coords(int l, int *c, int nd) const {
+		for (int d = 0; d < nd; d++) {
+			c[d] = lo[d] + l % n[d];
+			l /= n[d];
+		}
+	}
+};
+__device__ __forceinline__ Box make_box(const int *clo, const int *chi, int grow_lo, int grow_hi, int nd, int cap) {
+	Box b;
+	long v = 1;
+	for (int d = 0; d < 3; d++) {
+		b.lo[d] = d < nd ? clo[d] - grow_lo : 0;
+		b.n[d] = d < nd ? chi[d] - clo[d] + 1 + grow_lo + grow_hi : 1;
+		v *= b.n[d];
+	}
+	b.vol = (v <= cap && v > 0) ? (int)v : 0;
+	return b;
+}
+
+// LDS counter add of 1 per active lane at ctr[idx], aggregated over the
+// lanes that share an index: the two largest groups (first and last pending
+// lane's index) take one atomic each, the rest add individually.  Returns the
+// lane's rank (old value + rank among its group) when RET.
+template <bool RET>
+__device__ __forceinline__ int lds_agg_add(int *ctr, int idx, bool active) {
+	const int lane = threadIdx.x & 63;
+	unsigned long long pend = __ballot(active);
+	int mine = 0;
+#pragma unroll 1
+	for (int grp = 0; grp < 2 && pend; grp++) {
+		int leader = grp ? 63 - __clzll((long long)pend) : __ffsll((long long)pend) - 1;
+		int li = __shfl(idx, leader, 64);
+		unsigned long long m = __ballot(active && idx == li) & pend;
+		pend &= ~m;
+		int b = 0;
+		if (lane == leader) b = atomicAdd(&ctr[li], __popcll(m));
+		if (RET) {
+			b = __shfl(b, leader, 64);
+			if ((m >> lane) & 1ull) mine = b + __popcll(m & lanemask_lt());
+		}
+	}
+	if ((pend >> lane) & 1ull) {
+		int b = atomicAdd(&ctr[idx], 1);
+		if (RET) mine = b;
+	}
+	return mine;
+}
+
+// sort key of integer cell coordinates (tile_key's order)
+template <int ND>
+__device__ __forceinline__ int tile_key_cells(const TileGeo &tg, const int *cin) {
+	long tile = 0;
+	int cell = 0, cs = 1;
+#pragma unroll
+	for (int d = 0; d < ND; d++) {
+		int c = cin[d];
+		c = c < 0 ? 0 : (c > tg.cmax[d] ? tg.cmax[d] : c);
+		tile += (long)(c / tg.tw) * tg.ts[d];
+		cell += (c % tg.tw) * cs;
+		cs *= tg.tw;
+	}
+	return (int)(tile * cs + cell);
+}
+
+template <int ND, bool V3D, bool KICK, bool SORT>
+__global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_push(PushArgs a) {
 	constexpr int NC = 1 << ND;
-	__shared__ double acc[kDepCap];
-	__shared__ int red[2 * 3 * (kPushThreads / 64)];
-	__shared__ int box[7];
-	__shared__ double kered[kPushThreads / 64];
-	__shared__ int wcnt[kPushThreads / 64];
+	constexpr int NW = kPushThreads / 64;
+	__shared__ double rhoL[kRhoBoxCap];
+	__shared__ double eL[KICK ? kEBoxCap * ND : 1];
+	__shared__ int cntIn[SORT ? kInCellCap : 1];
+	__shared__ int cntOut[kOutCellCap];
+	__shared__ int red[2 * 3 * NW];
+	__shared__ int cbox[6];
+	__shared__ double kered[NW];
+	__shared__ int wcnt[NW];
 	const Geo32 G = make_geo32(a.g);
 	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-	const long base = (long)blockIdx.x * PINC_CHUNK;
+	const long base = (long)blockIdx.x * kPushChunk;
 
-	double px[kPushItems][ND];  // post-move positions of the particles that stay
-	unsigned dep = 0;
+	// ---- phase A: load every item, cell box of the input positions
+	double p[kPushItems][ND], vv[kPushItems][ND];
+	unsigned valid = 0;
 	int lo[3] = {INT32_MAX, INT32_MAX, INT32_MAX}, hi[3] = {INT32_MIN, INT32_MIN, INT32_MIN};
-	double ke = 0.0;
-	int cnt = 0, bad = 0;
-
-	// ---- phase 1: kick, drift, classify, store (unrolled: px stays in VGPRs)
 #pragma unroll
 	for (int k = 0; k < kPushItems; k++) {
 		const long i = base + k * kPushThreads + threadIdx.x;
-		if (i >= a.n) continue;
-		double p[ND], vv[ND];
+		const bool ok = i < a.n;
+		valid |= (unsigned)ok << k;
 #pragma unroll
 		for (int d = 0; d < ND; d++) {
-			p[d] = a.xi[d][i];
-			vv[d] = a.v[d][i];
+			p[k][d] = ok ? a.xi[d][i] : 1.0;
+			vv[k][d] = ok ? a.vi[d][i] : 0.0;
+			if (ok) {
+				int c = (int)p[k][d];
+				lo[d] = min(lo[d], c);
+				hi[d] = max(hi[d], c);
+			}
 		}
-		if (KICK) {
-			double dec[3], comp[3];
-			int o[3][2];
+	}
+#pragma unroll
+	for (int d = 0; d < ND; d++) {
+		int x = wave_min_i(lo[d]), y = wave_max_i(hi[d]);
+		if (lane == 0) {
+			red[(2 * d) * NW + wv] = x;
+			red[(2 * d + 1) * NW + wv] = y;
+		}
+	}
+	__syncthreads();
+	if (threadIdx.x < ND) {
+		int d = threadIdx.x, x = INT32_MAX, y = INT32_MIN;
+		for (int w = 0; w < NW; w++) {
+			x = min(x, red[(2 * d) * NW + w]);
+			y = max(y, red[(2 * d + 1) * NW + w]);
+		}
+		cbox[d] = x;
+		cbox[3 + d] = y;
+	}
+	__syncthreads();
+	int clo[3] = {0, 0, 0}, chi[3] = {0, 0, 0};
+#pragma unroll
+	for (int d = 0; d < ND; d++) {
+		clo[d] = cbox[d];
+		chi[d] = cbox[3 + d];
+	}
+	const bool empty = clo[0] > chi[0];
+	// E nodes of the input cells; charge nodes and cells after a move of at
+	// most one cell (|v| <= maxVel <= 1; wrapped particles fall outside)
+	const Box eB = (KICK && !empty) ? make_box(clo, chi, 0, 1, ND, kEBoxCap) : Box{{0, 0, 0}, {1, 1, 1}, 0};
+	const Box rB = !empty ? make_box(clo, chi, 1, 2, ND, kRhoBoxCap) : Box{{0, 0, 0}, {1, 1, 1}, 0};
+	const Box iB = (SORT && !empty) ? make_box(clo, chi, 0, 0, ND, kInCellCap) : Box{{0, 0, 0}, {1, 1, 1}, 0};
+	const Box oB = (a.cntNext && !empty) ? make_box(clo, chi, 1, 1, ND, kOutCellCap) : Box{{0, 0, 0}, {1, 1, 1}, 0};
+
+	// ---- phase B: LDS setup (zero the accumulators, stage E)
+	for (int t = threadIdx.x; t < rB.vol; t += kPushThreads) rhoL[t] = 0.0;
+	if (SORT)
+		for (int t = threadIdx.x; t < iB.vol; t += kPushThreads) cntIn[t] = 0;
+	for (int t = threadIdx.x; t < oB.vol; t += kPushThreads) cntOut[t] = 0;
+	if (KICK) {
+		for (int t = threadIdx.x; t < eB.vol; t += kPushThreads) {
+			int c[3] = {0, 0, 0};
+			eB.coords(t, c, ND);
+			int off = 0;
 #pragma unroll
 			for (int d = 0; d < ND; d++) {
-				int j = (int)p[d];
-				dec[d] = p[d] - j;
+				int o0, o1;
+				node_pair(G, d, c[d], o0, o1);
+				off += o0;
+			}
+			const double *ep = a.Es + (unsigned)(off * ND);
+#pragma unroll
+			for (int q = 0; q < ND; q++) eL[t * ND + q] = ep[q];
+		}
+	}
+	__syncthreads();
+
+	// ---- phase C (sorted output): destination of every item
+	int dst[kPushItems];
+	if (SORT) {
+		int rank[kPushItems], lc[kPushItems];
+#pragma unroll
+		for (int k = 0; k < kPushItems; k++) {
+			rank[k] = 0;
+			lc[k] = -1;
+			if ((valid >> k) & 1u) {
+				int c[3] = {0, 0, 0};
+#pragma unroll
+				for (int d = 0; d < ND; d++) c[d] = (int)p[k][d];
+				if (iB.vol) lc[k] = iB.index(c, ND);
+			}
+			rank[k] = lds_agg_add<true>(cntIn, lc[k] < 0 ? 0 : lc[k], iB.vol && lc[k] >= 0);
+		}
+		__syncthreads();
+		// one global reservation per input cell of the block
+		for (int t = threadIdx.x; t < iB.vol; t += kPushThreads) {
+			int m = cntIn[t];
+			if (m) {
+				int c[3] = {0, 0, 0};
+				iB.coords(t, c, ND);
+				cntIn[t] = atomicAdd(&a.cursor[tile_key_cells<ND>(a.tg, c)], m);
+			}
+		}
+		__syncthreads();
+#pragma unroll
+		for (int k = 0; k < kPushItems; k++) {
+			const bool ok = (valid >> k) & 1u;
+			if (iB.vol) {
+				dst[k] = ok ? cntIn[lc[k]] + rank[k] : 0;
+			} else {
+				// box too large for LDS: wave-aggregated global reservation
+				int c[3] = {0, 0, 0};
+#pragma unroll
+				for (int d = 0; d < ND; d++) c[d] = (int)p[k][d];
+				int key = ok ? tile_key_cells<ND>(a.tg, c) : 0;
+				dst[k] = agg_add(a.cursor, key, ok);
+			}
+		}
+	} else {
+#pragma unroll
+		for (int k = 0; k < kPushItems; k++) dst[k] = (int)(base + k * kPushThreads + threadIdx.x);
+	}
+
+	// ---- phase D: kick, drift, classify, store
+	double ke = 0.0;
+	int cnt = 0, bad = 0;
+	unsigned dep = 0;
+#pragma unroll
+	for (int k = 0; k < kPushItems; k++) {
+		if (!((valid >> k) & 1u)) continue;
+		const long i = base + k * kPushThreads + threadIdx.x;
+		if (KICK) {
+			double dec[3], comp[3];
+			int j[3] = {0, 0, 0};
+#pragma unroll
+			for (int d = 0; d < ND; d++) {
+				j[d] = (int)p[k][d];
+				dec[d] = p[k][d] - j[d];
 				comp[d] = 1 - dec[d];
-				node_pair(G, d, j, o[d][0], o[d][1]);
 			}
 			double e[NC][ND];
+			if (eB.vol) {
+				const int l0 = eB.index(j, ND);
 #pragma unroll
-			for (int c = 0; c < NC; c++) {
-				int off = 0;
+				for (int c = 0; c < NC; c++) {
+					int l = l0;
 #pragma unroll
-				for (int d = 0; d < ND; d++) off += o[d][(c >> d) & 1];
-				const double *ep = a.Es + (unsigned)(off * ND);
+					for (int d = 0; d < ND; d++) l += ((c >> d) & 1) ? (d == 0 ? 1 : (d == 1 ? eB.n[0] : eB.n[0] * eB.n[1])) : 0;
 #pragma unroll
-				for (int q = 0; q < ND; q++) e[c][q] = ep[q];
+					for (int q = 0; q < ND; q++) e[c][q] = eL[l * ND + q];
+				}
+			} else {
+				int o[3][2];
+#pragma unroll
+				for (int d = 0; d < ND; d++) node_pair(G, d, j[d], o[d][0], o[d][1]);
+#pragma unroll
+				for (int c = 0; c < NC; c++) {
+					int off = 0;
+#pragma unroll
+					for (int d = 0; d < ND; d++) off += o[d][(c >> d) & 1];
+					const double *ep = a.Es + (unsigned)(off * ND);
+#pragma unroll
+					for (int q = 0; q < ND; q++) e[c][q] = ep[q];
+				}
 			}
 			double dv[ND];
 			if (V3D) {
@@ -1347,115 +1598,83 @@ __global__ __launch_bounds__(kPushThreads) void k_push(PushArgs a) {
 			double vsq = 0;
 #pragma unroll
 			for (int d = 0; d < ND; d++) {
-				vsq += vv[d] * (vv[d] + dv[d]);
-				vv[d] = vv[d] + dv[d];
-				a.v[d][i] = vv[d];
+				vsq += vv[k][d] * (vv[k][d] + dv[d]);
+				vv[k][d] = vv[k][d] + dv[d];
 			}
 			ke += vsq;
 		}
 		// drift + pVelAssertMax (population.c:342-365)
 #pragma unroll
 		for (int d = 0; d < ND; d++) {
-			bad |= (vv[d] > a.maxVel);
-			p[d] += vv[d];
+			bad |= (vv[k][d] > a.maxVel);
+			p[k][d] += vv[k][d];
 		}
 		// neighbour digit per dimension, as k_move_classify
 		int ne = 0;
 #pragma unroll
 		for (int d = ND - 1; d >= 0; d--) {
-			int dig = 1 - (p[d] < a.thr.lo[d]) + (p[d] >= a.thr.up[d]);
-			double q = p[d] - (double)(dig - 1) * (a.thr.hi[d] - 1.0);
+			int dig = 1 - (p[k][d] < a.thr.lo[d]) + (p[k][d] >= a.thr.up[d]);
+			double q = p[k][d] - (double)(dig - 1) * (a.thr.hi[d] - 1.0);
 			bad |= (q < 0.0 || q > a.thr.hi[d]) << 1;
 			if ((a.wrapMask >> d) & 1) {
-				if (dig != 1) p[d] = p[d] + (double)((1 - dig) * a.thr.T[d]);
+				if (dig != 1) p[k][d] = p[k][d] + (double)((1 - dig) * a.thr.T[d]);
 				dig = 1;
 			}
 			ne = ne * 3 + dig;
 		}
+		const long o = SORT ? (long)dst[k] : i;
 #pragma unroll
-		for (int d = 0; d < ND; d++) a.xo[d][i] = p[d];
-		a.flags[i] = (unsigned char)ne;
+		for (int d = 0; d < ND; d++) {
+			a.xo[d][o] = p[k][d];
+			if (KICK || SORT) a.vo[d][o] = vv[k][d];
+		}
+		a.flags[o] = (unsigned char)ne;
+		if (SORT) a.perm[i] = (int)o;
 		if (ne != a.center) {
-			cnt++;
+			if (SORT) atomicAdd(&a.chunkCount[o / PINC_CHUNK], 1);
+			else cnt++;
 		} else {
 			dep |= 1u << k;
+		}
+	}
+	if (a.cntNext) {
+		// count the output cells of the particles that stay (next push's sort)
 #pragma unroll
-			for (int d = 0; d < ND; d++) {
-				px[k][d] = p[d];
-				int jj = (int)p[d];
-				lo[d] = min(lo[d], jj);
-				hi[d] = max(hi[d], jj + 1);
-			}
+		for (int k = 0; k < kPushItems; k++) {
+			const bool mine = (dep >> k) & 1u;
+			int c[3] = {0, 0, 0};
+#pragma unroll
+			for (int d = 0; d < ND; d++) c[d] = (int)p[k][d];
+			const bool inB = mine && oB.inside(c, ND);
+			lds_agg_add<false>(cntOut, inB ? oB.index(c, ND) : 0, inB);
+			if (mine && !inB) atomicAdd(&a.cntNext[tile_key_cells<ND>(a.tg, c)], 1);
 		}
 	}
 	if (bad) atomicOr(a.err, bad);
+	if (!SORT) {
+		int wc = wave_sum(cnt);
+		if (lane == 0) wcnt[wv] = wc;
+	}
 
-	// ---- phase 2: node box of the block's deposits
+	// ---- phase E: deposit of the particles that stay
+	auto add_corner = [&](const int *j, int c, double w) {
+		int cc[3] = {0, 0, 0};
 #pragma unroll
-	for (int d = 0; d < ND; d++) {
-		int x = wave_min_i(lo[d]), y = wave_max_i(hi[d]);
-		if (lane == 0) {
-			red[(2 * d) * (kPushThreads / 64) + wv] = x;
-			red[(2 * d + 1) * (kPushThreads / 64) + wv] = y;
-		}
-	}
-	int wc = wave_sum(cnt);
-	if (lane == 0) wcnt[wv] = wc;
-	__syncthreads();
-	if (threadIdx.x == 0) {
-		long vol = 1;
-		bool any = true;
-		for (int d = 0; d < ND; d++) {
-			int x = INT32_MAX, y = INT32_MIN;
-			for (int w = 0; w < kPushThreads / 64; w++) {
-				x = min(x, red[(2 * d) * (kPushThreads / 64) + w]);
-				y = max(y, red[(2 * d + 1) * (kPushThreads / 64) + w]);
+		for (int d = 0; d < ND; d++) cc[d] = j[d] + ((c >> d) & 1);
+		if (rB.inside(cc, ND)) {
+			atomicAdd(&rhoL[rB.index(cc, ND)], w);
+		} else {
+			int off = 0;
+#pragma unroll
+			for (int d = 0; d < ND; d++) {
+				int o0, o1;
+				node_pair(G, d, j[d], o0, o1);
+				off += ((c >> d) & 1) ? o1 : o0;
 			}
-			any = any && x <= y;
-			box[d] = x;
-			box[3 + d] = y - x + 1;
-			vol *= any ? (long)(y - x + 1) : 0;
-		}
-		box[6] = (any && vol <= kDepCap) ? (int)vol : 0;
-		int t = 0;
-		for (int w = 0; w < kPushThreads / 64; w++) t += wcnt[w];
-		a.chunkCount[blockIdx.x] = t;
-	}
-	__syncthreads();
-	const int vol = box[6];
-	int blo[3] = {0, 0, 0}, bn[3] = {1, 1, 1}, st[3] = {0, 0, 0};
-	if (vol) {
-		int sz = 1;
-#pragma unroll
-		for (int d = 0; d < ND; d++) {
-			blo[d] = box[d];
-			bn[d] = box[3 + d];
-			st[d] = sz;
-			sz *= bn[d];
-		}
-		for (int t = threadIdx.x; t < vol; t += kPushThreads) acc[t] = 0.0;
-		__syncthreads();
-	}
-	// per-dimension offsets of the cell's two node layers: LDS box slots, or
-	// global node offsets when the box does not fit
-	auto layer_offsets = [&](const int *j, int o[3][2]) {
-#pragma unroll
-		for (int d = 0; d < ND; d++) {
-			if (vol) {
-				o[d][0] = d ? mul24(j[d] - blo[d], st[d]) : j[d] - blo[d];
-				o[d][1] = o[d][0] + st[d];
-			} else {
-				node_pair(G, d, j[d], o[d][0], o[d][1]);
-			}
+			unsafeAtomicAdd(&a.rho[(unsigned)off], w);
 		}
 	};
-	auto add_at = [&](int off, double w) {
-		if (vol) atomicAdd(&acc[off], w);
-		else unsafeAtomicAdd(&a.rho[(unsigned)off], w);
-	};
-
-	// ---- phase 3: deposit
-	int keyMul[3] = {1, G.T[0] + 2, (G.T[0] + 2) * (G.T[1] + 2)};  // unique cell key
+	const int keyMul[3] = {1, G.T[0] + 2, (G.T[0] + 2) * (G.T[1] + 2)};  // unique cell key
 #pragma unroll
 	for (int k = 0; k < kPushItems; k++) {
 		const bool mine = (dep >> k) & 1u;
@@ -1469,13 +1688,14 @@ __global__ __launch_bounds__(kPushThreads) void k_push(PushArgs a) {
 			int kk = 0;
 #pragma unroll
 			for (int d = 0; d < ND; d++) {
-				j[d] = (int)px[k][d];
-				dec[d] = px[k][d] - j[d];
+				j[d] = (int)p[k][d];
+				dec[d] = p[k][d] - j[d];
 				comp[d] = 1 - dec[d];
 				kk += d ? mul24(j[d], keyMul[d]) : j[d];
 			}
 			key = kk;
 			cic_weights<ND, V3D>(dec, comp, w);
+			literal_ghost_weights<ND>(a.g, j, w);
 		}
 		unsigned long long pend = __ballot(mine);
 		unsigned long long indiv = 0;
@@ -1498,26 +1718,12 @@ __global__ __launch_bounds__(kPushThreads) void k_push(PushArgs a) {
 			int jl[3] = {0, 0, 0};  // leader's cell (read with every lane active)
 #pragma unroll
 			for (int d = 0; d < ND; d++) jl[d] = __shfl(j[d], leader, 64);
-			if ((lane & 7) == 0 && corner < NC) {
-				int o[3][2];
-				layer_offsets(jl, o);
-				int off = 0;
-#pragma unroll
-				for (int d = 0; d < ND; d++) off += o[d][(corner >> d) & 1];
-				add_at(off, sum);
-			}
+			if ((lane & 7) == 0 && corner < NC) add_corner(jl, corner, sum);
 		}
 		indiv |= pend;
 		if ((indiv >> lane) & 1ull) {
-			int o[3][2];
-			layer_offsets(j, o);
 #pragma unroll
-			for (int c = 0; c < NC; c++) {
-				int off = 0;
-#pragma unroll
-				for (int d = 0; d < ND; d++) off += o[d][(c >> d) & 1];
-				add_at(off, w[c]);
-			}
+			for (int c = 0; c < NC; c++) add_corner(j, c, w[c]);
 		}
 	}
 
@@ -1525,22 +1731,35 @@ __global__ __launch_bounds__(kPushThreads) void k_push(PushArgs a) {
 		double t = block_sum(ke, kered);
 		if (threadIdx.x == 0) a.kePartial[blockIdx.x] = t;
 	}
-	if (!vol) return;
 	__syncthreads();
-	for (int t = threadIdx.x; t < vol; t += kPushThreads) {
-		double v = acc[t];
+	if (!SORT && threadIdx.x == 0) {
+		int t = 0;
+		for (int w = 0; w < NW; w++) t += wcnt[w];
+		if (t) atomicAdd(&a.chunkCount[base / PINC_CHUNK], t);  // zeroed by the caller
+	}
+	// flush: one global atomic per touched node / output cell
+	for (int t = threadIdx.x; t < rB.vol; t += kPushThreads) {
+		double v = rhoL[t];
 		if (v == 0.0) continue;
-		int r = t;
+		int c[3] = {0, 0, 0};
+		rB.coords(t, c, ND);
 		int off = 0;
 #pragma unroll
 		for (int d = 0; d < ND; d++) {
-			int c = r % bn[d];
-			r /= bn[d];
 			int o0, o1;
-			node_pair(G, d, blo[d] + c, o0, o1);
+			node_pair(G, d, c[d], o0, o1);
 			off += o0;
 		}
 		unsafeAtomicAdd(&a.rho[(unsigned)off], v);
+	}
+	if (a.cntNext) {
+		for (int t = threadIdx.x; t < oB.vol; t += kPushThreads) {
+			int m = cntOut[t];
+			if (!m) continue;
+			int c[3] = {0, 0, 0};
+			oB.coords(t, c, ND);
+			atomicAdd(&a.cntNext[tile_key_cells<ND>(a.tg, c)], m);
+		}
 	}
 }
 
@@ -1843,51 +2062,113 @@ extern "C" int pinc_hip_deposit_cells(pinc_pop_t pop, int s, pinc_geom_t g, int 
 	return pinc_hip_deposit(tail, s, g, rho, stream);
 }
 
-extern "C" int pinc_hip_push(pinc_pop_t pop, int s, double *const *xout, int kick, pinc_geom_t g,
-                             const double *Es, double *rhoS, const double *thr, unsigned char *flags,
-                             int *chunkCount, double maxVel, int *errFlag, int wrapMask, double *kePartial,
-                             int *nBlocks, void *stream) {
+extern "C" int pinc_hip_push(pinc_pop_t pop, int s, pinc_geom_t g, const pinc_push_t *args, int *nBlocks,
+                             void *stream) {
 	long n = pop.iStop[s] - pop.iStart[s];
 	*nBlocks = 0;
 	if (n <= 0) return 0;
 	long b0 = pop.iStart[s];
 	int nd = pop.nd;
 	if (nd != g.nd) return set_error(hipErrorInvalidValue, "push: population and grid dimensions differ");
+	const bool sort = args->cursor != nullptr;
+	if (sort && (args->perm == nullptr)) return set_error(hipErrorInvalidValue, "push: sorted output needs perm");
+	if (sort && n > 2147483647L) return set_error(hipErrorInvalidValue, "push: species too large for int slots");
+	long nodes = 1;
+	for (int d = 0; d < nd; d++) nodes *= (d == nd - 1) ? (long)g.nloc + 2 : (long)g.T[d];
+	if (nodes * nd >= 2147483647L) return set_error(hipErrorInvalidValue, "push: grid too large for 32-bit offsets");
 	PushArgs a;
 	for (int d = 0; d < 3; d++) {
 		a.xi[d] = d < nd ? pop.x[d] + b0 : nullptr;
-		a.xo[d] = d < nd ? xout[d] + b0 : nullptr;
-		a.v[d] = d < nd ? pop.v[d] + b0 : nullptr;
-		a.thr.lo[d] = d < nd ? thr[d] : 0;
-		a.thr.up[d] = d < nd ? thr[nd + d] : 0;
-		a.thr.hi[d] = d < nd ? thr[2 * nd + d] : 0;
-		a.thr.T[d] = d < nd ? (int)(thr[2 * nd + d] - 1.0 + 0.5) : 1;
+		a.xo[d] = d < nd ? args->xout[d] + b0 : nullptr;
+		a.vi[d] = d < nd ? pop.v[d] + b0 : nullptr;
+		a.vo[d] = d < nd ? args->vout[d] + b0 : nullptr;
+		a.thr.lo[d] = d < nd ? args->thr[d] : 0;
+		a.thr.up[d] = d < nd ? args->thr[nd + d] : 0;
+		a.thr.hi[d] = d < nd ? args->thr[2 * nd + d] : 0;
+		a.thr.T[d] = d < nd ? (int)(args->thr[2 * nd + d] - 1.0 + 0.5) : 1;
 	}
 	a.n = n;
 	a.g = g;
-	a.Es = Es;
-	a.rho = rhoS;
+	a.Es = args->Es;
+	a.rho = args->rhoS;
 	a.center = 0;
 	for (int d = 0, p = 1; d < nd; d++, p *= 3) a.center += p;
-	a.wrapMask = wrapMask;
-	a.maxVel = maxVel;
-	a.flags = flags + b0;
-	a.chunkCount = chunkCount;
-	a.err = errFlag;
-	a.kePartial = kePartial;
-	unsigned nb = (unsigned)ceil_div(n, PINC_CHUNK);
+	a.wrapMask = args->wrapMask;
+	a.maxVel = args->maxVel;
+	a.flags = args->flags + b0;
+	a.chunkCount = args->chunkCount;
+	a.err = args->errFlag;
+	a.kePartial = args->kePartial;
+	long nKeys = 0;
+	a.tg = make_tile_geo(g, args->tileWidth > 0 ? args->tileWidth : 1, &nKeys);
+	a.cursor = args->cursor;
+	a.cntNext = args->cntNext;
+	a.perm = args->perm;
+	unsigned nb = (unsigned)ceil_div(n, kPushChunk);
 	*nBlocks = (int)nb;
 	hipStream_t st = (hipStream_t)stream;
-#define LAUNCH_PUSH(ND, V3D)                                                                          \
-	do {                                                                                              \
-		if (kick) hipLaunchKernelGGL((k_push<ND, V3D, true>), dim3(nb), dim3(kPushThreads), 0, st, a); \
-		else hipLaunchKernelGGL((k_push<ND, V3D, false>), dim3(nb), dim3(kPushThreads), 0, st, a);     \
+	const bool kick = args->kick != 0;
+#define LAUNCH_PUSH(ND, V3D)                                                                                 \
+	do {                                                                                                     \
+		if (kick && sort) hipLaunchKernelGGL((k_push<ND, V3D, true, true>), dim3(nb), dim3(kPushThreads), 0, st, a);   \
+		else if (kick) hipLaunchKernelGGL((k_push<ND, V3D, true, false>), dim3(nb), dim3(kPushThreads), 0, st, a);     \
+		else if (sort) hipLaunchKernelGGL((k_push<ND, V3D, false, true>), dim3(nb), dim3(kPushThreads), 0, st, a);     \
+		else hipLaunchKernelGGL((k_push<ND, V3D, false, false>), dim3(nb), dim3(kPushThreads), 0, st, a);              \
 	} while (0)
 	if (nd == 3) LAUNCH_PUSH(3, true);
 	else if (nd == 2) LAUNCH_PUSH(2, false);
 	else LAUNCH_PUSH(1, false);
 #undef LAUNCH_PUSH
 	return check_launch("push");
+}
+
+extern "C" long pinc_hip_tile_keys(pinc_geom_t g, int tileWidth) {
+	long nk = 0;
+	(void)make_tile_geo(g, tileWidth, &nk);
+	return nk;
+}
+
+extern "C" int pinc_hip_count_keys(pinc_pop_t pop, int s, long first, pinc_geom_t g, int tileWidth, int *counts,
+                                   void *stream) {
+	long b0 = pop.iStart[s] + first;
+	long n = pop.iStop[s] - b0;
+	if (n <= 0) return 0;
+	long nk = 0;
+	TileGeo tg = make_tile_geo(g, tileWidth, &nk);
+	long nb = ceil_div(n, (long)kThreads);
+	if (nb > 65536L * 8) nb = 65536L * 8;
+	int nd = g.nd;
+	const double *x0 = pop.x[0] + b0, *x1 = nd > 1 ? pop.x[1] + b0 : nullptr, *x2 = nd > 2 ? pop.x[2] + b0 : nullptr;
+	hipStream_t st = (hipStream_t)stream;
+	if (nd == 3) hipLaunchKernelGGL(k_sort_count<3>, dim3(nb), dim3(kThreads), 0, st, x0, x1, x2, n, tg, counts);
+	else if (nd == 2) hipLaunchKernelGGL(k_sort_count<2>, dim3(nb), dim3(kThreads), 0, st, x0, x1, x2, n, tg, counts);
+	else hipLaunchKernelGGL(k_sort_count<1>, dim3(nb), dim3(kThreads), 0, st, x0, x1, x2, n, tg, counts);
+	return check_launch("count_keys");
+}
+
+extern "C" int pinc_hip_scan_keys(const int *counts, long nKeys, int *offsets, int *work, void *stream) {
+	long nsb = ceil_div(nKeys, (long)kScanBlock);
+	if (nsb > 1024L * 1024L) return set_error(hipErrorInvalidValue, "scan_keys: too many keys");
+	int *bsum = work, *boff = work + nsb;
+	hipStream_t st = (hipStream_t)stream;
+	hipLaunchKernelGGL(k_scan_sums, dim3((unsigned)nsb), dim3(kThreads), 0, st, counts, nKeys, bsum);
+	hipLaunchKernelGGL(k_scan_single, dim3(1), dim3(1024), 0, st, bsum, boff, (int)nsb);
+	hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)nsb), dim3(kThreads), 0, st, counts, nKeys, boff, offsets);
+	return check_launch("scan_keys");
+}
+
+__global__ void k_gather_perm(const double *__restrict__ src, const int *__restrict__ perm, long n,
+                              double *__restrict__ dst) {
+	for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+		dst[i] = src[perm[i]];
+}
+
+extern "C" int pinc_hip_gather_perm(const double *src, const int *perm, long n, double *dst, void *stream) {
+	if (n <= 0) return 0;
+	long nb = ceil_div(n, (long)kThreads);
+	if (nb > 65536) nb = 65536;
+	hipLaunchKernelGGL(k_gather_perm, dim3((unsigned)nb), dim3(kThreads), 0, (hipStream_t)stream, src, perm, n, dst);
+	return check_launch("gather_perm");
 }
 
 extern "C" int pinc_hip_rho_combine(double *rho, const double *const *acc, const double *charge, int ns, long n,

@@ -83,6 +83,18 @@ struct PincDevPop {
 	long depEnd[PINC_MAX_SPECIES];      /* particles [iStart, depEnd) are in rhoS */
 	double *rhoS[PINC_MAX_SPECIES];
 	long rhoN;
+	/* tiled + fused: every push writes its output sorted by the cells of its
+	 * input (counting sort folded into the push; the push also counts the
+	 * cells of its output for the next one) */
+	int sorted;
+	int pendingSorted;                  /* pending velocities are in altV, in slot order */
+	long nKeys;
+	int *keyCnt[PINC_MAX_SPECIES];      /* cell counts of the current positions */
+	int *keyNext[PINC_MAX_SPECIES];     /* counts being built by the push */
+	int *keyCur[PINC_MAX_SPECIES];      /* cursors (exclusive offsets) */
+	int *keyWork[PINC_MAX_SPECIES];     /* scan scratch */
+	int cntValid[PINC_MAX_SPECIES];
+	int *perm;                          /* slot of each particle after a sorted push */
 	/* multi-rank migration buffers (AoS records: nd pos, nd vel, ne) */
 	double *sendBuf[2], *recvBuf[2];
 	long sendCap, recvCap;

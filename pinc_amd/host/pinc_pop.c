@@ -95,6 +95,11 @@ Population *pAlloc(const dictionary *ini) {
 		dv->tileWidth = nd == 3 ? 4 : (nd == 2 ? 8 : 32);
 		for (int s = 0; s < PINC_MAX_SPECIES; s++) dv->cellValid[s] = -1;
 	}
+	/* tiled + fused: the counting sort rides in every sortInterval-th push
+	 * (population:sortInPush=1, default) or runs as a pass of its own (0) */
+	dv->sorted = dv->tiled && dv->fused &&
+	             (iniHas(ini, "population:sortInPush") ? iniGetInt(ini, "population:sortInPush") : 1);
+	if (dv->sorted) pinc_check(pinc_hip_malloc((void **)&dv->perm, cap * sizeof(int)), "pAlloc perm");
 	if (dv->tiled || dv->fused) {
 		for (int d = 0; d < nd; d++) {
 			pinc_check(pinc_hip_malloc((void **)&dv->altX[d], cap * sizeof(double)), "pAlloc pos (tiled)");
@@ -111,7 +116,8 @@ Population *pAlloc(const dictionary *ini) {
 	long nChunks = maxS / PINC_CHUNK + 2;
 	int *chunkOffset = NULL;
 	pinc_check(pinc_hip_malloc((void **)&dv->chunkCount, dv->chunkBase[ns] * sizeof(int)), "pAlloc chunks");
-	pinc_check(pinc_hip_malloc((void **)&dv->kePartial, (maxS / 2048 + 16) * sizeof(double)), "pAlloc ke");
+	/* one KE partial per push block (PINC_CHUNK/2 particles) */
+	pinc_check(pinc_hip_malloc((void **)&dv->kePartial, (maxS / (PINC_CHUNK / 2) + 16) * sizeof(double)), "pAlloc ke");
 	pinc_check(pinc_hip_malloc((void **)&chunkOffset, (nChunks + 1) * sizeof(int)), "pAlloc chunks");
 	for (int s = 0; s < ns; s++) {
 		long capS = p->iStart[s + 1] - p->iStart[s];
@@ -147,7 +153,14 @@ void pFree(Population *p) {
 			pinc_hip_free(dv->altX[d]);
 			pinc_hip_free(dv->altV[d]);
 		}
-		for (int s = 0; s < PINC_MAX_SPECIES; s++) pinc_hip_free(dv->rhoS[s]);
+		for (int s = 0; s < PINC_MAX_SPECIES; s++) {
+			pinc_hip_free(dv->rhoS[s]);
+			pinc_hip_free(dv->keyCnt[s]);
+			pinc_hip_free(dv->keyNext[s]);
+			pinc_hip_free(dv->keyCur[s]);
+			pinc_hip_free(dv->keyWork[s]);
+		}
+		pinc_hip_free(dv->perm);
 		for (int s = 0; s < PINC_MAX_SPECIES; s++) pinc_hip_free(dv->sortWork[s]);
 		pinc_hip_free(dv->chunkCount);
 		pinc_hip_free(dv->ws[0].chunkOffset);
@@ -319,12 +332,23 @@ void pSyncToHost(Population *p) {
 		long a = p->iStart[s], n = p->iStop[s] - a;
 		if (n <= 0) continue;
 		double *tmp = malloc(n * sizeof(double));
+		double *dtmp = NULL;
+		/* a sorted fused push is pending: the kicked velocities sit in altV in
+		 * slot order; read them back in the current order through perm */
+		if (dv->pending && dv->pendingSorted)
+			pinc_check(pinc_hip_malloc((void **)&dtmp, n * sizeof(double)), "pSyncToHost tmp");
 		for (int d = 0; d < nd; d++) {
 			pinc_check(pinc_hip_d2h(tmp, dv->p.x[d] + a, n * sizeof(double), g_pinc.stream), "pSyncToHost");
 			for (long i = 0; i < n; i++) p->pos[(a + i) * nd + d] = tmp[i];
-			pinc_check(pinc_hip_d2h(tmp, dv->p.v[d] + a, n * sizeof(double), g_pinc.stream), "pSyncToHost");
+			const double *vsrc = dv->p.v[d] + a;
+			if (dtmp) {
+				pinc_check(pinc_hip_gather_perm(dv->altV[d] + a, dv->perm + a, n, dtmp, g_pinc.stream), "pSyncToHost");
+				vsrc = dtmp;
+			}
+			pinc_check(pinc_hip_d2h(tmp, vsrc, n * sizeof(double), g_pinc.stream), "pSyncToHost");
 			for (long i = 0; i < n; i++) p->vel[(a + i) * nd + d] = tmp[i];
 		}
+		pinc_hip_free(dtmp);
 		free(tmp);
 	}
 }
@@ -334,7 +358,8 @@ void pSyncToDevice(Population *p) {
 	int nd = p->nDims;
 	PincDevPop *dv = p->dev;
 	/* new particles: a pending fused move and its deposits no longer apply */
-	dv->pending = dv->depValid = dv->depExtracted = 0;
+	dv->pending = dv->pendingSorted = dv->depValid = dv->depExtracted = 0;
+	for (int s = 0; s < PINC_MAX_SPECIES; s++) dv->cntValid[s] = 0;
 	/* new particle order: the cell ranges of the last tile sort no longer apply */
 	for (int s = 0; s < PINC_MAX_SPECIES; s++) dv->cellValid[s] = -1;
 	for (int s = 0; s < p->nSpecies; s++) {

@@ -134,9 +134,35 @@ static int wrap_mask(const Population *pop) {
 	return !pop->dev->tiled ? 0 : (g_pinc.nranks == 1 ? (1 << nd) - 1 : (1 << (nd - 1)) - 1);
 }
 
-/* fused push of every species (pinc_hip_push): kick from E (or none), drift
- * into xout, classification, deposit of the particles that stay into rhoS */
-static void push_all(Population *pop, Grid *E, double *const *xout) {
+/* tiled + fused: key counts of the current positions and scratch */
+static void ensure_keys(Population *pop) {
+	PincDevPop *dv = pop->dev;
+	long nk = pinc_hip_tile_keys(dv->geom, dv->tileWidth);
+	if (dv->nKeys == nk && dv->keyCnt[0]) return;
+	for (int s = 0; s < PINC_MAX_SPECIES; s++) {
+		pinc_hip_free(dv->keyCnt[s]);
+		pinc_hip_free(dv->keyNext[s]);
+		pinc_hip_free(dv->keyCur[s]);
+		pinc_hip_free(dv->keyWork[s]);
+		dv->keyCnt[s] = dv->keyNext[s] = dv->keyCur[s] = dv->keyWork[s] = NULL;
+		dv->cntValid[s] = 0;
+	}
+	for (int s = 0; s < pop->nSpecies; s++) {
+		pinc_check(pinc_hip_malloc((void **)&dv->keyCnt[s], (nk + 1) * sizeof(int)), "key counts");
+		pinc_check(pinc_hip_malloc((void **)&dv->keyNext[s], (nk + 1) * sizeof(int)), "key counts");
+		pinc_check(pinc_hip_malloc((void **)&dv->keyCur[s], (nk + 1) * sizeof(int)), "key cursors");
+		pinc_check(pinc_hip_malloc((void **)&dv->keyWork[s], (2 * (nk / 4096 + 1) + 1) * sizeof(int)), "key scan");
+	}
+	dv->nKeys = nk;
+}
+
+/* fused push of every species (pinc_hip_push): kick from E (or none), drift,
+ * classification, deposit of the particles that stay into rhoS; positions to
+ * xout, velocities in place.  Tiled layout: every sortInterval-th push writes
+ * its output in cell order instead (to altX/altV, counting sort on the cell
+ * counts of its input), and the push before it counts those cells.  Returns
+ * 1 if this push sorted. */
+static int push_all(Population *pop, Grid *E, double *const *xout) {
 	PincDevPop *dv = pop->dev;
 	pinc_geom_t g = dv->geom;
 	long n = 1;
@@ -150,25 +176,61 @@ static void push_all(Population *pop, Grid *E, double *const *xout) {
 			pinc_check(pinc_hip_malloc((void **)&dv->rhoS[s], n * sizeof(double)), "species charge");
 		dv->rhoN = n;
 	}
+	int sortNow = 0, countNext = 0;
+	if (dv->sorted) {
+		ensure_keys(pop);
+		sortNow = dv->moves % dv->sortInterval == 0;
+		countNext = (dv->moves + 1) % dv->sortInterval == 0;
+		dv->moves++;
+	}
 	int nd = pop->nDims;
 	for (int s = 0; s < pop->nSpecies; s++) {
 		pinc_check(pinc_hip_zero(dv->rhoS[s], n, g_pinc.stream), "species charge zero");
-		const double *Es = NULL;
+		pinc_push_t a;
+		memset(&a, 0, sizeof(a));
 		if (E) {
 			PincDevGrid *eg = E->dev;
 			if (!eg->scaled) pinc_check(pinc_hip_malloc((void **)&eg->scaled, eg->n * sizeof(double)), "E scaled");
 			pinc_check(pinc_hip_field_chain(eg->d, eg->scaled, eg->n, dv->qm, dv->mq, 1.0, s, g_pinc.stream),
 			           "E chain");
-			Es = eg->scaled;
+			a.Es = eg->scaled;
+			a.kick = 1;
 		}
 		pinc_pop_t p = pinc_devpop(pop);
 		long np = pop->iStop[s] - pop->iStart[s];
+		long chunks = dv->chunkBase[s + 1] - dv->chunkBase[s];
+		for (int d = 0; d < 3; d++) {
+			a.xout[d] = sortNow ? dv->altX[d] : xout[d];
+			a.vout[d] = sortNow ? dv->altV[d] : dv->p.v[d];
+		}
+		a.rhoS = dv->rhoS[s];
+		a.thr = g_pinc.thr;
+		a.flags = dv->flags;
+		a.chunkCount = dv->chunkCount + dv->chunkBase[s];
+		a.maxVel = g_pinc.maxVel;
+		a.errFlag = g_pinc.dErr;
+		a.wrapMask = wrap_mask(pop);
+		a.kePartial = dv->kePartial;
+		a.tileWidth = dv->tileWidth;
+		pinc_check(pinc_hip_memset(a.chunkCount, 0, chunks * sizeof(int), g_pinc.stream), "chunk counts");
+		if (sortNow) {
+			if (!dv->cntValid[s]) {
+				pinc_check(pinc_hip_memset(dv->keyCnt[s], 0, (dv->nKeys + 1) * sizeof(int), g_pinc.stream), "keys");
+				pinc_check(pinc_hip_count_keys(p, s, 0, g, dv->tileWidth, dv->keyCnt[s], g_pinc.stream), "count keys");
+			}
+			pinc_check(pinc_hip_scan_keys(dv->keyCnt[s], dv->nKeys, dv->keyCur[s], dv->keyWork[s], g_pinc.stream),
+			           "scan keys");
+			a.cursor = dv->keyCur[s];
+			a.perm = dv->perm + pop->iStart[s];
+			dv->cellValid[s] = -1;
+		}
+		if (countNext) {
+			pinc_check(pinc_hip_memset(dv->keyNext[s], 0, (dv->nKeys + 1) * sizeof(int), g_pinc.stream), "keys");
+			a.cntNext = dv->keyNext[s];
+		}
 		int nb = 0;
 		int slot = E ? pinc_probe_begin(PINC_PROBE_PUSH) : -1;
-		pinc_check(pinc_hip_push(p, s, xout, E != NULL, g, Es, dv->rhoS[s], g_pinc.thr, dv->flags,
-		                         dv->chunkCount + dv->chunkBase[s], g_pinc.maxVel, g_pinc.dErr, wrap_mask(pop),
-		                         dv->kePartial, &nb, g_pinc.stream),
-		           "push");
+		pinc_check(pinc_hip_push(p, s, g, &a, &nb, g_pinc.stream), "push");
 		/* pos R+W, vel R+W (32 B per dim per particle) + E R (8 B per value
 		 * per node) + rho flush (8 B per node) */
 		if (E) pinc_probe_end(PINC_PROBE_PUSH, slot, 32.0 * nd * np + 8.0 * (nd + 1) * (double)n);
@@ -176,16 +238,30 @@ static void push_all(Population *pop, Grid *E, double *const *xout) {
 			if (nb > 0) pinc_check(pinc_hip_reduce(dv->kePartial, nb, 1.0, PINC_SLOT(16 + s), g_pinc.stream), "ke");
 			else pinc_check(pinc_hip_memset(PINC_SLOT(16 + s), 0, sizeof(double), g_pinc.stream), "ke");
 		}
+		if (countNext) {
+			int *t = dv->keyCnt[s];
+			dv->keyCnt[s] = dv->keyNext[s];
+			dv->keyNext[s] = t;
+			dv->cntValid[s] = 1;
+		} else if (dv->sorted) {
+			dv->cntValid[s] = 0;
+		}
 	}
 	dv->depValid = 1;
 	dv->depExtracted = 0;
+	return sortNow;
 }
 
-static void swap_pos(PincDevPop *dv, int nd) {
+static void swap_pos(PincDevPop *dv, int nd, int vel) {
 	for (int d = 0; d < nd; d++) {
 		double *t = dv->p.x[d];
 		dv->p.x[d] = dv->altX[d];
 		dv->altX[d] = t;
+		if (vel) {
+			t = dv->p.v[d];
+			dv->p.v[d] = dv->altV[d];
+			dv->altV[d] = t;
+		}
 	}
 }
 
@@ -193,22 +269,34 @@ static void classify(Population *pop, int doMove) {
 	if (!g_pinc.thrSet) msg(ERROR, "gCreateNeighborhood must run before puMove/extract");
 	PincDevPop *dv = pop->dev;
 	int nd = pop->nDims;
-	if (!doMove) dv->pending = 0; /* flags recomputed for the current positions */
+	if (!doMove && dv->pending) {
+		/* flags recomputed for the current positions: drop the pending move
+		 * (a sorted one first puts the kicked velocities back in order) */
+		if (dv->pendingSorted)
+			for (int s = 0; s < pop->nSpecies; s++)
+				for (int d = 0; d < nd; d++)
+					pinc_check(pinc_hip_gather_perm(dv->altV[d] + pop->iStart[s], dv->perm + pop->iStart[s],
+					                                pop->iStop[s] - pop->iStart[s], dv->p.v[d] + pop->iStart[s],
+					                                g_pinc.stream),
+					           "unsort velocities");
+		dv->pending = dv->pendingSorted = 0;
+	}
 	if (doMove && dv->pending) {
 		/* the fused puAcc already moved, classified and deposited */
-		swap_pos(dv, nd);
-		dv->pending = 0;
+		swap_pos(dv, nd, dv->pendingSorted);
+		dv->pending = dv->pendingSorted = 0;
 		dv->flagsValid = 1;
 		dv->depValid = 1;
 		dv->depExtracted = 0;
 		return;
 	}
-	if (doMove) maybe_sort(pop);
+	if (doMove && !dv->sorted) maybe_sort(pop);
 	if (doMove && dv->fused) {
-		push_all(pop, NULL, dv->p.x);
+		if (push_all(pop, NULL, dv->p.x)) swap_pos(dv, nd, 1);
 		dv->flagsValid = 1;
 		return;
 	}
+	for (int s = 0; s < PINC_MAX_SPECIES; s++) dv->cntValid[s] = 0;
 	dv->depValid = 0;
 	int wrapMask = wrap_mask(pop);
 	pinc_pop_t p = pinc_devpop(pop);
@@ -279,16 +367,13 @@ static void ensure_pair(double **buf, long *cap, long need) {
 	*cap = c;
 }
 
-void puMigrate(Population *pop, MpiInfo *m, Grid *grid) {
-	(void)grid;
-	pinc_phase_begin(2);
+static void puMigrateImport(Population *pop, MpiInfo *m) {
 	PincDevPop *dv = pop->dev;
 	int ns = pop->nSpecies, nd = pop->nDims;
 	pinc_geom_t g = dv->geom;
 	int T[3] = {1, 1, 1};
 	for (int d = 0; d < nd; d++) T[d] = d == nd - 1 ? g.nloc : g.T[d];
 	int P3 = pinc_ipow3(nd - 1);
-	memset(m->nImmigrants, 0, m->nNeighbors * ns * sizeof(long));
 	if (g_pinc.nranks == 1) {
 		/* every neighbour is this rank: messages arrive in the order they
 		 * were sent (by direction ne), each shifted by its receive tag */
@@ -303,7 +388,6 @@ void puMigrate(Population *pop, MpiInfo *m, Grid *grid) {
 				m->nImmigrants[puNeighborToReciprocal(ne, nd) * ns + s] = dv->neCount[s][ne];
 		}
 		dv->flagsValid = 0;
-		pinc_phase_end(2);
 		return;
 	}
 	/* slab decomposition: directions whose slab digit is 0 go down, 2 go up,
@@ -392,6 +476,26 @@ void puMigrate(Population *pop, MpiInfo *m, Grid *grid) {
 		offDown += fromDown[s];
 	}
 	dv->flagsValid = 0;
+	
+}
+
+void puMigrate(Population *pop, MpiInfo *m, Grid *grid) {
+	(void)grid;
+	pinc_phase_begin(2);
+	PincDevPop *dv = pop->dev;
+	int ns = pop->nSpecies;
+	memset(m->nImmigrants, 0, m->nNeighbors * ns * sizeof(long));
+	long before[PINC_MAX_SPECIES];
+	for (int s = 0; s < ns; s++) before[s] = pop->iStop[s] - pop->iStart[s];
+	puMigrateImport(pop, m);
+	/* sorted layout: the imported particles join the key counts */
+	if (dv->sorted)
+		for (int s = 0; s < ns; s++)
+			if (dv->cntValid[s] && pop->iStop[s] - pop->iStart[s] > before[s]) {
+				pinc_pop_t p = pinc_devpop(pop);
+				pinc_check(pinc_hip_count_keys(p, s, before[s], dv->geom, dv->tileWidth, dv->keyCnt[s], g_pinc.stream),
+				           "count immigrant keys");
+			}
 	pinc_phase_end(2);
 }
 
@@ -452,9 +556,9 @@ static void acc(Population *pop, Grid *E, int ke) {
 	if (dv->fused) {
 		/* kick now; the drift of the next puMove, its classification and its
 		 * deposit ride along (positions to altX, swapped in by puMove) */
-		maybe_sort(pop);
+		if (!dv->sorted) maybe_sort(pop);
 		dv->pending = 0;
-		push_all(pop, E, dv->altX);
+		dv->pendingSorted = push_all(pop, E, dv->altX);
 		dv->pending = 1;
 		dv->flagsValid = 0;
 		if (ke) {

@@ -89,6 +89,11 @@ static PincSim *sim_build(dictionary *ini, const PincSimOpts *opts) {
 	S->solve = (void (*)(void *, Grid *, Grid *, const MpiInfo *))solve;
 	S->solverFree = (void (*)(void *))solverFree;
 	S->spectral = solve == (void (*)())sSolve;
+	if (S->opts.literal) {
+		/* main.c:226,232 fold rho's ghosts twice; see literal_ghost_weights */
+		S->pop->dev->geom.literal = 1;
+		S->rho->dev->geom.literal = 1;
+	}
 	gCreateNeighborhood(ini, S->mpi, S->rho);
 	gSetBndSlices(S->phi, S->mpi);
 	g_pinc.maxVel = iniHas(ini, "population:maxVel") ? iniGetDouble(ini, "population:maxVel") : INFINITY;
@@ -111,8 +116,11 @@ static void sim_init(PincSim *S) {
 }
 
 static void sim_fields(PincSim *S) {
-	/* main.c:168-186 */
+	/* main.c:168-186: one FROMHALO here, also in the literal loop */
+	int lit = S->rho->dev->geom.literal;
+	S->rho->dev->geom.literal = 0;
 	S->distr(S->pop, S->rho);
+	S->rho->dev->geom.literal = lit;
 	gHaloOp((funPtr)addSlice, S->rho, S->mpi, FROMHALO);
 	S->solve(S->solver, S->rho, S->phi, S->mpi);
 	pinc_phase_begin(5);

@@ -65,7 +65,8 @@ def test_fused_sweep_rejects_untiled_level(hip):
 
 
 class Geom(C.Structure):
-    _fields_ = [("nd", C.c_int), ("T", C.c_int * 3), ("nloc", C.c_int), ("off", C.c_int), ("nranks", C.c_int)]
+    _fields_ = [("nd", C.c_int), ("T", C.c_int * 3), ("nloc", C.c_int), ("off", C.c_int), ("nranks", C.c_int),
+                ("literal", C.c_int)]
 
 
 class Pop(C.Structure):

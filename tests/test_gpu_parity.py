@@ -286,3 +286,23 @@ def test_fused_push_equals_separate_operators(sim_cls, name, kw, maxwell):
     assert np.abs(out["1"]["rho"] - out["0"]["rho"]).max() <= 1e-12 * rho_scale
     for a, b in zip(out["1"]["e"], out["0"]["e"]):
         assert abs(a - b) <= 1e-9 * abs(b)
+
+
+@pytest.mark.parametrize("name,fused", [("langmuir2d", "1"), ("langmuir2d", "0"), ("cold3d", "1")])
+def test_literal_mainc_energy_history(sim_cls, name, fused):
+    """The literal main.c loop (rho's ghosts folded twice, main.c:226,232,
+    plus the extra solve): energies follow the checker's literal loop to
+    1e-8 (the device wraps x/y at deposit, so the double fold is reproduced
+    by weighting periodic ghost nodes 2^g; see literal_ghost_weights)."""
+    cfg = configs.config(name)
+    cfg["population"]["fused"] = fused
+    ini = configs.write_ini(cfg)
+    steps = 5
+    ke_o, pe_o, _ = orc.run_steps(ini, [], steps, literal=True)
+    with sim_cls(ini, literal=True) as s:
+        s.init()
+        for n in range(steps):
+            s.step()
+            ke, pe, _ = s.energy()
+            assert abs(ke - ke_o[n]) <= 1e-8 * abs(ke_o[n]), (n, ke, ke_o[n])
+            assert abs(pe - pe_o[n]) <= 1e-8 * abs(pe_o[n]), (n, pe, pe_o[n])
