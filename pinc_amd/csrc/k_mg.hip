@@ -365,6 +365,132 @@ __global__ __launch_bounds__(256) void k_gs_sweep(const double *__restrict__ phi
 }
 
 
+// Variant of k_gs_sweep with the planes fetched two iterations ahead of
+// their use (the HBM latency of a plane is covered by two plane
+// relaxations), tile SX x SY per NT-thread workgroup.  Same ring scheme and
+// the same arithmetic as k_gs_sweep (bit-identical results).
+template <int SX, int SY, int NT>
+struct Sweep2 {
+	static constexpr int HX = SX + 4, HY = SY + 4;  // phi region (two-node halo)
+	static constexpr int RX = SX + 2, RY = SY + 2;  // red region (one-node halo)
+	static constexpr int PhiSlots = (HX * HY + NT - 1) / NT;
+	static constexpr int RhoSlots = (RX * RY + NT - 1) / NT;
+};
+
+template <int kS2X, int kS2Y, int kS2Threads>
+__global__ __launch_bounds__(kS2Threads) void k_gs_sweep2(const double *__restrict__ phiIn,
+                                                          double *__restrict__ phiOut,
+                                                          const double *__restrict__ rho, pinc_lvl_t Lp,
+                                                          int zPlanes) {
+	using S = Sweep2<kS2X, kS2Y, kS2Threads>;
+	constexpr int kS2HX = S::HX, kS2HY = S::HY, kS2RX = S::RX, kS2RY = S::RY;
+	constexpr int kS2PhiSlots = S::PhiSlots, kS2RhoSlots = S::RhoSlots;
+	__shared__ double cur[5][kS2HY][kS2HX];
+	__shared__ double rh[3][kS2RY][kS2RX];
+	const int TX = Lp.T[0], TY = Lp.T[1], TZ = Lp.T[2];
+	const long sy = TX, sz = (long)TX * TY;
+	const int ntx = TX / kS2X, nty = TY / kS2Y;
+	const int bx = blockIdx.x % ntx, by = (blockIdx.x / ntx) % nty, bz = blockIdx.x / (ntx * nty);
+	const int x0 = bx * kS2X, y0 = by * kS2Y, z0 = bz * zPlanes;
+	const int tid = threadIdx.x;
+	auto wrapi = [](int i, int T) { return i < 0 ? i + T : (i >= T ? i - T : i); };
+	auto gidx = [&](int x, int y, int z) {
+		return (long)wrapi(x, TX) + wrapi(y, TY) * sy + (long)wrapi(z, TZ) * sz;
+	};
+	auto ps = [](int z) { return (z + 10) % 5; };
+	auto rs = [](int z) { return (z + 9) % 3; };
+	auto fetch = [&](int zf, int zr, double *f, double *r) {
+#pragma unroll
+		for (int k = 0; k < kS2PhiSlots; k++) {
+			int i = tid + kS2Threads * k;
+			if (i < kS2HX * kS2HY) f[k] = phiIn[gidx(x0 + i % kS2HX - 2, y0 + i / kS2HX - 2, zf)];
+		}
+#pragma unroll
+		for (int k = 0; k < kS2RhoSlots; k++) {
+			int i = tid + kS2Threads * k;
+			if (i < kS2RX * kS2RY) r[k] = rho[gidx(x0 + i % kS2RX - 1, y0 + i / kS2RX - 1, zr)];
+		}
+	};
+	auto put = [&](int zf, int zr, const double *f, const double *r) {
+#pragma unroll
+		for (int k = 0; k < kS2PhiSlots; k++) {
+			int i = tid + kS2Threads * k;
+			if (i < kS2HX * kS2HY) cur[ps(zf)][i / kS2HX][i % kS2HX] = f[k];
+		}
+#pragma unroll
+		for (int k = 0; k < kS2RhoSlots; k++) {
+			int i = tid + kS2Threads * k;
+			if (i < kS2RX * kS2RY) rh[rs(zr)][i / kS2RX][i % kS2RX] = r[k];
+		}
+	};
+	auto red = [&](int z, bool wide) {
+		double(*c)[kS2HX] = cur[ps(z)];
+		double(*cm)[kS2HX] = cur[ps(z - 1)];
+		double(*cp)[kS2HX] = cur[ps(z + 1)];
+		double(*r)[kS2RX] = rh[rs(z)];
+		const int lo = wide ? 0 : 1, wx = wide ? kS2RX : kS2X, wy = wide ? kS2RY : kS2Y;
+		for (int i = tid; i < wx * wy; i += kS2Threads) {
+			int hx = lo + i % wx, hy = lo + i / wx;  // red-region coordinates
+			int gx = x0 + hx - 1, gy = y0 + hy - 1;
+			if (((gx + gy + z) & 1) != 0) continue;
+			int cx = hx + 1, cy = hy + 1;          // ring coordinates
+			double xp = c[cy][cx + 1], xm = c[cy][cx - 1];
+			double yp = c[cy + 1][cx], ym = c[cy - 1][cx];
+			double zp = cp[cy][cx], zm = cm[cy][cx];
+			c[cy][cx] = (1. / 6.) * (xp + xm + yp + ym + zp + zm + r[hy][hx]);
+		}
+	};
+
+	// prologue: phi z0-2 .. z0+2 and rho z0-1 .. z0+1 into LDS, phi z0+3 and
+	// rho z0+2 into registers (set A); red of z0-1 (tile) and z0 (wide)
+	double fa[kS2PhiSlots], ra[kS2RhoSlots], fb[kS2PhiSlots], rb[kS2RhoSlots];
+	for (int z = z0 - 2; z <= z0 + 2; z++) {
+		fetch(z, z, fb, rb);
+		if (z >= z0 - 1 && z <= z0 + 1) put(z, z, fb, rb);
+		else {
+#pragma unroll
+			for (int k = 0; k < kS2PhiSlots; k++) {
+				int i = tid + kS2Threads * k;
+				if (i < kS2HX * kS2HY) cur[ps(z)][i / kS2HX][i % kS2HX] = fb[k];
+			}
+		}
+	}
+	fetch(z0 + 3, z0 + 2, fa, ra);
+	__syncthreads();
+	red(z0 - 1, false);
+	__syncthreads();
+	red(z0, true);
+	__syncthreads();
+	const int tx = tid % kS2X, ty = tid / kS2X;
+	for (int z = z0; z < z0 + zPlanes; z++) {
+		// LDS: phi z-2 .. z+2, rho z-1 .. z+1; registers A: phi z+3, rho z+2
+		fetch(z + 4, z + 3, fb, rb);  // two iterations ahead of its use
+		red(z + 1, true);
+		__syncthreads();
+		double(*c)[kS2HX] = cur[ps(z)];
+		double(*cm)[kS2HX] = cur[ps(z - 1)];
+		double(*cp)[kS2HX] = cur[ps(z + 1)];
+		int gx = x0 + tx, gy = y0 + ty;
+		int cx = tx + 2, cy = ty + 2;
+		double v = c[cy][cx];
+		if (((gx + gy + z) & 1) != 0) {
+			double xp = c[cy][cx + 1], xm = c[cy][cx - 1];
+			double yp = c[cy + 1][cx], ym = c[cy - 1][cx];
+			double zp = cp[cy][cx], zm = cm[cy][cx];
+			v = (1. / 6.) * (xp + xm + yp + ym + zp + zm + rh[rs(z)][ty + 1][tx + 1]);
+		}
+		phiOut[gidx(gx, gy, z)] = v;
+		// phi z+3 into the slot of z-2 (last read by black z-1), rho z+2 into
+		// the slot of z-1 (last read by red z-1)
+		put(z + 3, z + 2, fa, ra);
+		__syncthreads();
+#pragma unroll
+		for (int k = 0; k < kS2PhiSlots; k++) fa[k] = fb[k];
+#pragma unroll
+		for (int k = 0; k < kS2RhoSlots; k++) ra[k] = rb[k];
+	}
+}
+
 // ------------------------------------------- coarse levels in one launch ---
 // Native mode: the V-cycle below level qc (every level with at most
 // kCoarseMax points, down to 2^3) runs inside one 1024-thread workgroup with
@@ -596,6 +722,21 @@ extern "C" int pinc_hip_prolong_add(double *phiF, const double *phiC, pinc_lvl_t
 
 extern "C" int pinc_hip_gs_sweep(const double *phiIn, double *phiOut, const double *rho, pinc_lvl_t L,
                                  void *stream) {
+	// 32x8 column tiles (measured best at 256^3: 0.115 ms against 0.165 ms
+	// for k_gs_sweep), planes per workgroup chosen for >= 1024 workgroups
+	if (L.nd == 3 && L.T[0] % 32 == 0 && L.T[1] % 8 == 0 && L.T[2] % 16 == 0) {
+		long cols = (long)(L.T[0] / 32) * (L.T[1] / 8);
+		int zp = 16;
+		for (int z = 64; z > 16; z /= 2)
+			if (L.T[2] % z == 0 && cols * (L.T[2] / z) >= 1024) {
+				zp = z;
+				break;
+			}
+		unsigned nb = (unsigned)(cols * (L.T[2] / zp));
+		hipLaunchKernelGGL((k_gs_sweep2<32, 8, 256>), dim3(nb), dim3(256), 0, (hipStream_t)stream, phiIn, phiOut, rho,
+		                   L, zp);
+		return check_launch("gs_sweep2");
+	}
 	if (L.nd != 3 || L.T[0] % kSwT || L.T[1] % kSwT || L.T[2] % kSwZ)
 		return set_error(hipErrorInvalidValue, "gs_sweep: level not a multiple of the 16x16x16 tile");
 	unsigned nb = (unsigned)((L.T[0] / kSwT) * (L.T[1] / kSwT) * (L.T[2] / kSwZ));

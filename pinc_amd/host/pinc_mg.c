@@ -155,7 +155,8 @@ static void neutralize(double *a, long N) {
 static void smooth_native(MultigridSolver *S, int q, int nIter, int nd3) {
 	const pinc_lvl_t L = S->L[q];
 	/* the z-marching fused sweep pays off on large levels only (measured at
-	 * 256^3: 128^3 and below are faster, launch-latency bound, as two passes) */
+	 * 256^3: 128^3 and below are as fast, launch-latency bound, as two
+	 * passes; rechecked with the 32x8 two-ahead sweep) */
 	int fused = nd3 && L.nd == 3 && L.T[0] % 16 == 0 && L.T[1] % 16 == 0 && L.T[2] % 16 == 0 &&
 	            S->N[q] >= (1L << 23);
 	int k = 0;

@@ -26,7 +26,7 @@ def hip(built):
     return h
 
 
-@pytest.mark.parametrize("shape", [(16, 16, 16), (32, 48, 64), (64, 32, 16)])
+@pytest.mark.parametrize("shape", [(16, 16, 16), (32, 48, 64), (64, 32, 16), (64, 32, 96)])
 def test_fused_sweep_equals_two_passes(hip, shape):
     """k_gs_sweep (native mode) is one red-black iteration of mgGS3D, bit for
     bit equal to the red pass followed by the black pass."""
