@@ -44,6 +44,27 @@ ROCPROF_NAMES = {
 }
 
 
+def _pmc_traffic(prefix: str):
+    """HBM bytes per launch of the kernels whose rocprof name starts with
+    `prefix`, from the newest profiles/*_hbm_traffic.json (rocprofv3 --pmc
+    FETCH_SIZE / WRITE_SIZE passes of this same bench command, summarised by
+    tools/pmc_summary.py), launch-weighted over the kernel's variants; None
+    if no profile covers it."""
+    files = sorted((ROOT / "profiles").glob("*_hbm_traffic.json"))
+    for f in reversed(files):
+        try:
+            ks = json.loads(f.read_text())["kernels"]
+        except (OSError, ValueError, KeyError):
+            continue
+        sel = [k for k in ks if k["name"].startswith(prefix) and k.get("traffic_bytes_per_launch_mean")
+               and k["grid_size"] >= 1 << 20]
+        if sel:
+            n = sum(k["launches"] for k in sel)
+            t = sum(k["traffic_bytes_per_launch_mean"] * k["launches"] for k in sel) / n
+            return {"bytes_per_launch": t, "source": f.name, "launches": n}
+    return None
+
+
 def _cpu_baseline(size: int, ppc: int, steps: int) -> dict:
     """The oracle (plain-C restatement of the reference, one core) on a
     bounded sample of the same workload."""
@@ -198,7 +219,7 @@ def main() -> int:
                phases["accelerate"]) / K
     kernels = {}
     ROCPROF_NAMES["spectral"] = "k_spectral_scale + rocFFT r2c/c2r kernels"
-    ROCPROF_NAMES["push"] = "k_push<3, true, true>"
+    ROCPROF_NAMES["push"] = "k_push<3, true, true, *>"
     if args.mg == "native":
         ROCPROF_NAMES["gs_pass"] = "k_gs_sweep"  # one fused red-black iteration per launch
     for k, p in probes.items():
@@ -260,6 +281,8 @@ def main() -> int:
             "unit": "GB/s",
             "frac": dk["frac"],
             "traffic": None,
+            "traffic_note": "PMC HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md) from the "
+                            "committed rocprofv3 passes of this bench command, see profiles/",
             "bytes_per_launch": dk["bytes_per_launch"],
             "mean_launch_ms": dk["mean_launch_ms"],
             "samples": dk["samples"],
@@ -271,6 +294,10 @@ def main() -> int:
         "kernels": kernels,
         "cpu_baseline": None,
     }
+    tr = _pmc_traffic(dk["rocprof_name"].rstrip("*").rstrip(" ,").split("*")[0])
+    if tr is not None:
+        result["roofline"]["traffic"] = tr["bytes_per_launch"]
+        result["roofline"]["traffic_source"] = tr["source"]
     sim.close()
     os.unlink(ini)
 

@@ -94,6 +94,7 @@ struct PincDevPop {
 	int *keyCur[PINC_MAX_SPECIES];      /* cursors (exclusive offsets) */
 	int *keyWork[PINC_MAX_SPECIES];     /* scan scratch */
 	int cntValid[PINC_MAX_SPECIES];
+	int everSorted;                     /* input already in cell order once */
 	int *perm;                          /* slot of each particle after a sorted push */
 	/* multi-rank migration buffers (AoS records: nd pos, nd vel, ne) */
 	double *sendBuf[2], *recvBuf[2];

@@ -359,6 +359,7 @@ void pSyncToDevice(Population *p) {
 	PincDevPop *dv = p->dev;
 	/* new particles: a pending fused move and its deposits no longer apply */
 	dv->pending = dv->pendingSorted = dv->depValid = dv->depExtracted = 0;
+	dv->everSorted = 0;
 	for (int s = 0; s < PINC_MAX_SPECIES; s++) dv->cntValid[s] = 0;
 	/* new particle order: the cell ranges of the last tile sort no longer apply */
 	for (int s = 0; s < PINC_MAX_SPECIES; s++) dv->cellValid[s] = -1;

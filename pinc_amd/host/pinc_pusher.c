@@ -182,6 +182,11 @@ static int push_all(Population *pop, Grid *E, double *const *xout) {
 		sortNow = dv->moves % dv->sortInterval == 0;
 		countNext = (dv->moves + 1) % dv->sortInterval == 0;
 		dv->moves++;
+		/* the in-push sort relies on an input in cell order (its LDS cell
+		 * boxes are per block); a population that was never sorted (lattice
+		 * order, new particles) gets a sort pass of its own first */
+		if (sortNow && !dv->everSorted) sort_tiles(pop);
+		dv->everSorted = 1;
 	}
 	int nd = pop->nDims;
 	for (int s = 0; s < pop->nSpecies; s++) {
@@ -235,7 +240,9 @@ static int push_all(Population *pop, Grid *E, double *const *xout) {
 		 * per node) + rho flush (8 B per node) */
 		if (E) pinc_probe_end(PINC_PROBE_PUSH, slot, 32.0 * nd * np + 8.0 * (nd + 1) * (double)n);
 		if (E) {
-			if (nb > 0) pinc_check(pinc_hip_reduce(dv->kePartial, nb, 1.0, PINC_SLOT(16 + s), g_pinc.stream), "ke");
+			/* two-stage (block partials of the partials): deterministic and
+			 * fast for a million partials */
+			if (nb > 0) pinc_check(pinc_hip_sum(dv->kePartial, nb, g_pinc.dScratch, PINC_SLOT(16 + s), g_pinc.stream), "ke");
 			else pinc_check(pinc_hip_memset(PINC_SLOT(16 + s), 0, sizeof(double), g_pinc.stream), "ke");
 		}
 		if (countNext) {
@@ -584,7 +591,7 @@ static void acc(Population *pop, Grid *E, int ke) {
 		/* read pos+vel, write vel (72 B per 3-D particle) + read E once */
 		pinc_probe_end(PINC_PROBE_ACCEL, slot,
 		               24.0 * pop->nDims * (pop->iStop[s] - pop->iStart[s]) + 8.0 * E->dev->n);
-		if (nb > 0) pinc_check(pinc_hip_reduce(dv->kePartial, nb, 1.0, PINC_SLOT(16 + s), g_pinc.stream), "ke");
+		if (nb > 0) pinc_check(pinc_hip_sum(dv->kePartial, nb, g_pinc.dScratch, PINC_SLOT(16 + s), g_pinc.stream), "ke");
 		else pinc_check(pinc_hip_memset(PINC_SLOT(16 + s), 0, sizeof(double), g_pinc.stream), "ke");
 	}
 	if (ke) {
