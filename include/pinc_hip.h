@@ -165,6 +165,7 @@ int pinc_hip_deposit_cells(pinc_pop_t pop, int s, pinc_geom_t g, int tileWidth, 
  * (iStop[s] decreases by *nEmig on the host side). */
 typedef struct {
 	int *chunkOffset;   /* nChunks+1 */
+	int *scanWork;      /* 2*ceil(nChunks/4096)+1 (multi-block scan of the chunk counts) */
 	int *tail;          /* >= nEmig+1 */
 	int *holes;         /* >= nEmig+1 */
 	int *order;         /* >= nEmig   */

@@ -1824,8 +1824,17 @@ extern "C" int pinc_hip_extract(pinc_pop_t pop, int s, const unsigned char *flag
 	for (int q = 0; q < kMaxNe; q++) neCount[q] = 0;
 	if (n <= 0) return 0;
 	int nChunks = (int)ceil_div(n, PINC_CHUNK);
-	hipLaunchKernelGGL(k_scan_single, dim3(1), dim3(1024), 0, st, chunkCount, ws.chunkOffset,
-	                   nChunks);
+	if (nChunks <= 4096 || !ws.scanWork) {
+		hipLaunchKernelGGL(k_scan_single, dim3(1), dim3(1024), 0, st, chunkCount, ws.chunkOffset, nChunks);
+	} else {
+		// multi-block scan (a single workgroup takes ~0.7 ms for 5e5 chunks)
+		long nsb = ceil_div(nChunks, (long)kScanBlock);
+		int *bsum = ws.scanWork, *boff = ws.scanWork + nsb;
+		hipLaunchKernelGGL(k_scan_sums, dim3((unsigned)nsb), dim3(kThreads), 0, st, chunkCount, (long)nChunks, bsum);
+		hipLaunchKernelGGL(k_scan_single, dim3(1), dim3(1024), 0, st, bsum, boff, (int)nsb);
+		hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)nsb), dim3(kThreads), 0, st, chunkCount, (long)nChunks, boff,
+		                   ws.chunkOffset);
+	}
 	int E = 0;
 	hipError_t e = hipMemcpyAsync(&E, ws.chunkOffset + nChunks, sizeof(int), hipMemcpyDeviceToHost, st);
 	if (e != hipSuccess) return set_error(e, "extract: count readback");

@@ -42,11 +42,12 @@ static void ws_free(pinc_extract_ws_t *ws) {
 /* grow the emigrant buffers of species s to hold at least n emigrants */
 void pinc_pop_grow_ws(Population *pop, int s, long n) {
 	PincDevPop *dv = pop->dev;
-	int *chunkOffset = dv->ws[s].chunkOffset;
+	int *chunkOffset = dv->ws[s].chunkOffset, *scanWork = dv->ws[s].scanWork;
 	pinc_check(pinc_hip_stream_sync(g_pinc.stream), "grow sync");
 	ws_free(&dv->ws[s]);
 	ws_alloc(&dv->ws[s], n + n / 4 + 1024);
 	dv->ws[s].chunkOffset = chunkOffset;
+	dv->ws[s].scanWork = scanWork;
 }
 
 Population *pAlloc(const dictionary *ini) {
@@ -118,13 +119,15 @@ Population *pAlloc(const dictionary *ini) {
 	pinc_check(pinc_hip_malloc((void **)&dv->chunkCount, dv->chunkBase[ns] * sizeof(int)), "pAlloc chunks");
 	/* one KE partial per push block (PINC_CHUNK/2 particles) */
 	pinc_check(pinc_hip_malloc((void **)&dv->kePartial, (maxS / (PINC_CHUNK / 2) + 16) * sizeof(double)), "pAlloc ke");
-	pinc_check(pinc_hip_malloc((void **)&chunkOffset, (nChunks + 1) * sizeof(int)), "pAlloc chunks");
+	long scanWork = 2 * (nChunks / 4096 + 1) + 1;
+	pinc_check(pinc_hip_malloc((void **)&chunkOffset, (nChunks + 1 + scanWork) * sizeof(int)), "pAlloc chunks");
 	for (int s = 0; s < ns; s++) {
 		long capS = p->iStart[s + 1] - p->iStart[s];
 		long ecap = capS / 64;
 		if (ecap < 65536) ecap = 65536;
 		ws_alloc(&dv->ws[s], ecap);
 		dv->ws[s].chunkOffset = chunkOffset;
+		dv->ws[s].scanWork = chunkOffset + nChunks + 1;
 	}
 	double qm[PINC_MAX_SPECIES] = {0}, mq[PINC_MAX_SPECIES] = {0};
 	for (int s = 0; s < ns; s++) {
