@@ -108,6 +108,11 @@ def main() -> int:
                     help="tiled: particles re-sorted by 4^3-cell tile every --sort-interval moves (default); "
                          "reference: the reference's particle order (bit-exact indices)")
     ap.add_argument("--sort-interval", type=int, default=4)
+    ap.add_argument("--sort-fraction", type=float, default=0.0,
+                    help="> 0: sort each species once this fraction of its particles left their cell since its "
+                         "last sort (adaptive, per species; --sort-max pushes apart at most) instead of every "
+                         "--sort-interval pushes")
+    ap.add_argument("--sort-max", type=int, default=32)
     ap.add_argument("--sort-in-push", type=int, default=1,
                     help="1: the tile sort rides in every sort-interval-th push (default); 0: separate sort pass")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -155,6 +160,8 @@ def main() -> int:
         cfg["population"]["layout"] = "tiled"
         cfg["population"]["sortInterval"] = str(args.sort_interval)
         cfg["population"]["sortInPush"] = str(args.sort_in_push)
+        cfg["population"]["sortFraction"] = str(args.sort_fraction)
+        cfg["population"]["sortMax"] = str(args.sort_max)
     ini = configs.write_ini(cfg)
 
     def barrier():

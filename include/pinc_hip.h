@@ -121,6 +121,8 @@ typedef struct {
 	int *cursor;
 	int *cntNext;
 	int *perm;
+	unsigned long long *moved; /* if set: += particles that stay and changed cell */
+	unsigned long long *tstamp; /* if set: 8 phase timestamps per block (diagnostics) */
 } pinc_push_t;
 int pinc_hip_push(pinc_pop_t pop, int s, pinc_geom_t g, const pinc_push_t *args, int *nBlocks, void *stream);
 /* number of sort keys (cells incl. the wrap layer) of the tiled layout */
@@ -132,6 +134,8 @@ int pinc_hip_count_keys(pinc_pop_t pop, int s, long first, pinc_geom_t g, int ti
 int pinc_hip_scan_keys(const int *counts, long nKeys, int *offsets, int *work, void *stream);
 /* dst[i] = src[perm[i]] (velocities of a sorted push in the old order) */
 int pinc_hip_gather_perm(const double *src, const int *perm, long n, double *dst, void *stream);
+/* perm[i] = i (a species left in order by a push that sorted another one) */
+int pinc_hip_iota(int *perm, long n, void *stream);
 /* rho = the reference's per-species chain (gZero; gMul(1/q_s); add species
  * s; gMul(q_s); pusher.c:512-572) applied to per-species sums acc[s], over
  * n slab elements */

@@ -33,6 +33,17 @@ __device__ __forceinline__ T wave_sum(T v) {
 	return v;
 }
 
+template <typename T>
+__device__ __forceinline__ T wave_incl_scan(T v) {
+	const int lane = threadIdx.x & 63;
+#pragma unroll
+	for (int o = 1; o < 64; o <<= 1) {
+		T u = __shfl_up(v, o, 64);
+		if (lane >= o) v += u;
+	}
+	return v;
+}
+
 // deterministic block sum (fixed shape: blockDim multiple of 64, <=1024)
 __device__ __forceinline__ double block_sum(double v, double *lds) {
 	v = wave_sum(v);

@@ -1192,7 +1192,12 @@ struct PushArgs {
 	int *cursor;
 	int *cntNext;
 	int *perm;           // perm[i] = destination of particle i
+	unsigned long long *moved;  // += particles that stay but changed cell (nullable)
+	unsigned long long *tstamp;  // 8 phase timestamps per block (diagnostics, nullable)
 };
+// phase timestamp of the block (thread 0, s_memrealtime at 100 MHz)
+#define PUSH_TS(slot) \
+	if (a.tstamp && threadIdx.x == 0) a.tstamp[(long)blockIdx.x * 8 + (slot)] = wall_clock64()
 
 // same-cell groups of at least kPushGroupMin lanes (at most kPushGroups of
 // them per wave and item) are summed across the wave before the LDS add
@@ -1328,13 +1333,36 @@ struct Box {
 		}
 	}
 };
-__device__ __forceinline__ Box make_box(const int *clo, const int *chi, int grow_lo, int grow_hi, int nd, int cap) {
+// Box of the cells clo..chi grown by grow_lo/grow_hi, trimmed to at most cap
+// entries: each dimension first to kBoxReach cells either side of the mean
+// cell mid, then the widest one cell at a time from its side farther from mid
+// (block-uniform; vol 0 if even a single cell does not fit).
+constexpr int kBoxReach = 4;
+__device__ __forceinline__ Box make_box(const int *clo, const int *chi, const int *mid, int grow_lo, int grow_hi,
+                                        int nd, int cap) {
+	int lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
+	for (int d = 0; d < nd; d++) {
+		lo[d] = max(clo[d], mid[d] - kBoxReach);
+		hi[d] = min(chi[d], mid[d] + kBoxReach);
+		if (lo[d] > hi[d]) lo[d] = hi[d] = mid[d];
+	}
+	long v = 0;
+#pragma unroll 1
+	for (int it = 0; it < 6 * kBoxReach + 3; it++) {
+		v = 1;
+		int w = 0;
+		for (int d = 0; d < nd; d++) {
+			v *= hi[d] - lo[d] + 1 + grow_lo + grow_hi;
+			if (hi[d] - lo[d] > hi[w] - lo[w]) w = d;
+		}
+		if (v <= cap || hi[w] == lo[w]) break;
+		if (hi[w] - mid[w] >= mid[w] - lo[w]) hi[w]--;
+		else lo[w]++;
+	}
 	Box b;
-	long v = 1;
 	for (int d = 0; d < 3; d++) {
-		b.lo[d] = d < nd ? clo[d] - grow_lo : 0;
-		b.n[d] = d < nd ? chi[d] - clo[d] + 1 + grow_lo + grow_hi : 1;
-		v *= b.n[d];
+		b.lo[d] = d < nd ? lo[d] - grow_lo : 0;
+		b.n[d] = d < nd ? hi[d] - lo[d] + 1 + grow_lo + grow_hi : 1;
 	}
 	b.vol = (v <= cap && v > 0) ? (int)v : 0;
 	return b;
@@ -1393,18 +1421,27 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(4)
 	__shared__ double eL[KICK ? kEBoxCap * ND : 1];
 	__shared__ int cntIn[SORT ? kInCellCap : 1];
 	__shared__ int cntOut[kOutCellCap];
-	__shared__ int red[2 * 3 * NW];
-	__shared__ int cbox[6];
+	__shared__ int red[3 * 3 * NW];
+	__shared__ int cbox[9];
 	__shared__ double kered[NW];
 	__shared__ int wcnt[NW];
+	__shared__ int wmov[NW];
+	// sorted output staged in slot order so that each cell's run is written
+	// with consecutive lanes (one component at a time)
+	__shared__ int locStart[SORT ? kInCellCap : 1];
+	__shared__ int rlL[SORT ? kPushChunk : 1];
+	__shared__ int gdst[SORT ? kPushChunk : 1];
+	__shared__ double stage[SORT ? kPushChunk : 1];
+	__shared__ unsigned char stageF[SORT ? 2 * kPushChunk : 1];
 	const Geo32 G = make_geo32(a.g);
 	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 	const long base = (long)blockIdx.x * kPushChunk;
 
+	PUSH_TS(0);
 	// ---- phase A: load every item, cell box of the input positions
 	double p[kPushItems][ND], vv[kPushItems][ND];
 	unsigned valid = 0;
-	int lo[3] = {INT32_MAX, INT32_MAX, INT32_MAX}, hi[3] = {INT32_MIN, INT32_MIN, INT32_MIN};
+	int lo[3] = {INT32_MAX, INT32_MAX, INT32_MAX}, hi[3] = {INT32_MIN, INT32_MIN, INT32_MIN}, sm[3] = {0, 0, 0};
 #pragma unroll
 	for (int k = 0; k < kPushItems; k++) {
 		const long i = base + k * kPushThreads + threadIdx.x;
@@ -1418,42 +1455,52 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(4)
 				int c = (int)p[k][d];
 				lo[d] = min(lo[d], c);
 				hi[d] = max(hi[d], c);
+				sm[d] += c;
 			}
 		}
 	}
 #pragma unroll
 	for (int d = 0; d < ND; d++) {
-		int x = wave_min_i(lo[d]), y = wave_max_i(hi[d]);
+		int x = wave_min_i(lo[d]), y = wave_max_i(hi[d]), z = wave_sum(sm[d]);
 		if (lane == 0) {
-			red[(2 * d) * NW + wv] = x;
-			red[(2 * d + 1) * NW + wv] = y;
+			red[(3 * d) * NW + wv] = x;
+			red[(3 * d + 1) * NW + wv] = y;
+			red[(3 * d + 2) * NW + wv] = z;
 		}
 	}
 	__syncthreads();
 	if (threadIdx.x < ND) {
-		int d = threadIdx.x, x = INT32_MAX, y = INT32_MIN;
+		int d = threadIdx.x, x = INT32_MAX, y = INT32_MIN, z = 0;
 		for (int w = 0; w < NW; w++) {
-			x = min(x, red[(2 * d) * NW + w]);
-			y = max(y, red[(2 * d + 1) * NW + w]);
+			x = min(x, red[(3 * d) * NW + w]);
+			y = max(y, red[(3 * d + 1) * NW + w]);
+			z += red[(3 * d + 2) * NW + w];
 		}
+		const int nv = (int)min((long)kPushChunk, a.n - base);
 		cbox[d] = x;
 		cbox[3 + d] = y;
+		cbox[6 + d] = nv > 0 ? z / nv : 0;
 	}
 	__syncthreads();
-	int clo[3] = {0, 0, 0}, chi[3] = {0, 0, 0};
+	int clo[3] = {0, 0, 0}, chi[3] = {0, 0, 0}, cmid[3] = {0, 0, 0};
 #pragma unroll
 	for (int d = 0; d < ND; d++) {
-		clo[d] = cbox[d];
-		chi[d] = cbox[3 + d];
+		// block-uniform: scalar registers, so the boxes cost no VGPRs
+		clo[d] = __builtin_amdgcn_readfirstlane(cbox[d]);
+		chi[d] = __builtin_amdgcn_readfirstlane(cbox[3 + d]);
+		cmid[d] = __builtin_amdgcn_readfirstlane(cbox[6 + d]);
 	}
 	const bool empty = clo[0] > chi[0];
 	// E nodes of the input cells; charge nodes and cells after a move of at
-	// most one cell (|v| <= maxVel <= 1; wrapped particles fall outside)
-	const Box eB = (KICK && !empty) ? make_box(clo, chi, 0, 1, ND, kEBoxCap) : Box{{0, 0, 0}, {1, 1, 1}, 0};
-	const Box rB = !empty ? make_box(clo, chi, 1, 2, ND, kRhoBoxCap) : Box{{0, 0, 0}, {1, 1, 1}, 0};
-	const Box iB = (SORT && !empty) ? make_box(clo, chi, 0, 0, ND, kInCellCap) : Box{{0, 0, 0}, {1, 1, 1}, 0};
-	const Box oB = (a.cntNext && !empty) ? make_box(clo, chi, 1, 1, ND, kOutCellCap) : Box{{0, 0, 0}, {1, 1, 1}, 0};
+	// most one cell (|v| <= maxVel <= 1).  Each box is trimmed around the
+	// block's mean cell to its LDS capacity; the items outside it (far movers,
+	// wrapped particles) take the global path.
+	const Box eB = (KICK && !empty) ? make_box(clo, chi, cmid, 0, 1, ND, kEBoxCap) : Box{{0, 0, 0}, {1, 1, 1}, 0};
+	const Box rB = !empty ? make_box(clo, chi, cmid, 1, 2, ND, kRhoBoxCap) : Box{{0, 0, 0}, {1, 1, 1}, 0};
+	const Box iB = (SORT && !empty) ? make_box(clo, chi, cmid, 0, 0, ND, kInCellCap) : Box{{0, 0, 0}, {1, 1, 1}, 0};
+	const Box oB = (a.cntNext && !empty) ? make_box(clo, chi, cmid, 1, 1, ND, kOutCellCap) : Box{{0, 0, 0}, {1, 1, 1}, 0};
 
+	PUSH_TS(1);
 	// ---- phase B: LDS setup (zero the accumulators, stage E)
 	for (int t = threadIdx.x; t < rB.vol; t += kPushThreads) rhoL[t] = 0.0;
 	if (SORT)
@@ -1477,53 +1524,55 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(4)
 	}
 	__syncthreads();
 
-	// ---- phase C (sorted output): destination of every item
-	int dst[kPushItems];
+	PUSH_TS(2);
+	// ---- phase C (sorted output): rank of every item inside its input cell,
+	// and one global reservation per input cell of the block.  Per item, in
+	// LDS (the sort push is tight on VGPRs): rank in its cell << 8 | box cell,
+	// or ~global slot for an item outside the box.
 	if (SORT) {
-		int rank[kPushItems], lc[kPushItems];
+		static_assert(kInCellCap <= 256 && kPushChunk <= (1 << 23), "rank/cell packing");
 #pragma unroll
 		for (int k = 0; k < kPushItems; k++) {
-			rank[k] = 0;
-			lc[k] = -1;
-			if ((valid >> k) & 1u) {
-				int c[3] = {0, 0, 0};
+			int lc = -1;
+			int c[3] = {0, 0, 0};
 #pragma unroll
-				for (int d = 0; d < ND; d++) c[d] = (int)p[k][d];
-				if (iB.vol) lc[k] = iB.index(c, ND);
-			}
-			rank[k] = lds_agg_add<true>(cntIn, lc[k] < 0 ? 0 : lc[k], iB.vol && lc[k] >= 0);
+			for (int d = 0; d < ND; d++) c[d] = (int)p[k][d];
+			const bool ok = (valid >> k) & 1u;
+			if (ok && iB.inside(c, ND)) lc = iB.index(c, ND);
+			const int rank = lds_agg_add<true>(cntIn, lc < 0 ? 0 : lc, lc >= 0);
+			// outside the box: its global slot right away (wave-aggregated), as ~slot
+			const bool out = ok && lc < 0;
+			const int g = agg_add(a.cursor, out ? tile_key_cells<ND>(a.tg, c) : 0, out);
+			rlL[k * kPushThreads + threadIdx.x] = lc >= 0 ? (rank << 8 | lc) : ~g;
 		}
 		__syncthreads();
-		// one global reservation per input cell of the block
-		for (int t = threadIdx.x; t < iB.vol; t += kPushThreads) {
-			int m = cntIn[t];
+		static_assert(kInCellCap <= kPushThreads, "one reservation per thread");
+		int m = 0;
+		if ((int)threadIdx.x < iB.vol) {
+			m = cntIn[threadIdx.x];
 			if (m) {
 				int c[3] = {0, 0, 0};
-				iB.coords(t, c, ND);
-				cntIn[t] = atomicAdd(&a.cursor[tile_key_cells<ND>(a.tg, c)], m);
+				iB.coords(threadIdx.x, c, ND);
+				cntIn[threadIdx.x] = atomicAdd(&a.cursor[tile_key_cells<ND>(a.tg, c)], m);
 			}
+		}
+		// block slot of each cell's run: exclusive scan of the counts
+		const int inc = wave_incl_scan(m);
+		if (lane == 63) red[wv] = inc;
+		__syncthreads();
+		int off = 0;
+		for (int w = 0; w < wv; w++) off += red[w];
+		if ((int)threadIdx.x < iB.vol) locStart[threadIdx.x] = off + inc - m;
+		if (threadIdx.x == 0) {
+			int t = 0;
+			for (int w = 0; w < NW; w++) t += red[w];
+			cbox[0] = t;  // items in the box (the box bounds are in registers by now)
 		}
 		__syncthreads();
-#pragma unroll
-		for (int k = 0; k < kPushItems; k++) {
-			const bool ok = (valid >> k) & 1u;
-			if (iB.vol) {
-				dst[k] = ok ? cntIn[lc[k]] + rank[k] : 0;
-			} else {
-				// box too large for LDS: wave-aggregated global reservation
-				int c[3] = {0, 0, 0};
-#pragma unroll
-				for (int d = 0; d < ND; d++) c[d] = (int)p[k][d];
-				int key = ok ? tile_key_cells<ND>(a.tg, c) : 0;
-				dst[k] = agg_add(a.cursor, key, ok);
-			}
-		}
-	} else {
-#pragma unroll
-		for (int k = 0; k < kPushItems; k++) dst[k] = (int)(base + k * kPushThreads + threadIdx.x);
 	}
 
-	// ---- phase D: kick, drift, classify, store
+	PUSH_TS(3);
+	// ---- phase D: kick, drift, classify (unsorted: store)
 	double ke = 0.0;
 	int cnt = 0, bad = 0;
 	unsigned dep = 0;
@@ -1540,8 +1589,11 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(4)
 				dec[d] = p[k][d] - j[d];
 				comp[d] = 1 - dec[d];
 			}
+			bool inE = eB.vol > 0;
+#pragma unroll
+			for (int d = 0; d < ND; d++) inE = inE && j[d] >= eB.lo[d] && j[d] + 1 < eB.lo[d] + eB.n[d];
 			double e[NC][ND];
-			if (eB.vol) {
+			if (inE) {
 				const int l0 = eB.index(j, ND);
 #pragma unroll
 				for (int c = 0; c < NC; c++) {
@@ -1604,10 +1656,13 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(4)
 			ke += vsq;
 		}
 		// drift + pVelAssertMax (population.c:342-365)
+		int chg = 0;
 #pragma unroll
 		for (int d = 0; d < ND; d++) {
 			bad |= (vv[k][d] > a.maxVel);
 			p[k][d] += vv[k][d];
+			// cell changed (statistic for the sort schedule; recomputed, not kept)
+			chg |= (int)p[k][d] != (int)(p[k][d] - vv[k][d]);
 		}
 		// neighbour digit per dimension, as k_move_classify
 		int ne = 0;
@@ -1622,21 +1677,88 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(4)
 			}
 			ne = ne * 3 + dig;
 		}
-		const long o = SORT ? (long)dst[k] : i;
-#pragma unroll
-		for (int d = 0; d < ND; d++) {
-			a.xo[d][o] = p[k][d];
-			if (KICK || SORT) a.vo[d][o] = vv[k][d];
+		if (SORT) {
+			// flag staged by block slot (outside the box: by item position)
+			const int r = rlL[k * kPushThreads + threadIdx.x];
+			const int t = r >= 0 ? locStart[r & 255] + (r >> 8)
+			                         : kPushChunk + k * kPushThreads + (int)threadIdx.x;
+			stageF[t] = (unsigned char)ne;
 		}
-		a.flags[o] = (unsigned char)ne;
-		if (SORT) a.perm[i] = (int)o;
+		if (!SORT) {
+#pragma unroll
+			for (int d = 0; d < ND; d++) {
+				a.xo[d][i] = p[k][d];
+				if (KICK || a.vo[d] != a.vi[d]) a.vo[d][i] = vv[k][d];
+			}
+			a.flags[i] = (unsigned char)ne;
+		}
 		if (ne != a.center) {
-			if (SORT) atomicAdd(&a.chunkCount[o / PINC_CHUNK], 1);
-			else cnt++;
+			if (!SORT) cnt++;
 		} else {
-			dep |= 1u << k;
+			dep |= (1u | (unsigned)chg << 16) << k;  // bits 16+: changed cell
 		}
 	}
+	PUSH_TS(4);
+	if (SORT) {
+		{
+			// items in the box: block slots 0..nv-1, stored through LDS;
+			// the others straight to their global slot
+			const int nv = __builtin_amdgcn_readfirstlane(cbox[0]);
+			int slot[kPushItems];
+#pragma unroll
+			for (int k = 0; k < kPushItems; k++) {
+				slot[k] = -1;
+				if (!((valid >> k) & 1u)) continue;
+				const long i = base + k * kPushThreads + threadIdx.x;
+				const int r = rlL[k * kPushThreads + threadIdx.x];
+				if (r >= 0) {
+					const int lc = r & 255, rank = r >> 8;
+					slot[k] = locStart[lc] + rank;
+					const int o = cntIn[lc] + rank;
+					gdst[slot[k]] = o;
+					a.perm[i] = o;
+				} else {
+					const long o = ~r;
+#pragma unroll
+					for (int d = 0; d < ND; d++) {
+						a.xo[d][o] = p[k][d];
+						a.vo[d][o] = vv[k][d];
+					}
+					const int f = stageF[kPushChunk + k * kPushThreads + threadIdx.x];
+					a.flags[o] = (unsigned char)f;
+					a.perm[i] = (int)o;
+					if (f != a.center) atomicAdd(&a.chunkCount[o / PINC_CHUNK], 1);
+				}
+			}
+			__syncthreads();
+			for (int t = threadIdx.x; t < nv; t += kPushThreads) {
+				const int o = gdst[t];
+				const int f = stageF[t];
+				a.flags[o] = (unsigned char)f;
+				if (f != a.center) atomicAdd(&a.chunkCount[o / PINC_CHUNK], 1);
+			}
+			auto flush = [&](double *out) {
+				__syncthreads();
+				for (int t = threadIdx.x; t < nv; t += kPushThreads) out[gdst[t]] = stage[t];
+				__syncthreads();
+			};
+#pragma unroll
+			for (int d = 0; d < ND; d++) {
+#pragma unroll
+				for (int k = 0; k < kPushItems; k++)
+					if (slot[k] >= 0) stage[slot[k]] = p[k][d];
+				flush(a.xo[d]);
+			}
+#pragma unroll
+			for (int d = 0; d < ND; d++) {
+#pragma unroll
+				for (int k = 0; k < kPushItems; k++)
+					if (slot[k] >= 0) stage[slot[k]] = vv[k][d];
+				flush(a.vo[d]);
+			}
+		}
+	}
+	PUSH_TS(5);
 	if (a.cntNext) {
 		// count the output cells of the particles that stay (next push's sort)
 #pragma unroll
@@ -1655,7 +1777,12 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(4)
 		int wc = wave_sum(cnt);
 		if (lane == 0) wcnt[wv] = wc;
 	}
+	if (a.moved) {
+		int wm = wave_sum(__popc(dep >> 16));
+		if (lane == 0) wmov[wv] = wm;
+	}
 
+	PUSH_TS(6);
 	// ---- phase E: deposit of the particles that stay
 	auto add_corner = [&](const int *j, int c, double w) {
 		int cc[3] = {0, 0, 0};
@@ -1737,6 +1864,11 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(4)
 		for (int w = 0; w < NW; w++) t += wcnt[w];
 		if (t) atomicAdd(&a.chunkCount[base / PINC_CHUNK], t);  // zeroed by the caller
 	}
+	if (a.moved && threadIdx.x == 0) {
+		int t = 0;
+		for (int w = 0; w < NW; w++) t += wmov[w];
+		if (t) atomicAdd(a.moved, (unsigned long long)t);
+	}
 	// flush: one global atomic per touched node / output cell
 	for (int t = threadIdx.x; t < rB.vol; t += kPushThreads) {
 		double v = rhoL[t];
@@ -1761,6 +1893,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(4)
 			atomicAdd(&a.cntNext[tile_key_cells<ND>(a.tg, c)], m);
 		}
 	}
+	PUSH_TS(7);
 }
 
 // rho = chain of the species accumulators with the reference's rescaling
@@ -2113,6 +2246,8 @@ extern "C" int pinc_hip_push(pinc_pop_t pop, int s, pinc_geom_t g, const pinc_pu
 	a.cursor = args->cursor;
 	a.cntNext = args->cntNext;
 	a.perm = args->perm;
+	a.moved = args->moved;
+	a.tstamp = args->tstamp;
 	unsigned nb = (unsigned)ceil_div(n, kPushChunk);
 	*nBlocks = (int)nb;
 	hipStream_t st = (hipStream_t)stream;
@@ -2178,6 +2313,19 @@ extern "C" int pinc_hip_gather_perm(const double *src, const int *perm, long n, 
 	if (nb > 65536) nb = 65536;
 	hipLaunchKernelGGL(k_gather_perm, dim3((unsigned)nb), dim3(kThreads), 0, (hipStream_t)stream, src, perm, n, dst);
 	return check_launch("gather_perm");
+}
+
+__global__ void k_iota(int *__restrict__ perm, long n) {
+	for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+		perm[i] = (int)i;
+}
+
+extern "C" int pinc_hip_iota(int *perm, long n, void *stream) {
+	if (n <= 0) return 0;
+	long nb = ceil_div(n, (long)kThreads);
+	if (nb > 65536) nb = 65536;
+	hipLaunchKernelGGL(k_iota, dim3((unsigned)nb), dim3(kThreads), 0, (hipStream_t)stream, perm, n);
+	return check_launch("iota");
 }
 
 extern "C" int pinc_hip_rho_combine(double *rho, const double *const *acc, const double *charge, int ns, long n,

@@ -26,6 +26,7 @@ typedef struct {
 	double maxVel;
 	double thr[9];      /* migration thresholds lo[nd], up[nd], assert bound[nd] */
 	int thrSet;
+	int traceSort; /* PINC_TRACE_SORT: print the adaptive sort schedule */
 	int verbose;        /* PINC_VERBOSE=n: progress every n V-cycles */
 	int timing;
 	void *ev[2*PINC_NPHASES];
@@ -96,6 +97,14 @@ struct PincDevPop {
 	int cntValid[PINC_MAX_SPECIES];
 	int everSorted;                     /* input already in cell order once */
 	int *perm;                          /* slot of each particle after a sorted push */
+	/* adaptive sort schedule (population:sortFraction > 0): a species is
+	 * sorted once the fraction of its particles that left their cell since
+	 * its last sort would pass sortFraction, at most sortMax pushes apart */
+	double sortFraction;
+	int sortMax;
+	unsigned long long *movedCnt;       /* device, per species, this push */
+	double movedFrac[PINC_MAX_SPECIES], lastRate[PINC_MAX_SPECIES];
+	int sinceSort[PINC_MAX_SPECIES], sortNext[PINC_MAX_SPECIES];
 	/* multi-rank migration buffers (AoS records: nd pos, nd vel, ne) */
 	double *sendBuf[2], *recvBuf[2];
 	long sendCap, recvCap;

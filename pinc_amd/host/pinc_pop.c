@@ -100,7 +100,17 @@ Population *pAlloc(const dictionary *ini) {
 	 * (population:sortInPush=1, default) or runs as a pass of its own (0) */
 	dv->sorted = dv->tiled && dv->fused &&
 	             (iniHas(ini, "population:sortInPush") ? iniGetInt(ini, "population:sortInPush") : 1);
-	if (dv->sorted) pinc_check(pinc_hip_malloc((void **)&dv->perm, cap * sizeof(int)), "pAlloc perm");
+	if (dv->sorted) {
+		pinc_check(pinc_hip_malloc((void **)&dv->perm, cap * sizeof(int)), "pAlloc perm");
+		dv->sortFraction = iniHas(ini, "population:sortFraction") ? iniGetDouble(ini, "population:sortFraction") : 0.0;
+		dv->sortMax = iniHas(ini, "population:sortMax") ? iniGetInt(ini, "population:sortMax") : 32;
+		if (dv->sortFraction < 0 || dv->sortMax < 1) msg(ERROR, "population:sortFraction/sortMax out of range");
+		if (dv->sortFraction > 0) {
+			pinc_check(pinc_hip_malloc((void **)&dv->movedCnt, PINC_MAX_SPECIES * sizeof(unsigned long long)),
+			           "pAlloc moved");
+			for (int s = 0; s < PINC_MAX_SPECIES; s++) dv->sortNext[s] = 1;
+		}
+	}
 	if (dv->tiled || dv->fused) {
 		for (int d = 0; d < nd; d++) {
 			pinc_check(pinc_hip_malloc((void **)&dv->altX[d], cap * sizeof(double)), "pAlloc pos (tiled)");
@@ -164,6 +174,7 @@ void pFree(Population *p) {
 			pinc_hip_free(dv->keyWork[s]);
 		}
 		pinc_hip_free(dv->perm);
+		pinc_hip_free(dv->movedCnt);
 		for (int s = 0; s < PINC_MAX_SPECIES; s++) pinc_hip_free(dv->sortWork[s]);
 		pinc_hip_free(dv->chunkCount);
 		pinc_hip_free(dv->ws[0].chunkOffset);
@@ -363,7 +374,12 @@ void pSyncToDevice(Population *p) {
 	/* new particles: a pending fused move and its deposits no longer apply */
 	dv->pending = dv->pendingSorted = dv->depValid = dv->depExtracted = 0;
 	dv->everSorted = 0;
-	for (int s = 0; s < PINC_MAX_SPECIES; s++) dv->cntValid[s] = 0;
+	for (int s = 0; s < PINC_MAX_SPECIES; s++) {
+		dv->cntValid[s] = 0;
+		dv->sortNext[s] = 1;
+		dv->movedFrac[s] = dv->lastRate[s] = 0.0;
+		dv->sinceSort[s] = 0;
+	}
 	/* new particle order: the cell ranges of the last tile sort no longer apply */
 	for (int s = 0; s < PINC_MAX_SPECIES; s++) dv->cellValid[s] = -1;
 	for (int s = 0; s < p->nSpecies; s++) {

@@ -156,6 +156,25 @@ static void ensure_keys(Population *pop) {
 	dv->nKeys = nk;
 }
 
+/* PINC_TRACE_SORT=2: mean per-block time of each push phase (s_memrealtime,
+ * 100 MHz) and the kernel's span */
+static void push_phase_report(const unsigned long long *dts, int nb, int s, int sort, int count) {
+	unsigned long long *t = malloc((size_t)nb * 8 * sizeof(*t));
+	pinc_check(pinc_hip_d2h(t, dts, (size_t)nb * 8 * sizeof(*t), g_pinc.stream), "push timestamps");
+	double ph[7] = {0};
+	unsigned long long t0 = ~0ull, t1 = 0;
+	for (int b = 0; b < nb; b++) {
+		for (int k = 0; k < 7; k++) ph[k] += (double)(t[b * 8 + k + 1] - t[b * 8 + k]);
+		if (t[b * 8] < t0) t0 = t[b * 8];
+		if (t[b * 8 + 7] > t1) t1 = t[b * 8 + 7];
+	}
+	fprintf(stderr, "[pinc] push species %d%s%s: span %.2f ms, per block us: load+box %.2f, lds %.2f, rank %.2f, "
+	        "kick/drift %.2f, sorted stores %.2f, count %.2f, deposit %.2f\n", s, sort ? " sort" : "",
+	        count ? " count" : "", (t1 - t0) * 1e-5, ph[0] / nb * 1e-2, ph[1] / nb * 1e-2, ph[2] / nb * 1e-2,
+	        ph[3] / nb * 1e-2, ph[4] / nb * 1e-2, ph[5] / nb * 1e-2, ph[6] / nb * 1e-2);
+	free(t);
+}
+
 /* fused push of every species (pinc_hip_push): kick from E (or none), drift,
  * classification, deposit of the particles that stay into rhoS; positions to
  * xout, velocities in place.  Tiled layout: every sortInterval-th push writes
@@ -176,11 +195,23 @@ static int push_all(Population *pop, Grid *E, double *const *xout) {
 			pinc_check(pinc_hip_malloc((void **)&dv->rhoS[s], n * sizeof(double)), "species charge");
 		dv->rhoN = n;
 	}
-	int sortNow = 0, countNext = 0;
+	int sortNow = 0, sortS[PINC_MAX_SPECIES] = {0}, countS[PINC_MAX_SPECIES] = {0};
+	int adaptive = dv->sorted && dv->sortFraction > 0;
 	if (dv->sorted) {
 		ensure_keys(pop);
-		sortNow = dv->moves % dv->sortInterval == 0;
-		countNext = (dv->moves + 1) % dv->sortInterval == 0;
+		for (int s = 0; s < pop->nSpecies; s++) {
+			if (adaptive) {
+				/* sort when this push's input is the one predicted to pass
+				 * the displaced fraction (counted by the push before) */
+				sortS[s] = dv->sortNext[s];
+				countS[s] = !sortS[s] && (dv->movedFrac[s] + dv->lastRate[s] >= dv->sortFraction ||
+				                          dv->sinceSort[s] + 1 >= dv->sortMax);
+			} else {
+				sortS[s] = dv->moves % dv->sortInterval == 0;
+				countS[s] = (dv->moves + 1) % dv->sortInterval == 0;
+			}
+			sortNow |= sortS[s];
+		}
 		dv->moves++;
 		/* the in-push sort relies on an input in cell order (its LDS cell
 		 * boxes are per block); a population that was never sorted (lattice
@@ -189,7 +220,11 @@ static int push_all(Population *pop, Grid *E, double *const *xout) {
 		dv->everSorted = 1;
 	}
 	int nd = pop->nDims;
+	if (adaptive)
+		pinc_check(pinc_hip_memset(dv->movedCnt, 0, PINC_MAX_SPECIES * sizeof(unsigned long long), g_pinc.stream),
+		           "moved counts");
 	for (int s = 0; s < pop->nSpecies; s++) {
+		int countNext = countS[s];
 		pinc_check(pinc_hip_zero(dv->rhoS[s], n, g_pinc.stream), "species charge zero");
 		pinc_push_t a;
 		memset(&a, 0, sizeof(a));
@@ -218,7 +253,12 @@ static int push_all(Population *pop, Grid *E, double *const *xout) {
 		a.kePartial = dv->kePartial;
 		a.tileWidth = dv->tileWidth;
 		pinc_check(pinc_hip_memset(a.chunkCount, 0, chunks * sizeof(int), g_pinc.stream), "chunk counts");
-		if (sortNow) {
+		if (adaptive) a.moved = dv->movedCnt + s;
+		/* a species left in order by a sorting push still goes to the
+		 * alternate arrays (swapped for all species), perm = identity */
+		if (sortNow && !sortS[s]) pinc_check(pinc_hip_iota(dv->perm + pop->iStart[s], np, g_pinc.stream), "perm");
+		if (sortS[s]) {
+			a.perm = dv->perm + pop->iStart[s];
 			if (!dv->cntValid[s]) {
 				pinc_check(pinc_hip_memset(dv->keyCnt[s], 0, (dv->nKeys + 1) * sizeof(int), g_pinc.stream), "keys");
 				pinc_check(pinc_hip_count_keys(p, s, 0, g, dv->tileWidth, dv->keyCnt[s], g_pinc.stream), "count keys");
@@ -226,7 +266,6 @@ static int push_all(Population *pop, Grid *E, double *const *xout) {
 			pinc_check(pinc_hip_scan_keys(dv->keyCnt[s], dv->nKeys, dv->keyCur[s], dv->keyWork[s], g_pinc.stream),
 			           "scan keys");
 			a.cursor = dv->keyCur[s];
-			a.perm = dv->perm + pop->iStart[s];
 			dv->cellValid[s] = -1;
 		}
 		if (countNext) {
@@ -234,8 +273,17 @@ static int push_all(Population *pop, Grid *E, double *const *xout) {
 			a.cntNext = dv->keyNext[s];
 		}
 		int nb = 0;
+		unsigned long long *ts = NULL;
+		if (g_pinc.traceSort > 1) {
+			pinc_check(pinc_hip_malloc((void **)&ts, (np / 1024 + 1) * 8 * sizeof(*ts)), "push timestamps");
+			a.tstamp = ts;
+		}
 		int slot = E ? pinc_probe_begin(PINC_PROBE_PUSH) : -1;
 		pinc_check(pinc_hip_push(p, s, g, &a, &nb, g_pinc.stream), "push");
+		if (ts) {
+			push_phase_report(ts, nb, s, sortS[s], countNext);
+			pinc_hip_free(ts);
+		}
 		/* pos R+W, vel R+W (32 B per dim per particle) + E R (8 B per value
 		 * per node) + rho flush (8 B per node) */
 		if (E) pinc_probe_end(PINC_PROBE_PUSH, slot, 32.0 * nd * np + 8.0 * (nd + 1) * (double)n);
@@ -252,6 +300,21 @@ static int push_all(Population *pop, Grid *E, double *const *xout) {
 			dv->cntValid[s] = 1;
 		} else if (dv->sorted) {
 			dv->cntValid[s] = 0;
+		}
+	}
+	if (adaptive) {
+		unsigned long long mv[PINC_MAX_SPECIES];
+		pinc_check(pinc_hip_d2h(mv, dv->movedCnt, pop->nSpecies * sizeof(mv[0]), g_pinc.stream), "moved readback");
+		for (int s = 0; s < pop->nSpecies; s++) {
+			long np = pop->iStop[s] - pop->iStart[s];
+			double rate = np > 0 ? (double)mv[s] / (double)np : 0.0;
+			dv->movedFrac[s] = sortS[s] ? rate : dv->movedFrac[s] + rate;
+			dv->sinceSort[s] = sortS[s] ? 1 : dv->sinceSort[s] + 1;
+			dv->lastRate[s] = rate;
+			dv->sortNext[s] = countS[s];
+			if (g_pinc.traceSort)
+				fprintf(stderr, "[pinc] push %ld species %d: moved %.4f, displaced %.4f%s%s\n", dv->moves, s, rate,
+				        dv->movedFrac[s], sortS[s] ? ", sorted" : "", countS[s] ? ", counted" : "");
 		}
 	}
 	dv->depValid = 1;

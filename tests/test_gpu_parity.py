@@ -206,19 +206,24 @@ def _sorted_rows(a):
     return a[np.lexsort(a.T[::-1])]
 
 
-@pytest.mark.parametrize("name,kw,maxwell", [("cold3d", {}, False),
-                                              ("warm", {"true_size": (32, 32, 32), "ppc": 8, "nalloc_pc": 16,
-                                                        "levels": 3}, True),
-                                              ("langmuir2d", {}, False)])
-def test_tiled_layout(sim_cls, name, kw, maxwell):
+_WARM32 = {"true_size": (32, 32, 32), "ppc": 8, "nalloc_pc": 16, "levels": 3}
+
+
+@pytest.mark.parametrize("name,kw,maxwell,sched", [("cold3d", {}, False, {"sortInterval": "2"}),
+                                                   ("warm", _WARM32, True, {"sortInterval": "2"}),
+                                                   ("warm", _WARM32, True, {"sortFraction": "0.03", "sortMax": "3"}),
+                                                   ("langmuir2d", {}, False, {"sortInterval": "2"}),
+                                                   ("langmuir2d", {}, False, {"sortFraction": "0.01"})])
+def test_tiled_layout(sim_cls, name, kw, maxwell, sched):
     """population:layout=tiled (particles re-sorted by tile every
-    sortInterval moves; not the reference's order) gives the same particles
-    and energies as the reference layout: the set of positions after the
-    first move is bit-identical, energies follow the oracle to 1e-8."""
+    sortInterval moves, or per species once sortFraction of them left their
+    cell; not the reference's order) gives the same particles and energies as
+    the reference layout: the set of positions after the first move is
+    bit-identical, energies follow the oracle to 1e-8."""
     cfg = configs.config(name, **kw)
     ini_ref = configs.write_ini(cfg)
     cfg["population"]["layout"] = "tiled"
-    cfg["population"]["sortInterval"] = "2"
+    cfg["population"].update(sched)
     ini_t = configs.write_ini(cfg)
     steps = 5
     w = orc.World(ini_ref)
