@@ -107,7 +107,7 @@ def main() -> int:
     ap.add_argument("--layout", default="tiled", choices=["tiled", "reference"],
                     help="tiled: particles re-sorted by 4^3-cell tile every --sort-interval moves (default); "
                          "reference: the reference's particle order (bit-exact indices)")
-    ap.add_argument("--sort-interval", type=int, default=4)
+    ap.add_argument("--sort-interval", type=int, default=8)
     ap.add_argument("--sort-fraction", type=float, default=0.0,
                     help="> 0: sort each species once this fraction of its particles left their cell since its "
                          "last sort (adaptive, per species; --sort-max pushes apart at most) instead of every "

@@ -91,7 +91,7 @@ Population *pAlloc(const dictionary *ini) {
 	}
 	dv->fused = iniHas(ini, "population:fused") ? iniGetInt(ini, "population:fused") : 1;
 	if (dv->tiled) {
-		dv->sortInterval = iniHas(ini, "population:sortInterval") ? iniGetInt(ini, "population:sortInterval") : 4;
+		dv->sortInterval = iniHas(ini, "population:sortInterval") ? iniGetInt(ini, "population:sortInterval") : 8;
 		if (dv->sortInterval < 1) msg(ERROR, "population:sortInterval must be >= 1");
 		dv->tileWidth = nd == 3 ? 4 : (nd == 2 ? 8 : 32);
 		for (int s = 0; s < PINC_MAX_SPECIES; s++) dv->cellValid[s] = -1;
