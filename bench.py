@@ -228,7 +228,8 @@ def main() -> int:
     ROCPROF_NAMES["spectral"] = "k_spectral_scale + rocFFT r2c/c2r kernels"
     ROCPROF_NAMES["push"] = "k_push<3, true, true, *>"
     if args.mg == "native":
-        ROCPROF_NAMES["gs_pass"] = "k_gs_sweep2<32, 8, 256>"  # one fused red-black iteration per launch
+        # two red-black iterations per launch (24 B per point: phi R+W, rho R)
+        ROCPROF_NAMES["gs_pass"] = "k_gs_sweep4<32, 8, 256>"
     for k, p in probes.items():
         if p["samples"] == 0 or p["mean_ms"] <= 0:
             continue

@@ -280,6 +280,11 @@ int pinc_hip_gs_pass(double *phi, const double *rho, pinc_lvl_t L, int pass, int
  * Needs a 3-D level with T[0], T[1], T[2] multiples of 16. */
 int pinc_hip_gs_sweep(const double *phiIn, double *phiOut, const double *rho, pinc_lvl_t L,
                       void *stream);
+/* Native mode: two full red-black iterations phiIn -> phiOut in one pass
+ * (z-march four stages deep); bit-identical to two pinc_hip_gs_sweep calls.
+ * Needs T[0] % 32, T[1] % 8 and T[2] % 16 == 0. */
+int pinc_hip_gs_sweep2x(const double *phiIn, double *phiOut, const double *rho, pinc_lvl_t L,
+                        void *stream);
 /* Native mode: the whole V-cycle below (and including) a coarse level in one
  * 1024-thread workgroup, grids in LDS (at most 4800 points over all levels,
  * 3-D, each level half the previous).  levels[0] is the top coarse level:

@@ -491,6 +491,173 @@ __global__ __launch_bounds__(kS2Threads) void k_gs_sweep2(const double *__restri
 	}
 }
 
+// ------------------------------------ two red-black iterations per launch ---
+// The same z-march as k_gs_sweep2, four stages deep.  At step s the
+// workgroup updates, in a first phase, red (1st iteration) on plane s+3, red
+// (2nd) on s and black (2nd) on s-2, which it writes out; then, after one
+// barrier, black (1st) on s+2.  The stages of a phase only read planes the
+// others do not write, and each reads the phi plane ring as the stage before
+// it left it (in place: a stage overwrites only values no later stage
+// needs), so a step costs two barriers.  Each stage is computed on a region
+// one node wider than the next, so the tile needs a four-node halo and no
+// exchange with its neighbours.  rho is not staged: every thread loads the
+// rho values of its own stage nodes two steps ahead into registers, which
+// keeps the LDS at 40 KB and four workgroups on a CU (the march is
+// latency-bound: a step waits for loads issued two steps earlier).  phiIn is read and phiOut
+// written once per two iterations; the arithmetic is that of mgGS3D's red
+// and black passes, so the result is bit-identical to two k_gs_sweep2
+// launches.
+template <int SX, int SY, int NT>
+struct Sweep4 {
+	static constexpr int H = 4;  // phi halo
+	static constexpr int HX = SX + 2 * H, HY = SY + 2 * H;
+	static constexpr int NP = 8;  // ring planes
+	static constexpr int PhiSlots = (HX * HY + NT - 1) / NT;
+	// nodes of one colour on the tile grown by h (rows have even length)
+	static constexpr int nodes(int h) { return (SX + 2 * h) / 2 * (SY + 2 * h); }
+	static constexpr int K3 = (nodes(3) + NT - 1) / NT, K2 = (nodes(2) + NT - 1) / NT,
+	                     K1 = (nodes(1) + NT - 1) / NT;
+};
+
+template <int SX, int SY, int NT>
+__global__ __launch_bounds__(NT) void k_gs_sweep4(const double *__restrict__ phiIn, double *__restrict__ phiOut,
+                                                  const double *__restrict__ rho, pinc_lvl_t Lp, int zPlanes) {
+	using S = Sweep4<SX, SY, NT>;
+	constexpr int HX = S::HX, HY = S::HY, H = S::H, K3 = S::K3, K2 = S::K2, K1 = S::K1;
+	__shared__ double cur[S::NP][HY][HX];
+	const int TX = Lp.T[0], TY = Lp.T[1], TZ = Lp.T[2];
+	const long sy = TX, sz = (long)TX * TY;
+	const int ntx = TX / SX, nty = TY / SY;
+	const int bx = blockIdx.x % ntx, by = (blockIdx.x / ntx) % nty, bz = blockIdx.x / (ntx * nty);
+	const int x0 = bx * SX, y0 = by * SY, z0 = bz * zPlanes;
+	const int tid = threadIdx.x;
+	auto wrapi = [](int i, int T) { return i < 0 ? i + T : (i >= T ? i - T : i); };
+	auto gidx = [&](int x, int y, int z) {
+		return (long)wrapi(x, TX) + wrapi(y, TY) * sy + (long)wrapi(z, TZ) * sz;
+	};
+	auto ps = [](int z) { return (z + 8 * 16) % S::NP; };
+	auto fetch = [&](int zf, double *f) {
+#pragma unroll
+		for (int k = 0; k < S::PhiSlots; k++) {
+			int i = tid + NT * k;
+			if (i < HX * HY) f[k] = phiIn[gidx(x0 + i % HX - H, y0 + i / HX - H, zf)];
+		}
+	};
+	auto putPhi = [&](int zf, const double *f) {
+#pragma unroll
+		for (int k = 0; k < S::PhiSlots; k++) {
+			int i = tid + NT * k;
+			if (i < HX * HY) cur[ps(zf)][i / HX][i % HX] = f[k];
+		}
+	};
+	// node j of colour `parity` on plane p, tile grown by h: tile coordinates
+	auto node = [&](int j, int p, int parity, int h, int &tx, int &ty) {
+		const int hw = (SX + 2 * h) / 2;
+		ty = j / hw - h;
+		tx = -h + 2 * (j % hw) + ((parity - (x0 - h + y0 + ty + p)) & 1);
+	};
+	// rho of this thread's nodes in the four stages of step s
+	struct Rho {
+		double r1[K3], b1[K2], r2[K1], b2;
+	};
+	auto fetchRho = [&](int s, Rho &R) {
+		int tx, ty;
+#pragma unroll
+		for (int k = 0; k < K3; k++) {
+			const int j = tid + NT * k;
+			if (j < S::nodes(3)) {
+				node(j, s + 3, 0, 3, tx, ty);
+				R.r1[k] = rho[gidx(x0 + tx, y0 + ty, s + 3)];
+			}
+		}
+#pragma unroll
+		for (int k = 0; k < K2; k++) {
+			const int j = tid + NT * k;
+			if (j < S::nodes(2)) {
+				node(j, s + 2, 1, 2, tx, ty);
+				R.b1[k] = rho[gidx(x0 + tx, y0 + ty, s + 2)];
+			}
+		}
+#pragma unroll
+		for (int k = 0; k < K1; k++) {
+			const int j = tid + NT * k;
+			if (j < S::nodes(1)) {
+				node(j, s, 0, 1, tx, ty);
+				R.r2[k] = rho[gidx(x0 + tx, y0 + ty, s)];
+			}
+		}
+		R.b2 = rho[gidx(x0 + tid % SX, y0 + tid / SX, s - 2)];
+	};
+	// colour `parity` of plane p on the tile grown by h, in place
+	auto stage = [&](int p, int parity, int h, const double *rv, int nk) {
+		double(*c)[HX] = cur[ps(p)];
+		double(*cm)[HX] = cur[ps(p - 1)];
+		double(*cp)[HX] = cur[ps(p + 1)];
+#pragma unroll
+		for (int k = 0; k < 2; k++) {
+			const int j = tid + NT * k;
+			if (k >= nk || j >= S::nodes(h)) break;
+			int tx, ty;
+			node(j, p, parity, h, tx, ty);
+			const int cx = tx + H, cy = ty + H;
+			double xp = c[cy][cx + 1], xm = c[cy][cx - 1];
+			double yp = c[cy + 1][cx], ym = c[cy - 1][cx];
+			double zp = cp[cy][cx], zm = cm[cy][cx];
+			c[cy][cx] = (1. / 6.) * (xp + xm + yp + ym + zp + zm + rv[k]);
+		}
+	};
+	static_assert(K3 <= 2 && K2 <= 2 && K1 <= 2, "stage loops are unrolled twice");
+	static_assert(SX * SY == NT, "one output node per thread and plane");
+
+	// prologue: phi z0-4 .. z0-2 into LDS, z0-1 into registers A; rho of
+	// the first two steps
+	double fa[S::PhiSlots], fb[S::PhiSlots];
+	for (int z = z0 - 4; z <= z0 - 2; z++) {
+		fetch(z, fb);
+		putPhi(z, fb);
+	}
+	fetch(z0 - 1, fa);
+	Rho RA, RB, RC;
+	fetchRho(z0 - 6, RA);
+	fetchRho(z0 - 5, RB);
+	__syncthreads();
+	const int tx = tid % SX, ty = tid / SX;
+	const int zEnd = z0 + zPlanes;  // outputs z0 .. zEnd-1
+	for (int s = z0 - 6; s <= zEnd + 1; s++) {
+		// LDS: phi s-3 .. s+4 (those each stage reads)
+		if (s <= zEnd) {  // two steps ahead of their use
+			fetch(s + 6, fb);
+			fetchRho(s + 2, RC);
+		}
+		if (s + 3 <= zEnd + 2) stage(s + 3, 0, 3, RA.r1, K3);          // red, 1st iteration
+		if (s >= z0 - 1 && s <= zEnd) stage(s, 0, 1, RA.r2, K1);       // red, 2nd
+		if (s - 2 >= z0 && s - 2 < zEnd) {                              // black, 2nd: out
+			const int zo = s - 2;
+			double(*c)[HX] = cur[ps(zo)];
+			double(*cm)[HX] = cur[ps(zo - 1)];
+			double(*cp)[HX] = cur[ps(zo + 1)];
+			const int gx = x0 + tx, gy = y0 + ty, cx = tx + H, cy = ty + H;
+			double v = c[cy][cx];
+			if (((gx + gy + zo) & 1) != 0) {
+				double xp = c[cy][cx + 1], xm = c[cy][cx - 1];
+				double yp = c[cy + 1][cx], ym = c[cy - 1][cx];
+				double zp = cp[cy][cx], zm = cm[cy][cx];
+				v = (1. / 6.) * (xp + xm + yp + ym + zp + zm + RA.b2);
+			}
+			phiOut[gidx(gx, gy, zo)] = v;
+		}
+		__syncthreads();
+		if (s + 2 >= z0 - 2 && s + 2 <= zEnd + 1) stage(s + 2, 1, 2, RA.b1, K2);  // black, 1st
+		// phi s+5 into the slot of s-3 (last read by the black output above)
+		putPhi(s + 5, fa);
+		__syncthreads();
+#pragma unroll
+		for (int k = 0; k < S::PhiSlots; k++) fa[k] = fb[k];
+		RA = RB;
+		RB = RC;
+	}
+}
+
 // ------------------------------------------- coarse levels in one launch ---
 // Native mode: the V-cycle below level qc (every level with at most
 // kCoarseMax points, down to 2^3) runs inside one 1024-thread workgroup with
@@ -742,6 +909,25 @@ extern "C" int pinc_hip_gs_sweep(const double *phiIn, double *phiOut, const doub
 	unsigned nb = (unsigned)((L.T[0] / kSwT) * (L.T[1] / kSwT) * (L.T[2] / kSwZ));
 	hipLaunchKernelGGL(k_gs_sweep, dim3(nb), dim3(256), 0, (hipStream_t)stream, phiIn, phiOut, rho, L);
 	return check_launch("gs_sweep");
+}
+
+extern "C" int pinc_hip_gs_sweep2x(const double *phiIn, double *phiOut, const double *rho, pinc_lvl_t L,
+                                   void *stream) {
+	// two iterations per launch; 32x8 column tiles, planes per workgroup for
+	// >= 1024 workgroups where the level allows (at least 16)
+	if (L.nd != 3 || L.T[0] % 32 || L.T[1] % 8 || L.T[2] % 16)
+		return set_error(hipErrorInvalidValue, "gs_sweep2x: level not a multiple of the 32x8x16 tile");
+	long cols = (long)(L.T[0] / 32) * (L.T[1] / 8);
+	int zp = 16;
+	for (int z = 64; z > 16; z /= 2)
+		if (L.T[2] % z == 0 && cols * (L.T[2] / z) >= 1024) {
+			zp = z;
+			break;
+		}
+	unsigned nb = (unsigned)(cols * (L.T[2] / zp));
+	hipLaunchKernelGGL((k_gs_sweep4<32, 8, 256>), dim3(nb), dim3(256), 0, (hipStream_t)stream, phiIn, phiOut, rho, L,
+	                   zp);
+	return check_launch("gs_sweep2x");
 }
 
 extern "C" int pinc_hip_mg_coarse(const double *rho, double *phi, int nLevels, const pinc_lvl_t *levels, int nPre,

@@ -160,9 +160,21 @@ static void smooth_native(MultigridSolver *S, int q, int nIter, int nd3) {
 	int fused = nd3 && L.nd == 3 && L.T[0] % 16 == 0 && L.T[1] % 16 == 0 && L.T[2] % 16 == 0 &&
 	            S->N[q] >= (1L << 23);
 	int k = 0;
+	/* two iterations per launch (pinc_hip_gs_sweep2x) in pairs, so that the
+	 * ping-pong ends in phi */
+	int fused2 = fused && L.T[0] % 32 == 0 && L.T[1] % 8 == 0;
+	if (fused2) {
+		for (; k + 4 <= nIter; k += 4) {
+			int slot = q == 0 ? pinc_probe_begin(PINC_PROBE_GS) : -1;
+			pinc_check(pinc_hip_gs_sweep2x(S->phi[q], S->res[q], S->rho[q], L, g_pinc.stream), "gs sweep2x");
+			/* two full iterations: phi R + W, rho R (24 B per point) once */
+			pinc_probe_end(PINC_PROBE_GS, slot, 24.0 * S->N[q]);
+			pinc_check(pinc_hip_gs_sweep2x(S->res[q], S->phi[q], S->rho[q], L, g_pinc.stream), "gs sweep2x");
+		}
+	}
 	if (fused) {
 		for (; k + 2 <= nIter; k += 2) {
-			int slot = q == 0 ? pinc_probe_begin(PINC_PROBE_GS) : -1;
+			int slot = q == 0 && !fused2 ? pinc_probe_begin(PINC_PROBE_GS) : -1;
 			pinc_check(pinc_hip_gs_sweep(S->phi[q], S->res[q], S->rho[q], L, g_pinc.stream), "gs sweep");
 			/* one full iteration: phi R + W, rho R (24 B per point) */
 			pinc_probe_end(PINC_PROBE_GS, slot, 24.0 * S->N[q]);

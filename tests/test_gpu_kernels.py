@@ -22,6 +22,7 @@ def hip(built):
     h = _lib.HIP
     vp = C.c_void_p
     h.pinc_hip_gs_sweep.argtypes = [vp, vp, vp, Lvl, vp]
+    h.pinc_hip_gs_sweep2x.argtypes = [vp, vp, vp, Lvl, vp]
     h.pinc_hip_gs_pass.argtypes = [vp, vp, Lvl, C.c_int, C.c_int, vp, vp, C.POINTER(C.c_int), vp]
     return h
 
@@ -52,6 +53,37 @@ def test_fused_sweep_equals_two_passes(hip, shape):
     r = rho.cpu().numpy().reshape(tz, ty, tx)
     z, y, x = np.meshgrid(np.arange(tz), np.arange(ty), np.arange(tx), indexing="ij")
     for colour in (0, 1):
+        m = ((x + y + z) & 1) == colour
+        s = (np.roll(a, -1, 2) + np.roll(a, 1, 2)) + np.roll(a, -1, 1)
+        s = ((s + np.roll(a, 1, 1)) + np.roll(a, -1, 0)) + np.roll(a, 1, 0)
+        a = np.where(m, (1.0 / 6.0) * (s + r), a)
+    np.testing.assert_array_equal(out.cpu().numpy().reshape(tz, ty, tx), a)
+
+
+@pytest.mark.parametrize("shape", [(32, 8, 16), (64, 32, 96), (32, 16, 64), (96, 24, 32)])
+def test_double_sweep_equals_two_sweeps(hip, shape):
+    """k_gs_sweep4 (two red-black iterations per launch, four-stage z-march)
+    is bit for bit equal to two single-iteration sweeps, and to the numpy
+    restatement of two red-black iterations."""
+    import torch
+    tx, ty, tz = shape
+    n = tx * ty * tz
+    g = torch.Generator(device="cpu").manual_seed(2)
+    phi = torch.randn(n, dtype=torch.float64, generator=g).cuda()
+    rho = torch.randn(n, dtype=torch.float64, generator=g).cuda()
+    out = torch.full_like(phi, float("nan"))
+    mid = torch.empty_like(phi)
+    ref = torch.empty_like(phi)
+    L = Lvl(3, (C.c_int * 3)(tx, ty, tz))
+    assert hip.pinc_hip_gs_sweep2x(phi.data_ptr(), out.data_ptr(), rho.data_ptr(), L, None) == 0
+    assert hip.pinc_hip_gs_sweep(phi.data_ptr(), mid.data_ptr(), rho.data_ptr(), L, None) == 0
+    assert hip.pinc_hip_gs_sweep(mid.data_ptr(), ref.data_ptr(), rho.data_ptr(), L, None) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    a = phi.cpu().numpy().reshape(tz, ty, tx).copy()
+    r = rho.cpu().numpy().reshape(tz, ty, tx)
+    z, y, x = np.meshgrid(np.arange(tz), np.arange(ty), np.arange(tx), indexing="ij")
+    for colour in (0, 1, 0, 1):
         m = ((x + y + z) & 1) == colour
         s = (np.roll(a, -1, 2) + np.roll(a, 1, 2)) + np.roll(a, -1, 1)
         s = ((s + np.roll(a, 1, 1)) + np.roll(a, -1, 0)) + np.roll(a, 1, 0)
