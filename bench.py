@@ -41,6 +41,7 @@ ROCPROF_NAMES = {
     "move_classify": "k_move_classify<3>",
     "deposit": "k_deposit_tiled<3, true>",
     "residual_sumsq": "k_residual_sumsq<3>",
+    "mg_cycle": "one V-cycle, replayed as a HIP graph (all levels)",
 }
 
 

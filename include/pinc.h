@@ -254,7 +254,8 @@ int pinc_sim_timers_reset(PincSim *sim);
 #define PINC_PROBE_RESIDUAL 4  /* residual norm, finest level */
 #define PINC_PROBE_SPECTRAL 5  /* spectral solve (r2c + scale + c2r) */
 #define PINC_PROBE_PUSH 6      /* fused kick + drift + classify + deposit */
-#define PINC_NPROBES 7
+#define PINC_PROBE_CYCLE 7     /* one V-cycle replayed as a graph (multigrid:graph) */
+#define PINC_NPROBES 8
 #define PINC_PROBE_ALL (-1)
 int pinc_probe_start(int kernel, int maxSamples);
 int pinc_probe_read(int kernel, double *meanMs, double *meanBytes, int *samples, long *launches);

@@ -58,6 +58,14 @@ const char *pinc_hip_error_string(void);
 int pinc_hip_set_device(int dev);
 int pinc_hip_device_count(int *n);
 int pinc_hip_stream_create(void **stream);
+/* Stream capture of a fixed launch sequence into a graph (MG V-cycle replay;
+ * replaces the reference's per-call dispatch, no reference counterpart):
+ * begin on a non-default stream, end -> instantiated executable, launch on a
+ * stream, destroy. */
+int pinc_hip_capture_begin(void *stream);
+int pinc_hip_capture_end(void *stream, void **exec);
+int pinc_hip_graph_launch(void *exec, void *stream);
+int pinc_hip_graph_destroy(void *exec);
 int pinc_hip_stream_destroy(void *stream);
 int pinc_hip_stream_sync(void *stream);
 int pinc_hip_device_sync(void);

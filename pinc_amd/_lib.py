@@ -70,7 +70,7 @@ _sigs = {
     "pinc_probe_read": (C.c_int, [C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_int),
                                   C.POINTER(C.c_long)]),
 }
-PROBES = {"gs_pass": 0, "accelerate": 1, "move_classify": 2, "deposit": 3, "residual_sumsq": 4, "spectral": 5, "push": 6}
+PROBES = {"gs_pass": 0, "accelerate": 1, "move_classify": 2, "deposit": 3, "residual_sumsq": 4, "spectral": 5, "push": 6, "mg_cycle": 7}
 
 
 def probe_start(kernel: str = "all", max_samples: int = 4096) -> None:

@@ -62,6 +62,34 @@ extern "C" int pinc_hip_stream_destroy(void *stream) {
 	return 0;
 }
 
+// stream capture into a replayable graph (a fixed launch sequence, e.g. one
+// V-cycle): begin, end -> instantiated executable, launch, destroy
+extern "C" int pinc_hip_capture_begin(void *stream) {
+	HIPCALL(hipStreamBeginCapture((hipStream_t)stream, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
+	return 0;
+}
+
+extern "C" int pinc_hip_capture_end(void *stream, void **exec) {
+	hipGraph_t g = nullptr;
+	HIPCALL(hipStreamEndCapture((hipStream_t)stream, &g), "hipStreamEndCapture");
+	hipGraphExec_t e = nullptr;
+	hipError_t r = hipGraphInstantiate(&e, g, nullptr, nullptr, 0);
+	(void)hipGraphDestroy(g);
+	HIPCALL(r, "hipGraphInstantiate");
+	*exec = (void *)e;
+	return 0;
+}
+
+extern "C" int pinc_hip_graph_launch(void *exec, void *stream) {
+	HIPCALL(hipGraphLaunch((hipGraphExec_t)exec, (hipStream_t)stream), "hipGraphLaunch");
+	return 0;
+}
+
+extern "C" int pinc_hip_graph_destroy(void *exec) {
+	if (exec) HIPCALL(hipGraphExecDestroy((hipGraphExec_t)exec), "hipGraphExecDestroy");
+	return 0;
+}
+
 extern "C" int pinc_hip_stream_sync(void *stream) {
 	HIPCALL(hipStreamSynchronize((hipStream_t)stream), "hipStreamSynchronize");
 	return 0;

@@ -529,7 +529,7 @@ int pinc_probe_start(int kernel, int maxSamples) {
 }
 
 int pinc_probe_begin(int k) {
-	if (!g_pinc.probeOn[k]) return -1;
+	if (!g_pinc.probeOn[k] || g_pinc.capturing) return -1;
 	g_pinc.probeLaunches[k]++;
 	if (g_pinc.probeN[k] >= g_pinc.probeMax) return -1;
 	int slot = g_pinc.probeN[k]++;

@@ -26,6 +26,7 @@ typedef struct {
 	double maxVel;
 	double thr[9];      /* migration thresholds lo[nd], up[nd], assert bound[nd] */
 	int thrSet;
+	int capturing; /* a stream capture is open: no event probes */
 	int traceSort; /* PINC_TRACE_SORT: print the adaptive sort schedule */
 	int verbose;        /* PINC_VERBOSE=n: progress every n V-cycles */
 	int timing;
@@ -132,6 +133,8 @@ struct MultigridSolver {
 	long cycles;
 	Grid *rhoGrid, *phiGrid;
 	int native;
+	int useGraph;      /* multigrid:graph: replay one captured V-cycle */
+	void *cycleGraph;  /* instantiated graph of vrec(S, 0) */
 };
 
 /* collectives over RCCL or the host transport (pinc_comm.c) */

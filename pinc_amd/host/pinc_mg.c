@@ -75,6 +75,10 @@ MultigridSolver *mgAllocSolver(const dictionary *ini, Grid *rho, Grid *phi) {
 	free(re);
 	free(pr);
 	S->native = iniHas(ini, "multigrid:native") ? iniGetInt(ini, "multigrid:native") : 0;
+	/* graph replay of the V-cycle (native mode, opt-in: measured neutral at
+	 * C4, the gaps between dependent kernels are GPU-side) */
+	S->useGraph = S->native && iniHas(ini, "multigrid:graph") && iniGetInt(ini, "multigrid:graph");
+	S->cycleGraph = NULL;
 	for (int d = 1; d <= nd; d++)
 		if (rho->trueSize[d] % (1 << S->nLevels))
 			msg(ERROR, "All elements in grid:trueSize must be a multiple of 2^mgLevels=%d", 1 << S->nLevels);
@@ -128,6 +132,7 @@ MultigridSolver *mgAllocSolver(const dictionary *ini, Grid *rho, Grid *phi) {
 
 void mgFreeSolver(MultigridSolver *S) {
 	if (!S) return;
+	pinc_hip_graph_destroy(S->cycleGraph);
 	for (int q = 0; q < S->nLevels; q++) {
 		if (q > 0) {
 			pinc_hip_free(S->rho[q]);
@@ -277,7 +282,22 @@ void mgSolve(MultigridSolver *S, Grid *rho, Grid *phi, const MpiInfo *mpiInfo) {
 		double barRes = 2.;
 		long c = 0;
 		while (barRes > 1.E-10) {
-			vrec(S, 0);
+			if (S->useGraph) {
+				/* the V-cycle is a fixed launch sequence on fixed buffers:
+				 * captured once, then replayed (no per-kernel dispatch) */
+				if (!S->cycleGraph) {
+					g_pinc.capturing = 1;
+					pinc_check(pinc_hip_capture_begin(g_pinc.stream), "capture V-cycle");
+					vrec(S, 0);
+					pinc_check(pinc_hip_capture_end(g_pinc.stream, &S->cycleGraph), "capture V-cycle");
+					g_pinc.capturing = 0;
+				}
+				int gslot = pinc_probe_begin(PINC_PROBE_CYCLE);
+				pinc_check(pinc_hip_graph_launch(S->cycleGraph, g_pinc.stream), "V-cycle graph");
+				pinc_probe_end(PINC_PROBE_CYCLE, gslot, 0.0);
+			} else {
+				vrec(S, 0);
+			}
 			S->cycles++;
 			int nb = 0;
 			int slot = pinc_probe_begin(PINC_PROBE_RESIDUAL);

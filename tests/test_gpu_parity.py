@@ -170,6 +170,28 @@ def test_native_mg_same_solution(sim_cls, name, kw):
     assert cyc_native <= 12, (cyc_native, cyc_ref)
 
 
+def test_native_mg_graph_replay(sim_cls):
+    """multigrid:graph=1 (the V-cycle captured once into a HIP graph and
+    replayed) gives the solution and cycle count of direct launches over
+    several steps (the graph is reused across solves).  The kernels are the
+    same; the deposit's atomics make rho differ by rounding between any two
+    runs, so phi is compared to 1e-9 of its scale and the cycle count to 1."""
+    cfg = configs.config("warm", true_size=(32, 32, 64), ppc=8, nalloc_pc=16, levels=4)
+    cfg["multigrid"]["native"] = "1"
+    out = {}
+    for graph in ("0", "1"):
+        cfg["multigrid"]["graph"] = graph
+        with sim_cls(configs.write_ini(cfg), maxwell=True, perturb=False, seed=3) as s:
+            s.init()
+            for _ in range(3):
+                s.step()
+            out[graph] = (s.grid(1).copy(), s.cycles, s.energy()[:2])
+    scale = np.abs(out["0"][0]).max()
+    np.testing.assert_allclose(out["1"][0], out["0"][0], rtol=0, atol=1e-9 * scale)
+    assert abs(out["0"][1] - out["1"][1]) <= 1
+    np.testing.assert_allclose(out["1"][2], out["0"][2], rtol=1e-9)
+
+
 @pytest.mark.parametrize("layout", ["sorted", "scattered", "mixed"])
 def test_deposit_layouts(sim_cls, layout):
     """puDistr3D1 on particle orders that exercise both deposit paths: the
