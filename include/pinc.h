@@ -164,6 +164,14 @@ void puAcc3D1(Population *pop, Grid *E);
 void puAcc3D1KE(Population *pop, Grid *E);
 void puAccND1(Population *pop, Grid *E);
 void puAccND1KE(Population *pop, Grid *E);
+/* Boris with a uniform external B (puBoris3D1/KE, pusher.c:394-483), the
+ * reference's indexing defect corrected; puGet3DRotationParameters
+ * (pusher.c:485-505) reads fields:BExt, population:charge/mass */
+funPtr puBoris3D1_set(dictionary *ini);
+funPtr puBoris3D1KE_set(dictionary *ini);
+void puBoris3D1(Population *pop, Grid *E, const double *T, const double *S);
+void puBoris3D1KE(Population *pop, Grid *E, const double *T, const double *S);
+void puGet3DRotationParameters(dictionary *ini, double *T, double *S);
 funPtr puDistr3D1_set(dictionary *ini);
 funPtr puDistrND1_set(dictionary *ini);
 void puDistr3D1(const Population *pop, Grid *rho);

@@ -141,6 +141,13 @@ int pinc_hip_count_keys(pinc_pop_t pop, int s, long first, pinc_geom_t g, int ti
  * 2*ceil(nKeys/4096)+1 ints */
 int pinc_hip_scan_keys(const int *counts, long nKeys, int *offsets, int *work, void *stream);
 /* dst[i] = src[perm[i]] (velocities of a sorted push in the old order) */
+/* puBoris3D1KE (pusher.c:433-483; rotation parameters pusher.c:485-505) with
+ * the reference's indexing defect corrected: per particle a half kick from
+ * Es (E as rescaled for species s), v' = v + v x T, v += v' x S (addCross
+ * order), KE partial of v^2, half kick.  T, S: host pointers to species s's
+ * three components each.  3-D only. */
+int pinc_hip_boris(pinc_pop_t pop, int s, pinc_geom_t g, const double *Es, const double *T, const double *S,
+                   double *kePartial, int *nBlocks, void *stream);
 int pinc_hip_gather_perm(const double *src, const int *perm, long n, double *dst, void *stream);
 /* perm[i] = i (a species left in order by a push that sorted another one) */
 int pinc_hip_iota(int *perm, long n, void *stream);

@@ -98,7 +98,7 @@ typedef struct {
 	OMg mgRho, mgPhi, mgRes;
 } ORank;
 
-enum { ORC_ACC_3D1KE, ORC_ACC_ND1KE, ORC_ACC_3D1, ORC_ACC_ND1 };
+enum { ORC_ACC_3D1KE, ORC_ACC_ND1KE, ORC_ACC_3D1, ORC_ACC_ND1, ORC_ACC_BORIS3D1KE, ORC_ACC_BORIS3D1 };
 enum { ORC_DISTR_3D1, ORC_DISTR_ND1 };
 enum { ORC_MIG_3D, ORC_MIG_ND };
 enum { ORC_SMOOTH_GS3D, ORC_SMOOTH_GSND };
@@ -113,6 +113,7 @@ typedef struct {
 	OIni *ini;
 	/* selected operators */
 	int acc, distr, migrate, poisson;
+	double borisT[24], borisS[24];  /* puGet3DRotationParameters, per species */
 	int preSmooth, postSmooth, coarseSolv, restrictor, prolongator;
 	int nLevels, nPre, nPost, nCoarse, mgCycles;
 	double maxVel;
@@ -162,6 +163,9 @@ void op_sum_kin(OPop *p);
 /* ------------------------------------------------------------- pusher -- */
 void opu_move(OPop *p);
 void opu_acc3d1(OPop *p, OGrid *E, int ke);
+void opu_boris3d1(OPop *p, OGrid *E, const double *T, const double *S, int ke);
+void opu_rotation_params(int nSpecies, const double *BExt, const double *charge, const double *mass, double *T,
+                         double *S);
 void opu_accnd1(OPop *p, OGrid *E, int ke);
 void opu_distr3d1(const OPop *p, OGrid *rho);
 void opu_distrnd1(const OPop *p, OGrid *rho);

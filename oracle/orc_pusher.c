@@ -67,6 +67,56 @@ void opu_acc3d1(OPop *p, OGrid *E, int ke){
 	}
 }
 
+/* puBoris3D1 / puBoris3D1KE (pusher.c:394-483) as the algorithm they state,
+ * with the indexing corrected (fact 7: the reference rotates vel[0..2], the
+ * first particle, instead of vel[p..p+2], and memcpy's the wrong source):
+ * v- = v + dv/2; v' = v- + v- x T; v+ = v- + v' x S (addCross,
+ * pusher.c:1234-1238, same expression order); KE sums v+^2 (pow(v,2) is the
+ * correctly rounded square); v = v+ + dv/2.  T and S per species from
+ * puGet3DRotationParameters (pusher.c:485-505). */
+static void add_cross(const double *a, const double *b, double *res){
+	res[0] +=  (a[1]*b[2]-a[2]*b[1]);
+	res[1] += -(a[0]*b[2]-a[2]*b[0]);
+	res[2] +=  (a[0]*b[1]-a[1]*b[0]);
+}
+
+void opu_boris3d1(OPop *p, OGrid *E, const double *T, const double *S, int ke){
+	const long *sp = E->sizeProd;
+	for(int s = 0; s < p->nSpecies; s++){
+		og_mul(E, p->charge[s]/p->mass[s]);
+		if(ke) p->kinEnergy[s] = 0;
+		for(long i = p->iStart[s]; i < p->iStop[s]; i++){
+			double dv[3], vPrime[3];
+			double *v = &p->vel[3*i];
+			interp3d1(dv, &p->pos[3*i], E->val, sp);
+			for(int d = 0; d < 3; d++) v[d] += 0.5*dv[d];
+			for(int d = 0; d < 3; d++) vPrime[d] = v[d];
+			add_cross(v, &T[3*s], vPrime);
+			add_cross(vPrime, &S[3*s], v);
+			double vs = 0;
+			for(int d = 0; d < 3; d++) vs += v[d]*v[d];
+			if(ke) p->kinEnergy[s] += vs;
+			for(int d = 0; d < 3; d++) v[d] += 0.5*dv[d];
+		}
+		if(ke) p->kinEnergy[s] *= 0.5*p->mass[s];
+		og_mul(E, p->mass[s]/p->charge[s]);
+	}
+}
+
+void opu_rotation_params(int nSpecies, const double *BExt, const double *charge, const double *mass, double *T,
+                         double *S){
+	for(int s = 0; s < nSpecies; s++){
+		double factor = 0.5*charge[s]/mass[s];
+		double denom = 1;
+		for(int q = 0; q < 3; q++){
+			T[3*s+q] = factor*BExt[q];
+			denom += T[3*s+q]*T[3*s+q];
+		}
+		double mul = 2.0/denom;
+		for(int q = 0; q < 3; q++) S[3*s+q] = mul*T[3*s+q];
+	}
+}
+
 /* recursion from the highest dimension down to x; factor carries the product
  * of the weights of the outer dimensions (pusher.c:1147-1162). */
 static void interpnd_inner(double *res, const double *val, long p, const long *mul, long lastMul,

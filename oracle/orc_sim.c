@@ -129,9 +129,9 @@ static void sanity(const OIni *ini, int dim, int order){
 
 static void select_methods(OWorld *w){
 	OIni *ini = w->ini;
-	const char *acc[] = {"puAcc3D1KE", "puAccND1KE", "puAcc3D1", "puAccND1"};
-	w->acc = pick(ini, "methods:acc", acc, 4);
-	sanity(ini, (w->acc == ORC_ACC_3D1KE || w->acc == ORC_ACC_3D1) ? 3 : 0, 1);
+	const char *acc[] = {"puAcc3D1KE", "puAccND1KE", "puAcc3D1", "puAccND1", "puBoris3D1KE", "puBoris3D1"};
+	w->acc = pick(ini, "methods:acc", acc, 6);
+	sanity(ini, (w->acc == ORC_ACC_ND1KE || w->acc == ORC_ACC_ND1) ? 0 : 3, 1);
 	const char *distr[] = {"puDistr3D1", "puDistrND1"};
 	w->distr = pick(ini, "methods:distr", distr, 2);
 	sanity(ini, w->distr == ORC_DISTR_3D1 ? 3 : 0, 1);
@@ -187,6 +187,15 @@ OWorld *ow_create(OIni *ini, int literal){
 	units_normalize(w);
 	int nd = oini_int(ini, "grid:nDims");
 	int ns = oini_int(ini, "population:nSpecies");
+	if(w->acc == ORC_ACC_BORIS3D1KE || w->acc == ORC_ACC_BORIS3D1){
+		/* puGet3DRotationParameters on the normalised ini (pusher.c:485-505) */
+		if(ns > 8) orc_die("Boris: at most 8 species");
+		double *B = oini_doublearr(ini, "fields:BExt", nd);
+		double *c = oini_doublearr(ini, "population:charge", ns);
+		double *m = oini_doublearr(ini, "population:mass", ns);
+		opu_rotation_params(ns, B, c, m, w->borisT, w->borisS);
+		free(B); free(c); free(m);
+	}
 	w->nDims = nd; w->nSpecies = ns;
 	int *nsub = oini_intarr(ini, "grid:nSubdomains", nd);
 	int *ng = oini_intarr(ini, "grid:nGhostLayers", 2*nd);
@@ -294,6 +303,8 @@ static void do_acc(OWorld *w){
 		case ORC_ACC_3D1KE: opu_acc3d1(p, E, 1); break;
 		case ORC_ACC_3D1:   opu_acc3d1(p, E, 0); break;
 		case ORC_ACC_ND1KE: opu_accnd1(p, E, 1); break;
+		case ORC_ACC_BORIS3D1KE: opu_boris3d1(p, E, w->borisT, w->borisS, 1); break;
+		case ORC_ACC_BORIS3D1:   opu_boris3d1(p, E, w->borisT, w->borisS, 0); break;
 		default:            opu_accnd1(p, E, 0); break;
 		}
 	}
@@ -338,7 +349,23 @@ void ow_init_fields(OWorld *w){
 	 * E from the periodic phi; the checker follows. */
 	do_efield(w, w->poisson == ORC_POISSON_SPECTRAL);
 	for(int r = 0; r < w->P; r++) og_mul(&w->r[r].E, 0.5);
-	do_acc(w);
+	if(w->acc == ORC_ACC_BORIS3D1KE || w->acc == ORC_ACC_BORIS3D1){
+		/* half step of the Boris extension: E and T halved, S for the halved
+		 * T (pusher.h:66-70 documents halving E, S and T) */
+		double T[24], S[24];
+		memcpy(T, w->borisT, sizeof(T));
+		memcpy(S, w->borisS, sizeof(S));
+		for(int i = 0; i < 24; i += 3){
+			double denom = 1;
+			for(int q = 0; q < 3; q++){ w->borisT[i+q] = 0.5*T[i+q]; denom += w->borisT[i+q]*w->borisT[i+q]; }
+			for(int q = 0; q < 3; q++) w->borisS[i+q] = 2.0/denom*w->borisT[i+q];
+		}
+		do_acc(w);
+		memcpy(w->borisT, T, sizeof(T));
+		memcpy(w->borisS, S, sizeof(S));
+	} else {
+		do_acc(w);
+	}
 	for(int r = 0; r < w->P; r++) og_mul(&w->r[r].E, 2.0);
 }
 

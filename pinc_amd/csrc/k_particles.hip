@@ -630,14 +630,27 @@ __global__ void k_field_chain(const double *__restrict__ E, double *__restrict__
 	}
 }
 
-template <int ND, bool V3D, bool KE>
+// Boris rotation parameters of one species (puGet3DRotationParameters,
+// pusher.c:485-505)
+struct BorisRot {
+	double T[3], S[3];
+};
+
+// v x b added to res in addCross's expression order (pusher.c:1234-1238)
+__device__ __forceinline__ void add_cross(const double *a, const double *b, double *res) {
+	res[0] += (a[1] * b[2] - a[2] * b[1]);
+	res[1] += -(a[0] * b[2] - a[2] * b[0]);
+	res[2] += (a[0] * b[1] - a[1] * b[0]);
+}
+
+template <int ND, bool V3D, bool KE, bool BORIS = false>
 __global__ __launch_bounds__(kThreads) void k_accel(const double *__restrict__ x0,
                                                     const double *__restrict__ x1,
                                                     const double *__restrict__ x2,
                                                     double *__restrict__ v0, double *__restrict__ v1,
                                                     double *__restrict__ v2, long b0, long n,
                                                     pinc_geom_t g, const double *__restrict__ E,
-                                                    double *__restrict__ kePartial) {
+                                                    double *__restrict__ kePartial, BorisRot rot = {}) {
 	constexpr int NC = 1 << ND;
 	__shared__ double red[kThreads / 64];
 	Geo G = make_geo(g);
@@ -732,11 +745,27 @@ __global__ __launch_bounds__(kThreads) void k_accel(const double *__restrict__ x
 				}
 			}
 			double vsq = 0;
+			if constexpr (BORIS) {
+				// puBoris3D1KE (pusher.c:455-476) with the indexing corrected:
+				// half kick, rotation about B, KE of v+, half kick
+				double vm[3], vp[3];
 #pragma unroll
-			for (int d = 0; d < ND; d++) {
-				double vv = v[d][h];
-				vsq += vv * (vv + dv[d]);
-				v[d][h] = vv + dv[d];
+				for (int d = 0; d < 3; d++) vm[d] = v[d][h] + 0.5 * dv[d];
+#pragma unroll
+				for (int d = 0; d < 3; d++) vp[d] = vm[d];
+				add_cross(vm, rot.T, vp);
+				add_cross(vp, rot.S, vm);
+#pragma unroll
+				for (int d = 0; d < 3; d++) vsq += vm[d] * vm[d];
+#pragma unroll
+				for (int d = 0; d < 3; d++) v[d][h] = vm[d] + 0.5 * dv[d];
+			} else {
+#pragma unroll
+				for (int d = 0; d < ND; d++) {
+					double vv = v[d][h];
+					vsq += vv * (vv + dv[d]);
+					v[d][h] = vv + dv[d];
+				}
 			}
 			ke += vsq;
 		}
@@ -2072,6 +2101,25 @@ extern "C" int pinc_hip_accelerate(pinc_pop_t pop, int s, pinc_geom_t g, const d
 		hipLaunchKernelGGL((k_accel<1, false, true>), dim3(nb), dim3(kThreads), 0, st, x0, x1, x2, v0, v1, v2, b0,
 		                   n, g, Es, kePartial);
 	return check_launch("accelerate");
+}
+
+extern "C" int pinc_hip_boris(pinc_pop_t pop, int s, pinc_geom_t g, const double *Es, const double *T,
+                              const double *S, double *kePartial, int *nBlocks, void *stream) {
+	long n = pop.iStop[s] - pop.iStart[s];
+	*nBlocks = 0;
+	if (g.nd != 3 || pop.nd != 3) return set_error(hipErrorInvalidValue, "boris: 3-D only (puBoris3D1)");
+	if (n <= 0) return 0;
+	long b0 = pop.iStart[s];
+	long nb = ceil_div(n + (b0 & 1L), (long)kAccChunk);
+	*nBlocks = (int)nb;
+	BorisRot rot;
+	for (int q = 0; q < 3; q++) {
+		rot.T[q] = T[q];
+		rot.S[q] = S[q];
+	}
+	hipLaunchKernelGGL((k_accel<3, true, true, true>), dim3(nb), dim3(kThreads), 0, (hipStream_t)stream, pop.x[0],
+	                   pop.x[1], pop.x[2], pop.v[0], pop.v[1], pop.v[2], b0, n, g, Es, kePartial, rot);
+	return check_launch("boris");
 }
 
 extern "C" int pinc_hip_init_species(pinc_pop_t pop, int s, pinc_geom_t g, long nGlobal,

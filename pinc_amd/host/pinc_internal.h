@@ -124,6 +124,10 @@ struct PincDevGrid {
 	double *scaled;     /* E as rescaled for the species being pushed (lazy) */
 };
 
+/* Boris selected through methods:acc: its initial half step (pinc_regular.c) */
+void pinc_boris_half_step(int on);
+int pinc_boris_selected(funPtr acc);
+
 struct MultigridSolver {
 	int nLevels, nPre, nPost, nCoarse, mgCycles;
 	int pre3d, post3d, coarse3d, restr3d;

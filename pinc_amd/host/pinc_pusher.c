@@ -44,6 +44,77 @@ funPtr puAcc3D1_set(dictionary *ini) { puSanity(ini, "puAcc3D1", 3, 1); return (
 funPtr puAcc3D1KE_set(dictionary *ini) { puSanity(ini, "puAcc3D1KE", 3, 1); return (funPtr)puAcc3D1KE; }
 funPtr puAccND1_set(dictionary *ini) { puSanity(ini, "puAccND1", 0, 1); return (funPtr)puAccND1; }
 funPtr puAccND1KE_set(dictionary *ini) { puSanity(ini, "puAccND1KE", 0, 1); return (funPtr)puAccND1KE; }
+/* Boris (puBoris3D1/KE, pusher.c:394-505), an extension: the reference's
+ * version rotates the wrong particle (fact 7) and main.c does not offer it.
+ * Selected as methods:acc=puBoris3D1KE; the rotation parameters come from
+ * the normalised ini at the first push (select runs before uNormalize,
+ * main.c:55-85), and the initial half step halves E and T (S recomputed for
+ * the halved T, so the half rotation stays norm-preserving). */
+static struct {
+	const dictionary *ini;
+	int ready, half;
+	double T[3 * PINC_MAX_SPECIES], S[3 * PINC_MAX_SPECIES];
+	double Th[3 * PINC_MAX_SPECIES], Sh[3 * PINC_MAX_SPECIES];
+} g_boris;
+
+void puGet3DRotationParameters(dictionary *ini, double *T, double *S) {
+	int nDims = iniGetInt(ini, "grid:nDims");
+	int nSpecies = iniGetInt(ini, "population:nSpecies");
+	if (nDims != 3) msg(ERROR, "Boris rotation parameters need grid:nDims=3");
+	double *BExt = iniGetDoubleArr(ini, "fields:BExt", nDims);
+	double *charge = iniGetDoubleArr(ini, "population:charge", nSpecies);
+	double *mass = iniGetDoubleArr(ini, "population:mass", nSpecies);
+	for (int s = 0; s < nSpecies; s++) {
+		double factor = 0.5 * charge[s] / mass[s];
+		double denom = 1;
+		for (int p = 0; p < 3; p++) {
+			T[3 * s + p] = factor * BExt[p];
+			denom += T[3 * s + p] * T[3 * s + p];
+		}
+		double mul = 2.0 / denom;
+		for (int p = 0; p < 3; p++) S[3 * s + p] = mul * T[3 * s + p];
+	}
+	free(BExt);
+	free(charge);
+	free(mass);
+}
+
+static void boris(Population *pop, Grid *E, const double *T, const double *S, int ke);
+static void boris_params(void) {
+	if (g_boris.ready) return;
+	if (!g_boris.ini) msg(ERROR, "Boris pusher used without puBoris3D1*_set");
+	puGet3DRotationParameters((dictionary *)g_boris.ini, g_boris.T, g_boris.S);
+	for (int i = 0; i < 3 * PINC_MAX_SPECIES; i += 3) {
+		double denom = 1;
+		for (int p = 0; p < 3; p++) {
+			g_boris.Th[i + p] = 0.5 * g_boris.T[i + p];
+			denom += g_boris.Th[i + p] * g_boris.Th[i + p];
+		}
+		for (int p = 0; p < 3; p++) g_boris.Sh[i + p] = 2.0 / denom * g_boris.Th[i + p];
+	}
+	g_boris.ready = 1;
+}
+static void boris_selected(Population *pop, Grid *E, int ke) {
+	boris_params();
+	if (g_boris.half) boris(pop, E, g_boris.Th, g_boris.Sh, ke);
+	else boris(pop, E, g_boris.T, g_boris.S, ke);
+}
+static void boris_sel(Population *pop, Grid *E) { boris_selected(pop, E, 0); }
+static void boris_sel_ke(Population *pop, Grid *E) { boris_selected(pop, E, 1); }
+void pinc_boris_half_step(int on) { g_boris.half = on; }
+int pinc_boris_selected(funPtr acc) { return acc == (funPtr)boris_sel || acc == (funPtr)boris_sel_ke; }
+funPtr puBoris3D1_set(dictionary *ini) {
+	puSanity(ini, "puBoris3D1", 3, 1);
+	g_boris.ini = ini;
+	g_boris.ready = 0;
+	return (funPtr)boris_sel;
+}
+funPtr puBoris3D1KE_set(dictionary *ini) {
+	puSanity(ini, "puBoris3D1KE", 3, 1);
+	g_boris.ini = ini;
+	g_boris.ready = 0;
+	return (funPtr)boris_sel_ke;
+}
 funPtr puDistr3D1_set(dictionary *ini) { puSanity(ini, "puDistr3D1", 3, 1); return (funPtr)puDistr3D1; }
 funPtr puDistrND1_set(dictionary *ini) { puSanity(ini, "puDistrND1", 0, 1); return (funPtr)puDistrND1; }
 funPtr puExtractEmigrants3D_set(dictionary *ini) {
@@ -664,6 +735,40 @@ static void acc(Population *pop, Grid *E, int ke) {
 	}
 	pinc_phase_end(6);
 }
+
+/* per species: E as rescaled for s, half kick, rotation, half kick, KE */
+static void boris(Population *pop, Grid *E, const double *T, const double *S, int ke) {
+	pinc_phase_begin(6);
+	PincDevPop *dv = pop->dev;
+	if (dv->pending) msg(ERROR, "Boris push after a fused puAcc without its puMove");
+	pinc_pop_t p = pinc_devpop(pop);
+	int ns = pop->nSpecies;
+	for (int s = 0; s < ns; s++) {
+		int nb = 0;
+		PincDevGrid *eg = E->dev;
+		if (!eg->scaled)
+			pinc_check(pinc_hip_malloc((void **)&eg->scaled, eg->n * sizeof(double)), "E scaled");
+		pinc_check(pinc_hip_field_chain(eg->d, eg->scaled, eg->n, dv->qm, dv->mq, 1.0, s, g_pinc.stream),
+		           "E chain");
+		int slot = pinc_probe_begin(PINC_PROBE_ACCEL);
+		pinc_check(pinc_hip_boris(p, s, eg->geom, eg->scaled, T + 3 * s, S + 3 * s, dv->kePartial, &nb,
+		                          g_pinc.stream),
+		           "boris");
+		pinc_probe_end(PINC_PROBE_ACCEL, slot,
+		               24.0 * pop->nDims * (pop->iStop[s] - pop->iStart[s]) + 8.0 * E->dev->n);
+		if (nb > 0) pinc_check(pinc_hip_sum(dv->kePartial, nb, g_pinc.dScratch, PINC_SLOT(16 + s), g_pinc.stream), "ke");
+		else pinc_check(pinc_hip_memset(PINC_SLOT(16 + s), 0, sizeof(double), g_pinc.stream), "ke");
+	}
+	if (ke) {
+		double sums[PINC_MAX_SPECIES];
+		pinc_check(pinc_hip_d2h(sums, PINC_SLOT(16), ns * sizeof(double), g_pinc.stream), "ke readback");
+		for (int s = 0; s < ns; s++) pop->kinEnergy[s] = sums[s] * (0.5 * pop->mass[s]);
+	}
+	pinc_phase_end(6);
+}
+
+void puBoris3D1(Population *pop, Grid *E, const double *T, const double *S) { boris(pop, E, T, S, 0); }
+void puBoris3D1KE(Population *pop, Grid *E, const double *T, const double *S) { boris(pop, E, T, S, 1); }
 
 void puAcc3D1(Population *pop, Grid *E) { acc(pop, E, 0); }
 void puAcc3D1KE(Population *pop, Grid *E) { acc(pop, E, 1); }

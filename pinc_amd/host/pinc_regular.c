@@ -68,7 +68,7 @@ static PincSim *sim_build(dictionary *ini, const PincSimOpts *opts) {
 	}
 	/* method selection (main.c:55-79) */
 	S->acc = (void (*)(Population *, Grid *))select(ini, "methods:acc", puAcc3D1_set, puAcc3D1KE_set, puAccND1_set,
-	                                                 puAccND1KE_set);
+	                                                 puAccND1KE_set, puBoris3D1_set, puBoris3D1KE_set);
 	S->distr = (void (*)(const Population *, Grid *))select(ini, "methods:distr", puDistr3D1_set, puDistrND1_set);
 	S->extractEmigrants = (void (*)(Population *, MpiInfo *))select(ini, "methods:migrate", puExtractEmigrants3D_set,
 	                                                                puExtractEmigrantsND_set);
@@ -129,7 +129,10 @@ static void sim_fields(PincSim *S) {
 	gMul(S->E, -1.);
 	pinc_phase_end(5);
 	gMul(S->E, 0.5);
+	int bor = pinc_boris_selected((funPtr)S->acc);
+	if (bor) pinc_boris_half_step(1);
 	S->acc(S->pop, S->E);
+	if (bor) pinc_boris_half_step(0);
 	gMul(S->E, 2.0);
 }
 
