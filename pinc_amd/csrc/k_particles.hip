@@ -1230,8 +1230,14 @@ struct PushArgs {
 
 // same-cell groups of at least kPushGroupMin lanes (at most kPushGroups of
 // them per wave and item) are summed across the wave before the LDS add
-constexpr int kPushGroupMin = 2;
-constexpr int kPushGroups = 4;
+#ifndef PINC_PUSH_GROUP_MIN
+#define PINC_PUSH_GROUP_MIN 2
+#endif
+#ifndef PINC_PUSH_GROUPS
+#define PINC_PUSH_GROUPS 4
+#endif
+constexpr int kPushGroupMin = PINC_PUSH_GROUP_MIN;
+constexpr int kPushGroups = PINC_PUSH_GROUPS;
 // 8 waves x 4 particles per thread per PINC_CHUNK block: fewer live VGPRs
 // (px) than 4 waves x 8, so more waves per SIMD hide the gather latency
 constexpr int kPushThreads = 256;
@@ -1465,26 +1471,51 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(4)
 	const Geo32 G = make_geo32(a.g);
 	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 	const long base = (long)blockIdx.x * kPushChunk;
+	// item k of a thread: particles in lane-contiguous pairs (16-B loads and
+	// stores, 1 KiB per wave instruction), pair k/2 of the thread
+	auto item = [&](int k) -> long { return base + (long)((k >> 1) * (2 * kPushThreads) + 2 * threadIdx.x + (k & 1)); };
+	// pairs are 16-B aligned when every species array is (the species
+	// offset iStart is even); otherwise one 8-B access per particle
+	bool al = true;
+#pragma unroll
+	for (int d = 0; d < ND; d++)
+		al = al && !((reinterpret_cast<unsigned long>(a.xi[d]) | reinterpret_cast<unsigned long>(a.vi[d]) |
+		              reinterpret_cast<unsigned long>(a.xo[d]) | reinterpret_cast<unsigned long>(a.vo[d])) & 15);
 
 	PUSH_TS(0);
 	// ---- phase A: load every item, cell box of the input positions
 	double p[kPushItems][ND], vv[kPushItems][ND];
 	unsigned valid = 0;
 	int lo[3] = {INT32_MAX, INT32_MAX, INT32_MAX}, hi[3] = {INT32_MIN, INT32_MIN, INT32_MIN}, sm[3] = {0, 0, 0};
+	static_assert(kPushItems % 2 == 0, "items come in pairs");
 #pragma unroll
-	for (int k = 0; k < kPushItems; k++) {
-		const long i = base + k * kPushThreads + threadIdx.x;
-		const bool ok = i < a.n;
-		valid |= (unsigned)ok << k;
+	for (int k = 0; k < kPushItems; k += 2) {
+		const long i = item(k);
+		const bool ok0 = i < a.n, ok1 = i + 1 < a.n;
+		valid |= ((unsigned)ok0 | (unsigned)ok1 << 1) << k;
 #pragma unroll
 		for (int d = 0; d < ND; d++) {
-			p[k][d] = ok ? a.xi[d][i] : 1.0;
-			vv[k][d] = ok ? a.vi[d][i] : 0.0;
-			if (ok) {
-				int c = (int)p[k][d];
-				lo[d] = min(lo[d], c);
-				hi[d] = max(hi[d], c);
-				sm[d] += c;
+			if (ok1 && al) {
+				const double2 x = *reinterpret_cast<const double2 *>(a.xi[d] + i);
+				const double2 v = *reinterpret_cast<const double2 *>(a.vi[d] + i);
+				p[k][d] = x.x;
+				p[k + 1][d] = x.y;
+				vv[k][d] = v.x;
+				vv[k + 1][d] = v.y;
+			} else {
+				p[k][d] = ok0 ? a.xi[d][i] : 1.0;
+				vv[k][d] = ok0 ? a.vi[d][i] : 0.0;
+				p[k + 1][d] = ok1 ? a.xi[d][i + 1] : 1.0;
+				vv[k + 1][d] = ok1 ? a.vi[d][i + 1] : 0.0;
+			}
+#pragma unroll
+			for (int h = 0; h < 2; h++) {
+				if ((valid >> (k + h)) & 1u) {
+					int c = (int)p[k + h][d];
+					lo[d] = min(lo[d], c);
+					hi[d] = max(hi[d], c);
+					sm[d] += c;
+				}
 			}
 		}
 	}
@@ -1608,7 +1639,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(4)
 #pragma unroll
 	for (int k = 0; k < kPushItems; k++) {
 		if (!((valid >> k) & 1u)) continue;
-		const long i = base + k * kPushThreads + threadIdx.x;
+		const long i = item(k);
 		if (KICK) {
 			double dec[3], comp[3];
 			int j[3] = {0, 0, 0};
@@ -1713,18 +1744,32 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(4)
 			                         : kPushChunk + k * kPushThreads + (int)threadIdx.x;
 			stageF[t] = (unsigned char)ne;
 		}
-		if (!SORT) {
-#pragma unroll
-			for (int d = 0; d < ND; d++) {
-				a.xo[d][i] = p[k][d];
-				if (KICK || a.vo[d] != a.vi[d]) a.vo[d][i] = vv[k][d];
-			}
-			a.flags[i] = (unsigned char)ne;
-		}
+		if (!SORT) a.flags[i] = (unsigned char)ne;
 		if (ne != a.center) {
 			if (!SORT) cnt++;
 		} else {
 			dep |= (1u | (unsigned)chg << 16) << k;  // bits 16+: changed cell
+		}
+	}
+	if (!SORT) {
+		// positions (and velocities if kicked or moved) in pairs
+		const bool wv = KICK || a.vo[0] != a.vi[0];
+#pragma unroll
+		for (int k = 0; k < kPushItems; k += 2) {
+			const long i = item(k);
+			const bool ok0 = (valid >> k) & 1u, ok1 = (valid >> (k + 1)) & 1u;
+#pragma unroll
+			for (int d = 0; d < ND; d++) {
+				if (ok1 && al) {
+					*reinterpret_cast<double2 *>(a.xo[d] + i) = make_double2(p[k][d], p[k + 1][d]);
+					if (wv) *reinterpret_cast<double2 *>(a.vo[d] + i) = make_double2(vv[k][d], vv[k + 1][d]);
+				} else {
+					if (ok0) a.xo[d][i] = p[k][d];
+					if (ok0 && wv) a.vo[d][i] = vv[k][d];
+					if (ok1) a.xo[d][i + 1] = p[k + 1][d];
+					if (ok1 && wv) a.vo[d][i + 1] = vv[k + 1][d];
+				}
+			}
 		}
 	}
 	PUSH_TS(4);
@@ -1738,7 +1783,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(4)
 			for (int k = 0; k < kPushItems; k++) {
 				slot[k] = -1;
 				if (!((valid >> k) & 1u)) continue;
-				const long i = base + k * kPushThreads + threadIdx.x;
+				const long i = item(k);
 				const int r = rlL[k * kPushThreads + threadIdx.x];
 				if (r >= 0) {
 					const int lc = r & 255, rank = r >> 8;
@@ -1831,28 +1876,25 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(4)
 		}
 	};
 	const int keyMul[3] = {1, G.T[0] + 2, (G.T[0] + 2) * (G.T[1] + 2)};  // unique cell key
+	// CIC weights and cell key of item k (a particle that stays)
+	auto weights = [&](int k, int *j, double *w) -> int {
+		double dec[3], comp[3];
+		int kk = 0;
 #pragma unroll
-	for (int k = 0; k < kPushItems; k++) {
-		const bool mine = (dep >> k) & 1u;
-		int j[3] = {0, 0, 0};
-		double w[8];
-#pragma unroll
-		for (int c = 0; c < 8; c++) w[c] = 0.0;
-		int key = -1;
-		if (mine) {
-			double dec[3], comp[3];
-			int kk = 0;
-#pragma unroll
-			for (int d = 0; d < ND; d++) {
-				j[d] = (int)p[k][d];
-				dec[d] = p[k][d] - j[d];
-				comp[d] = 1 - dec[d];
-				kk += d ? mul24(j[d], keyMul[d]) : j[d];
-			}
-			key = kk;
-			cic_weights<ND, V3D>(dec, comp, w);
-			literal_ghost_weights<ND>(a.g, j, w);
+		for (int d = 0; d < ND; d++) {
+			j[d] = (int)p[k][d];
+			dec[d] = p[k][d] - j[d];
+			comp[d] = 1 - dec[d];
+			kk += d ? mul24(j[d], keyMul[d]) : j[d];
 		}
+		cic_weights<ND, V3D>(dec, comp, w);
+		literal_ghost_weights<ND>(a.g, j, w);
+		return kk;
+	};
+	// one wave pass: lanes sharing a cell (up to kPushGroups groups of at
+	// least kPushGroupMin lanes) are summed across the wave and added once,
+	// the others add their weights one by one
+	auto deposit_pass = [&](bool mine, const int *j, const double *w, int key) {
 		unsigned long long pend = __ballot(mine);
 		unsigned long long indiv = 0;
 #pragma unroll 1
@@ -1880,6 +1922,37 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(4)
 		if ((indiv >> lane) & 1ull) {
 #pragma unroll
 			for (int c = 0; c < NC; c++) add_corner(j, c, w[c]);
+		}
+	};
+	// the two particles of a lane's pair are neighbours in memory and mostly
+	// share a cell: their weights are summed in the lane first, so one wave
+	// pass covers the pair's 128 particles; the second particle of a pair
+	// that straddles a cell adds its weights one by one
+#pragma unroll
+	for (int k = 0; k < kPushItems; k += 2) {
+		const bool m0 = (dep >> k) & 1u, m1 = (dep >> (k + 1)) & 1u;
+		int j[3] = {0, 0, 0}, j1[3] = {0, 0, 0};
+		double w[8], w1[8];
+#pragma unroll
+		for (int c = 0; c < 8; c++) w[c] = w1[c] = 0.0;
+		int key = -1, key1 = -2;
+		if (m0) key = weights(k, j, w);
+		if (m1) key1 = weights(k + 1, j1, w1);
+		const bool merge = m0 && m1 && key == key1;
+		if (merge) {
+#pragma unroll
+			for (int c = 0; c < 8; c++) w[c] += w1[c];
+		} else if (!m0 && m1) {
+#pragma unroll
+			for (int d = 0; d < 3; d++) j[d] = j1[d];
+#pragma unroll
+			for (int c = 0; c < 8; c++) w[c] = w1[c];
+			key = key1;
+		}
+		deposit_pass(m0 || m1, j, w, key);
+		if (m0 && m1 && !merge) {
+#pragma unroll
+			for (int c = 0; c < NC; c++) add_corner(j1, c, w1[c]);
 		}
 	}
 

@@ -69,24 +69,39 @@ extern "C" int pinc_hip_capture_begin(void *stream) {
 	return 0;
 }
 
+// the executable keeps its graph alive until both are destroyed together
+struct PincGraph {
+	hipGraph_t g;
+	hipGraphExec_t e;
+};
+
 extern "C" int pinc_hip_capture_end(void *stream, void **exec) {
 	hipGraph_t g = nullptr;
 	HIPCALL(hipStreamEndCapture((hipStream_t)stream, &g), "hipStreamEndCapture");
 	hipGraphExec_t e = nullptr;
 	hipError_t r = hipGraphInstantiate(&e, g, nullptr, nullptr, 0);
-	(void)hipGraphDestroy(g);
-	HIPCALL(r, "hipGraphInstantiate");
-	*exec = (void *)e;
+	if (r != hipSuccess) {
+		(void)hipGraphDestroy(g);
+		HIPCALL(r, "hipGraphInstantiate");
+	}
+	PincGraph *pg = new PincGraph{g, e};
+	*exec = (void *)pg;
 	return 0;
 }
 
 extern "C" int pinc_hip_graph_launch(void *exec, void *stream) {
-	HIPCALL(hipGraphLaunch((hipGraphExec_t)exec, (hipStream_t)stream), "hipGraphLaunch");
+	HIPCALL(hipGraphLaunch(((PincGraph *)exec)->e, (hipStream_t)stream), "hipGraphLaunch");
 	return 0;
 }
 
 extern "C" int pinc_hip_graph_destroy(void *exec) {
-	if (exec) HIPCALL(hipGraphExecDestroy((hipGraphExec_t)exec), "hipGraphExecDestroy");
+	if (!exec) return 0;
+	PincGraph *pg = (PincGraph *)exec;
+	hipError_t r1 = hipGraphExecDestroy(pg->e);
+	hipError_t r2 = hipGraphDestroy(pg->g);
+	delete pg;
+	HIPCALL(r1, "hipGraphExecDestroy");
+	HIPCALL(r2, "hipGraphDestroy");
 	return 0;
 }
 

@@ -22,6 +22,11 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def built():
     import subprocess
+    # torch (device memory for the kernel-level tests) brings up the HIP
+    # runtime first, whichever test file runs first: with the native
+    # library initialised before it, the process aborted at exit in the
+    # runtimes' teardown (a double free after all tests had passed)
+    import torch  # noqa: F401
     from pinc_amd.build import build
     subprocess.run(["make", "-s", "-C", str(ROOT / "oracle"), "-j4"], check=True)
     return build()
