@@ -1448,6 +1448,8 @@ __device__ __forceinline__ int tile_key_cells(const TileGeo &tg, const int *cin)
 	return (int)(tile * cs + cell);
 }
 
+typedef double dvec2 __attribute__((ext_vector_type(2)));
+
 template <int ND, bool V3D, bool KICK, bool SORT>
 __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_push(PushArgs a) {
 	constexpr int NC = 1 << ND;
@@ -1496,8 +1498,9 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(4)
 #pragma unroll
 		for (int d = 0; d < ND; d++) {
 			if (ok1 && al) {
-				const double2 x = *reinterpret_cast<const double2 *>(a.xi[d] + i);
-				const double2 v = *reinterpret_cast<const double2 *>(a.vi[d] + i);
+				// streamed once per step (far beyond L2/MALL): non-temporal
+				const dvec2 x = __builtin_nontemporal_load(reinterpret_cast<const dvec2 *>(a.xi[d] + i));
+				const dvec2 v = __builtin_nontemporal_load(reinterpret_cast<const dvec2 *>(a.vi[d] + i));
 				p[k][d] = x.x;
 				p[k + 1][d] = x.y;
 				vv[k][d] = v.x;
@@ -1761,8 +1764,9 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(4)
 #pragma unroll
 			for (int d = 0; d < ND; d++) {
 				if (ok1 && al) {
-					*reinterpret_cast<double2 *>(a.xo[d] + i) = make_double2(p[k][d], p[k + 1][d]);
-					if (wv) *reinterpret_cast<double2 *>(a.vo[d] + i) = make_double2(vv[k][d], vv[k + 1][d]);
+					__builtin_nontemporal_store(dvec2{p[k][d], p[k + 1][d]}, reinterpret_cast<dvec2 *>(a.xo[d] + i));
+					if (wv)
+						__builtin_nontemporal_store(dvec2{vv[k][d], vv[k + 1][d]}, reinterpret_cast<dvec2 *>(a.vo[d] + i));
 				} else {
 					if (ok0) a.xo[d][i] = p[k][d];
 					if (ok0 && wv) a.vo[d][i] = vv[k][d];
@@ -1813,7 +1817,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(4)
 			}
 			auto flush = [&](double *out) {
 				__syncthreads();
-				for (int t = threadIdx.x; t < nv; t += kPushThreads) out[gdst[t]] = stage[t];
+				for (int t = threadIdx.x; t < nv; t += kPushThreads) __builtin_nontemporal_store(stage[t], out + gdst[t]);
 				__syncthreads();
 			};
 #pragma unroll
