@@ -119,6 +119,9 @@ def main() -> int:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-size", type=int, default=64)
     ap.add_argument("--cpu-steps", type=int, default=8)
+    ap.add_argument("--host-transport", action="store_true",
+                    help="rehearsal only: N ranks share GPU 0 and the collectives go through the gloo host "
+                         "transport (RCCL refuses two ranks on one device); never the measured configuration")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -129,18 +132,28 @@ def main() -> int:
         return 2
 
     import torch
+    if args.host_transport:
+        local = 0
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.host_transport:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    red_dev = "cpu" if args.host_transport else "cuda"
 
     from pinc_amd import configs, _lib
     from pinc_amd.sim import Sim
 
     comm_id = None
-    if world > 1:
+    transport = None
+    if world > 1 and args.host_transport:
+        from pinc_amd.transport import GlooTransport
+        transport = GlooTransport()
+    elif world > 1:
         obj = [_lib.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         comm_id = obj[0]
@@ -175,7 +188,7 @@ def main() -> int:
     t_init0 = time.perf_counter()
     log(f"creating {S}^3 x {args.ppc} ppc on {world} GPU(s)")
     sim = Sim(ini, rank=rank, nranks=world, device=local, comm_id=comm_id, maxwell=True, perturb=False,
-              device_init=True, seed=20260101, timing=True)
+              device_init=True, seed=20260101, timing=True, transport=transport)
     sim.init()
     sim.sync()
     t_init = time.perf_counter() - t_init0
@@ -212,10 +225,10 @@ def main() -> int:
     dt_max = dt
     n_total = n_local
     if dist is not None:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        t = torch.tensor([dt], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt_max = float(t.item())
-        c = torch.tensor([n_local], dtype=torch.int64, device="cuda")
+        c = torch.tensor([n_local], dtype=torch.int64, device=red_dev)
         dist.all_reduce(c, op=dist.ReduceOp.SUM)
         n_total = int(c.item())
 
