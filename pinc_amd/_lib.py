@@ -7,9 +7,11 @@ or fail to load, importing this module raises.  Build with
 from __future__ import annotations
 
 import ctypes as C
+import os
 from pathlib import Path
 
-LIBDIR = Path(__file__).resolve().parent / "lib"
+# PINC_LIBDIR: an alternative in-tree build (kernel-variant experiments)
+LIBDIR = Path(os.environ.get("PINC_LIBDIR") or Path(__file__).resolve().parent / "lib")
 PINC_COMM_ID_BYTES = 128
 NPHASES = 8
 PHASES = ["move", "extract", "migrate", "deposit", "solve", "efield", "accelerate", "energy"]

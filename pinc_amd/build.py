@@ -17,8 +17,10 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parent.parent
 CSRC = ROOT / "pinc_amd" / "csrc"
 HOST = ROOT / "pinc_amd" / "host"
-LIB = ROOT / "pinc_amd" / "lib"
-OBJ = ROOT / "build" / "obj"
+# PINC_LIBDIR / PINC_HIP_DEFINES: a variant build (kernel experiments) next to
+# the default one, e.g. PINC_LIBDIR=pinc_amd/lib_i2 PINC_HIP_DEFINES="-DPINC_PUSH_ITEMS=2"
+LIB = Path(os.environ.get("PINC_LIBDIR") or ROOT / "pinc_amd" / "lib").resolve()
+OBJ = ROOT / "build" / ("obj" if LIB == (ROOT / "pinc_amd" / "lib").resolve() else "obj_" + LIB.name)
 INC = ROOT / "include"
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -26,7 +28,7 @@ ARCH = os.environ.get("PINC_ARCH", "gfx950")
 # -ffp-contract=off: the kernels reproduce the reference's fp64 association
 # order; a fused multiply-add would change the rounding.
 HIP_FLAGS = ["-std=c++17", "-O3", f"--offload-arch={ARCH}", "-ffp-contract=off", "-fPIC",
-             "-munsafe-fp-atomics", f"-I{INC}", f"-I{CSRC}"]
+             "-munsafe-fp-atomics", f"-I{INC}", f"-I{CSRC}", *os.environ.get("PINC_HIP_DEFINES", "").split()]
 C_FLAGS = ["-std=c11", "-O2", "-fPIC", "-Wall", "-ffp-contract=off", f"-I{INC}", f"-I{HOST}"]
 
 HIP_SRC = ["runtime.hip", "k_particles.hip", "k_grid.hip", "k_mg.hip", "k_spectral.hip"]

@@ -1240,9 +1240,19 @@ constexpr int kPushGroupMin = PINC_PUSH_GROUP_MIN;
 constexpr int kPushGroups = PINC_PUSH_GROUPS;
 // 8 waves x 4 particles per thread per PINC_CHUNK block: fewer live VGPRs
 // (px) than 4 waves x 8, so more waves per SIMD hide the gather latency
+#ifndef PINC_PUSH_ITEMS
+#define PINC_PUSH_ITEMS 4
+#endif
+#ifndef PINC_PUSH_WPE
+#define PINC_PUSH_WPE 4
+#endif
+#ifndef PINC_PUSH_XCD
+#define PINC_PUSH_XCD 1
+#endif
 constexpr int kPushThreads = 256;
-constexpr int kPushItems = 4;
-constexpr int kPushChunk = kPushThreads * kPushItems;  // particles per block (PINC_CHUNK / 2)
+constexpr int kPushItems = PINC_PUSH_ITEMS;  // particles per thread, in lane-contiguous pairs
+constexpr int kPushChunk = kPushThreads * kPushItems;  // particles per block (PINC_CHUNK / 2 by default)
+static_assert(kPushChunk >= PINC_CHUNK / 8 && PINC_CHUNK % kPushChunk == 0, "kePartial holds PINC_CHUNK/8 per chunk");
 
 // double-precision lane exchange helpers on the two 32-bit halves
 __device__ __forceinline__ void permlane32_swap(double &a, double &b) {
@@ -1451,7 +1461,7 @@ __device__ __forceinline__ int tile_key_cells(const TileGeo &tg, const int *cin)
 typedef double dvec2 __attribute__((ext_vector_type(2)));
 
 template <int ND, bool V3D, bool KICK, bool SORT>
-__global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_push(PushArgs a) {
+__global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PINC_PUSH_WPE))) void k_push(PushArgs a) {
 	constexpr int NC = 1 << ND;
 	constexpr int NW = kPushThreads / 64;
 	__shared__ double rhoL[kRhoBoxCap];
@@ -1472,7 +1482,22 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(4)
 	__shared__ unsigned char stageF[SORT ? 2 * kPushChunk : 1];
 	const Geo32 G = make_geo32(a.g);
 	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-	const long base = (long)blockIdx.x * kPushChunk;
+	// chunk of this block.  PINC_PUSH_XCD: consecutive chunks (the same cell
+	// tiles after a sort: shared E nodes and rho atomics) on one XCD's L2.
+	// Blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md,
+	// workgroup dispatch), so block b runs on XCD b % 8; the map is a
+	// bijection for any grid size and only a placement hint, never needed
+	// for correctness.
+#if PINC_PUSH_XCD
+	const unsigned chunk = [] {
+		const unsigned nb = gridDim.x, x = blockIdx.x & 7u, y = blockIdx.x >> 3;
+		const unsigned q = nb >> 3, r = nb & 7u;
+		return x * q + min(x, r) + y;
+	}();
+#else
+	const unsigned chunk = blockIdx.x;
+#endif
+	const long base = (long)chunk * kPushChunk;
 	// item k of a thread: particles in lane-contiguous pairs (16-B loads and
 	// stores, 1 KiB per wave instruction), pair k/2 of the thread
 	auto item = [&](int k) -> long { return base + (long)((k >> 1) * (2 * kPushThreads) + 2 * threadIdx.x + (k & 1)); };
@@ -1962,7 +1987,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(4)
 
 	if (KICK) {
 		double t = block_sum(ke, kered);
-		if (threadIdx.x == 0) a.kePartial[blockIdx.x] = t;
+		if (threadIdx.x == 0) a.kePartial[chunk] = t;
 	}
 	__syncthreads();
 	if (!SORT && threadIdx.x == 0) {

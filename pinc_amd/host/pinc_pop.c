@@ -127,8 +127,9 @@ Population *pAlloc(const dictionary *ini) {
 	long nChunks = maxS / PINC_CHUNK + 2;
 	int *chunkOffset = NULL;
 	pinc_check(pinc_hip_malloc((void **)&dv->chunkCount, dv->chunkBase[ns] * sizeof(int)), "pAlloc chunks");
-	/* one KE partial per push block (PINC_CHUNK/2 particles) */
-	pinc_check(pinc_hip_malloc((void **)&dv->kePartial, (maxS / (PINC_CHUNK / 2) + 16) * sizeof(double)), "pAlloc ke");
+	/* one KE partial per push block (PINC_CHUNK/2 particles by default, at
+	 * least PINC_CHUNK/8) */
+	pinc_check(pinc_hip_malloc((void **)&dv->kePartial, (maxS / (PINC_CHUNK / 8) + 16) * sizeof(double)), "pAlloc ke");
 	long scanWork = 2 * (nChunks / 4096 + 1) + 1;
 	pinc_check(pinc_hip_malloc((void **)&chunkOffset, (nChunks + 1 + scanWork) * sizeof(int)), "pAlloc chunks");
 	for (int s = 0; s < ns; s++) {
