@@ -47,6 +47,7 @@ typedef struct {
 	int nSpecies;
 	int nDims;
 	PincDevPop *dev;     /* device twin */
+	long long h5;        /* .pop.h5 file (hid_t; rank 0 only, pOpenH5) */
 } Population;
 
 /* core.h:112-138 (MPI request/handle fields replaced by the RCCL context) */
@@ -71,6 +72,7 @@ typedef struct {
 	int *nGhostLayers;
 	bndType *bnd;
 	PincDevGrid *dev;    /* device twin */
+	long long h5;        /* .grid.h5 file (hid_t; rank 0 only, gOpenH5) */
 } Grid;
 
 /* core.h:392-417 */
@@ -204,6 +206,30 @@ void sFree(SpectralSolver *solver);
 void sSolve(SpectralSolver *solver, Grid *rho, Grid *phi, const MpiInfo *mpiInfo);
 long sSolveCount(const SpectralSolver *solver);
 
+/* ------------------------------------------------------- h5 output -- */
+/* The reference's output files (grid.c:1161-1270, population.c:497-698,
+ * io.c:566-734), written by rank 0 with serial HDF5 loaded at run time
+ * (PINC_HDF5_LIB or libhdf5.so); hid_t is passed as long long and MPI_Op as
+ * PINC_OP_SUM / PINC_OP_MAX. */
+#define PINC_OP_SUM 0
+#define PINC_OP_MAX 1
+void gOpenH5(const dictionary *ini, Grid *grid, const MpiInfo *mpiInfo, const Units *units, double denorm,
+             const char *fName);
+void gWriteH5(const Grid *grid, const MpiInfo *mpiInfo, double n);
+void gCloseH5(Grid *grid);
+void pOpenH5(const dictionary *ini, Population *pop, const Units *units, const char *fName);
+void pWriteH5(Population *pop, const MpiInfo *mpiInfo, double posN, double velN);
+void pCloseH5(Population *pop);
+long long xyOpenH5(const dictionary *ini, const char *fName);
+void xyCreateDataset(long long h5, const char *name);
+void xyWrite(long long h5, const char *name, double x, double y, int op);
+void xyCloseH5(long long h5);
+void pCreateEnergyDatasets(long long xy, Population *pop);
+void pWriteEnergy(long long xy, Population *pop, double x);
+int pinc_h5_available(void);
+long pinc_h5_read(const char *path, const char *name, int isAttr, double *out, long cap);
+int pinc_h5_dims(const char *path, const char *name, long *dimsOut);
+
 /* ---------------------------------------------------------- run mode -- */
 void regular(dictionary *ini);
 funPtr regular_set(dictionary *ini);
@@ -244,6 +270,11 @@ int pinc_sim_grid_set(PincSim *sim, int which, const double *in);
 int pinc_sim_emigrants(PincSim *sim, long *nEmigrants);
 int pinc_sim_species(PincSim *sim, double *charge, double *mass);
 int pinc_sim_sync(PincSim *sim);
+/* main.c's output (main.c:120-131, 262-266): open pop, rho, phi, E and the
+ * history under files:output, then write them for step n (positions at n,
+ * velocities at n+0.5, energies) -- what regular() does when files:h5 = 1 */
+int pinc_sim_open_output(PincSim *sim);
+int pinc_sim_write_output(PincSim *sim, double n);
 /* per-phase device times accumulated since the last reset (ms):
  * 0 move+classify, 1 extract, 2 migrate, 3 deposit(+fold), 4 solve,
  * 5 efield, 6 accelerate, 7 energy */

@@ -64,6 +64,11 @@ _sigs = {
     "pinc_sim_emigrants": (C.c_int, [C.c_void_p, C.c_void_p]),
     "pinc_sim_species": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "pinc_sim_sync": (C.c_int, [C.c_void_p]),
+    "pinc_sim_open_output": (C.c_int, [C.c_void_p]),
+    "pinc_sim_write_output": (C.c_int, [C.c_void_p, C.c_double]),
+    "pinc_h5_available": (C.c_int, []),
+    "pinc_h5_read": (C.c_long, [C.c_char_p, C.c_char_p, C.c_int, C.c_void_p, C.c_long]),
+    "pinc_h5_dims": (C.c_int, [C.c_char_p, C.c_char_p, C.c_void_p]),
     "pinc_sim_timers": (C.c_int, [C.c_void_p, C.c_void_p]),
     "pinc_sim_timers_reset": (C.c_int, [C.c_void_p]),
     "pinc_sim_total_particles": (C.c_long, [C.c_void_p]),

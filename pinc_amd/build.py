@@ -32,7 +32,7 @@ HIP_FLAGS = ["-std=c++17", "-O3", f"--offload-arch={ARCH}", "-ffp-contract=off",
 C_FLAGS = ["-std=c11", "-O2", "-fPIC", "-Wall", "-ffp-contract=off", f"-I{INC}", f"-I{HOST}"]
 
 HIP_SRC = ["runtime.hip", "k_particles.hip", "k_grid.hip", "k_mg.hip", "k_spectral.hip"]
-C_SRC = ["pinc_core.c", "pinc_comm.c", "pinc_grid.c", "pinc_pop.c", "pinc_pusher.c", "pinc_mg.c", "pinc_spectral.c", "pinc_regular.c"]
+C_SRC = ["pinc_core.c", "pinc_comm.c", "pinc_grid.c", "pinc_pop.c", "pinc_pusher.c", "pinc_mg.c", "pinc_spectral.c", "pinc_regular.c", "pinc_h5.c"]
 
 
 def _run(cmd: list[str]) -> None:
@@ -71,7 +71,7 @@ def build(verbose: bool = False, jobs: int = 8) -> dict:
     if jobs_list or not libhip.exists() or not libhost.exists():
         _run([HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", str(libhip), *hip_objs,
               "-L/opt/rocm/lib", "-lrccl", "-lrocfft", "-Wl,-rpath,/opt/rocm/lib"])
-        _run(["gcc", "-shared", "-o", str(libhost), *c_objs, f"-L{LIB}", "-lpinc_hip", "-lm",
+        _run(["gcc", "-shared", "-o", str(libhost), *c_objs, f"-L{LIB}", "-lpinc_hip", "-lm", "-ldl",
               "-Wl,-rpath,$ORIGIN"])
     out = {"libpinc_hip": str(libhip), "libpinc": str(libhost)}
     if verbose:

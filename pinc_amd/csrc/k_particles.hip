@@ -1249,7 +1249,10 @@ constexpr int kPushGroups = PINC_PUSH_GROUPS;
 #ifndef PINC_PUSH_XCD
 #define PINC_PUSH_XCD 1
 #endif
-constexpr int kPushThreads = 256;
+#ifndef PINC_PUSH_THREADS
+#define PINC_PUSH_THREADS 256
+#endif
+constexpr int kPushThreads = PINC_PUSH_THREADS;
 constexpr int kPushItems = PINC_PUSH_ITEMS;  // particles per thread, in lane-contiguous pairs
 constexpr int kPushChunk = kPushThreads * kPushItems;  // particles per block (PINC_CHUNK / 2 by default)
 static_assert(kPushChunk >= PINC_CHUNK / 8 && PINC_CHUNK % kPushChunk == 0, "kePartial holds PINC_CHUNK/8 per chunk");

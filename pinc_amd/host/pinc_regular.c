@@ -37,6 +37,8 @@ struct PincSim {
 	PincSimOpts opts;
 	int initialised;
 	long steps;
+	int output;        /* pinc_sim_open_output ran: files below are open */
+	long long history;
 };
 
 static int g_simActive = 0;
@@ -163,8 +165,41 @@ static void sim_step(PincSim *S) {
 	S->steps++;
 }
 
+static void output_close(PincSim *S) {
+	if (!S->output) return;
+	pCloseH5(S->pop);
+	gCloseH5(S->rho);
+	gCloseH5(S->phi);
+	gCloseH5(S->E);
+	xyCloseH5(S->history);
+	S->output = 0;
+}
+
+/* main.c:118-131: pop, rho, phi, E and history files, denorm 1 */
+static void output_open(PincSim *S) {
+	if (S->output) return;
+	double denorm = 1.;
+	pOpenH5(S->ini, S->pop, S->units, "pop");
+	gOpenH5(S->ini, S->rho, S->mpi, S->units, denorm, "rho");
+	gOpenH5(S->ini, S->phi, S->mpi, S->units, denorm, "phi");
+	gOpenH5(S->ini, S->E, S->mpi, S->units, denorm, "E");
+	S->history = xyOpenH5(S->ini, "history");
+	pCreateEnergyDatasets(S->history, S->pop);
+	S->output = 1;
+}
+
+/* main.c:262-266 */
+static void output_write(PincSim *S, double n) {
+	gWriteH5(S->E, S->mpi, n);
+	gWriteH5(S->rho, S->mpi, n);
+	gWriteH5(S->phi, S->mpi, n);
+	pWriteH5(S->pop, S->mpi, n, n + 0.5);
+	pWriteEnergy(S->history, S->pop, n);
+}
+
 static void sim_free(PincSim *S) {
 	if (!S) return;
+	output_close(S);
 	if (S->solverFree) S->solverFree(S->solver);
 	gFree(S->E);
 	gFree(S->rho);
@@ -181,11 +216,17 @@ void regular(dictionary *ini) {
 	PincSim *S = sim_build(ini, NULL);
 	sim_init(S);
 	sim_fields(S);
+	/* the reference writes rho, phi, E, the particles and the energies every
+	 * step (main.c:262-266); here only with files:h5 = 1, since at C4 that
+	 * is tens of GB per step */
+	int h5 = iniHas(ini, "files:h5") && iniGetInt(ini, "files:h5");
+	if (h5) output_open(S);
 	int nTimeSteps = iniGetInt(ini, "time:nTimeSteps");
 	for (int n = 1; n <= nTimeSteps; n++) {
 		msg(STATUS, "Computing time-step %i", n);
 		sim_step(S);
 		msg(STATUS, "KE %.17g PE %.17g", S->pop->kinEnergy[S->pop->nSpecies], S->pop->potEnergy[S->pop->nSpecies]);
+		if (h5) output_write(S, (double)n);
 	}
 	S->ini = NULL; /* owned by the caller */
 	sim_free(S);
@@ -344,6 +385,17 @@ int pinc_sim_emigrants(PincSim *S, long *nEmigrants) {
 int pinc_sim_species(PincSim *S, double *charge, double *mass) {
 	memcpy(charge, S->pop->charge, S->pop->nSpecies * sizeof(double));
 	memcpy(mass, S->pop->mass, S->pop->nSpecies * sizeof(double));
+	return 0;
+}
+
+int pinc_sim_open_output(PincSim *S) {
+	output_open(S);
+	return 0;
+}
+
+int pinc_sim_write_output(PincSim *S, double n) {
+	if (!S->output) output_open(S);
+	output_write(S, n);
 	return 0;
 }
 

@@ -75,6 +75,16 @@ class Sim:
     def sync(self) -> None:
         HOST.pinc_sim_sync(self._h)
 
+    # -- output (the reference's .h5 files) ---------------------------------
+    def open_output(self) -> None:
+        """pop/rho/phi/E/history files under files:output (main.c:118-131)."""
+        HOST.pinc_sim_open_output(self._h)
+
+    def write_output(self, n: float) -> None:
+        """main.c:262-266 for step n: E, rho, phi at n, positions at n,
+        velocities at n + 0.5, energy rows."""
+        HOST.pinc_sim_write_output(self._h, float(n))
+
     # -- diagnostics -------------------------------------------------------
     def energy(self) -> tuple[float, float, np.ndarray]:
         ke, pe = C.c_double(), C.c_double()
@@ -142,3 +152,28 @@ class Sim:
 
     def timers_reset(self) -> None:
         HOST.pinc_sim_timers_reset(self._h)
+
+
+def h5_available() -> bool:
+    return bool(HOST.pinc_h5_available())
+
+
+def h5_read(path: str, name: str, attr: bool = False) -> np.ndarray:
+    """A dataset (or double attribute) of an .h5 file, through the same
+    run-time HDF5 binding the writer uses (h5py is not installed)."""
+    if attr:
+        out = np.zeros(1)
+        n = HOST.pinc_h5_read(str(path).encode(), name.encode(), 1, out.ctypes.data, 1)
+        if n < 0:
+            raise KeyError(f"{path}: attribute {name}")
+        return out
+    dims = np.zeros(8, dtype=np.int64)
+    r = HOST.pinc_h5_dims(str(path).encode(), name.encode(), dims.ctypes.data)
+    if r < 0:
+        raise KeyError(f"{path}: {name}")
+    shape = tuple(int(d) for d in dims[:r])
+    out = np.zeros(int(np.prod(shape)) if shape else 1)
+    n = HOST.pinc_h5_read(str(path).encode(), name.encode(), 0, out.ctypes.data, out.size)
+    if n < 0:
+        raise KeyError(f"{path}: {name}")
+    return out.reshape(shape)
