@@ -195,6 +195,19 @@ void ow_init(OWorld *w, int perturb, int maxwell, unsigned long long seed);
 void ow_init_fields(OWorld *w);
 void ow_step(OWorld *w);
 
+/* ------------------------------------------------ immersed objects -- */
+/* orc_obj.c: object.c restated for one subdomain (defects corrected, see
+ * the file header) */
+typedef struct OObj OObj;
+OObj *oo_create(OWorld *w, const double *maskTrue);
+void oo_free(OObj *o);
+void oo_capacitance(OObj *o, OWorld *w);
+void oo_apply(OObj *o, OWorld *w, double *phiC);
+void oo_collect(OObj *o, OWorld *w);
+void oo_init_collect(OObj *o, OWorld *w);
+void oo_step(OWorld *w, OObj *o);
+const OGrid *oo_rho_obj_grid(const OObj *o);
+
 /* Splittable counter-based RNG shared with the product's initialiser (the
  * reference's GSL mt19937+ziggurat is absent: parity of draws is unpinned,
  * SURVEY.md 8(c)).  normal = Box-Muller on two 53-bit uniforms of

@@ -50,6 +50,20 @@ def _load() -> C.CDLL:
         "orc_kat_neighborhood": (None, [C.c_char_p, vp, vp]),
         "orc_world_ndims": (C.c_int, [vp]),
         "orc_world_nspecies": (C.c_int, [vp]),
+        "oo_create": (vp, [vp, vp]),
+        "oo_free": (None, [vp]),
+        "oo_capacitance": (None, [vp, vp]),
+        "oo_apply": (None, [vp, vp, vp]),
+        "oo_collect": (None, [vp, vp]),
+        "oo_init_collect": (None, [vp, vp]),
+        "oo_step": (None, [vp, vp]),
+        "oo_nobjects": (C.c_int, [vp]),
+        "oo_nsurface": (C.c_long, [vp, C.c_int]),
+        "oo_ninterior": (C.c_long, [vp, C.c_int]),
+        "oo_surface_nodes": (None, [vp, C.c_int, vp]),
+        "oo_interior_nodes": (None, [vp, C.c_int, vp]),
+        "oo_collected": (C.c_double, [vp, C.c_int]),
+        "oo_rho_obj": (None, [vp, vp]),
     }
     for n, (r, a) in sigs.items():
         f = getattr(lib, n)
@@ -169,3 +183,60 @@ def run_steps(ini: str, overrides: Sequence[str], steps: int, literal=False, per
         cyc.append(w.cycles)
     w.close()
     return np.array(ke), np.array(pe), np.array(cyc)
+
+
+class Objects:
+    """Immersed objects of a one-subdomain World (orc_obj.c, object.c
+    restated with its defects corrected).  mask: [z, y, x] object ids over
+    the true nodes."""
+
+    def __init__(self, world: "World", mask):
+        m = np.ascontiguousarray(mask, dtype=np.float64)
+        self.w = world
+        self._h = LIB.oo_create(world._h, m.ctypes.data)
+        self.n = LIB.oo_nobjects(self._h)
+
+    def close(self):
+        if self._h:
+            LIB.oo_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def surface(self, a: int = 0) -> np.ndarray:
+        out = np.zeros(LIB.oo_nsurface(self._h, a), dtype=np.int64)
+        LIB.oo_surface_nodes(self._h, a, out.ctypes.data)
+        return out
+
+    def interior(self, a: int = 0) -> np.ndarray:
+        out = np.zeros(LIB.oo_ninterior(self._h, a), dtype=np.int64)
+        LIB.oo_interior_nodes(self._h, a, out.ctypes.data)
+        return out
+
+    def capacitance(self):
+        LIB.oo_capacitance(self._h, self.w._h)
+
+    def apply(self) -> np.ndarray:
+        pc = np.zeros(max(1, self.n))
+        LIB.oo_apply(self._h, self.w._h, pc.ctypes.data)
+        return pc[:self.n]
+
+    def collect(self):
+        LIB.oo_collect(self._h, self.w._h)
+
+    def init_collect(self):
+        LIB.oo_init_collect(self._h, self.w._h)
+
+    def step(self, n: int = 1):
+        for _ in range(n):
+            LIB.oo_step(self.w._h, self._h)
+
+    def collected(self, a: int = 0) -> float:
+        return LIB.oo_collected(self._h, a)
+
+    def rho_obj(self) -> np.ndarray:
+        g = self.w.grid(0)
+        out = np.zeros(g.size)
+        LIB.oo_rho_obj(self._h, out.ctypes.data)
+        return out.reshape(g.shape)

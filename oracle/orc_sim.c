@@ -386,6 +386,36 @@ void ow_step(OWorld *w){
 	do_energy(w);
 }
 
+/* main.c:197-274 with the immersed-object calls (main.c:221-238):
+ * collect after migration, rho += rhoObj after the fold (the literal mode
+ * folds again, main.c:232), solve, capacitance correction, solve again */
+void oo_step(OWorld *w, OObj *o){
+	if(w->P != 1) orc_die("object oracle: one subdomain only");
+	opu_move(&w->r[0].pop);
+	do_extract(w);
+	ow_migrate(w);
+	oo_collect(o, w);
+	do_distr(w);
+	og_addto(&w->r[0].rho, oo_rho_obj_grid(o));
+	if(w->literal){
+		OGrid *rho[1] = {&w->r[0].rho};
+		ow_halo(w, rho, OP_ADD, FROMHALO);
+	}
+	do_solve(w);
+	oo_apply(o, w, NULL);
+	do_solve(w);
+	do_efield(w, 1);
+	do_acc(w);
+	do_energy(w);
+}
+
+/* main.c:163-166: particles initially inside an object are removed and
+ * their charge discarded */
+void oo_init_collect(OObj *o, OWorld *w){
+	oo_collect(o, w);
+	og_zero((OGrid *)oo_rho_obj_grid(o));
+}
+
 /* ======================================================= ctypes API ===== */
 OWorld *orc_world_new(const char *iniPath, int nOver, const char **over, int literal){
 	OIni *ini = oini_load(iniPath);
