@@ -199,6 +199,20 @@ int pinc_hip_extract(pinc_pop_t pop, int s, const unsigned char *flags, int *chu
                      int center, int nNeighbors, pinc_extract_ws_t ws, long *nEmig,
                      long *neCount, void *stream);
 
+/* immersed objects (k_objects.hip; object.c, config C5).  inside: one byte
+ * per node of the padded reference layout (strides 1, sy, sz; nNodes
+ * nodes), 1 for interior nodes of an object.  obj_flag writes flags/chunk
+ * counts in pinc_hip_extract's format (flag 0 = remove, 13 = keep) for
+ * oCollectObjectCharge (object.c:460-515).  idx: device indices of the
+ * surface nodes in a grid's slab storage.  obj_correct adds
+ * sum_j M[j*n+i] (phiC - phiS[j]) to rho[idx[i]] (object.c:349-362). */
+int pinc_hip_obj_flag(pinc_pop_t pop, int s, const unsigned char *inside, long sy, long sz, long nNodes,
+                      unsigned char *flags, int *chunkCount, void *stream);
+int pinc_hip_obj_gather(const double *grid, const long *idx, long n, double *out, void *stream);
+int pinc_hip_obj_correct(const double *M, const double *phiS, long n, double phiC, const long *idx, double *rho,
+                         void *stream);
+int pinc_hip_obj_add(double *grid, const long *idx, long n, double v, void *stream);
+
 /* multi-rank migration payload: records of 7 doubles (nd positions, nd
  * velocities, padding, direction) packed from buffer entries [first,
  * first+n), and appended to species s at index dst with the receiver's

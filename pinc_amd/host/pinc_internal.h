@@ -124,6 +124,17 @@ struct PincDevGrid {
 	double *scaled;     /* E as rescaled for the species being pushed (lazy) */
 };
 
+/* immersed objects (pinc_obj.c; object.c, config C5) */
+typedef struct PincObj PincObj;
+PincObj *pinc_obj_create(const dictionary *ini, const Grid *rho);
+void pinc_obj_free(PincObj *o);
+void pinc_obj_capacitance(PincObj *o, Grid *rho, Grid *phi, void *solver,
+                          void (*solve)(void *, Grid *, Grid *, const MpiInfo *), const MpiInfo *mpi);
+void pinc_obj_collect(PincObj *o, Population *pop, int discard);
+void pinc_obj_add_rho(PincObj *o, Grid *rho);
+double pinc_obj_apply(PincObj *o, Grid *rho, const Grid *phi);
+long pinc_obj_nsurface(const PincObj *o);
+double pinc_obj_collected(const PincObj *o);
 /* Boris selected through methods:acc: its initial half step (pinc_regular.c) */
 void pinc_boris_half_step(int on);
 int pinc_boris_selected(funPtr acc);

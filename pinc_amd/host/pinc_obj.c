@@ -1,0 +1,256 @@
+/*
+ * pinc_obj.c -- immersed objects (object.c, config C5) on the device path,
+ * one subdomain (P = 1), reference particle layout, unfused operators.
+ *
+ *   pinc_obj_create       oFillLookupTables (object.c:111-160) and
+ *                         oFindObjectSurfaceNodes (object.c:368-458) on the
+ *                         object mask.  The mask is a sphere given by
+ *                         objects:sphere = cx,cy,cz,r in true-node
+ *                         coordinates (an extension: the reference reads an
+ *                         HDF5 /Object grid, object.c:727-756)
+ *   pinc_obj_capacitance  oComputeCapacitanceMatrix (object.c:163-298): one
+ *                         device solve per surface node with a unit charge
+ *                         there; the inverse (host Gauss-Jordan, GSL's LU in
+ *                         the reference) goes to the device
+ *   pinc_obj_collect      oCollectObjectCharge (object.c:460-515): flag kernel
+ *                         + the emigrant back-fill (pinc_hip_extract) removes
+ *                         the particles; their charge is spread over the
+ *                         surface nodes of rhoObj
+ *   pinc_obj_add_rho      gAddTo(rho, rhoObj) (main.c:230)
+ *   pinc_obj_apply        oApplyCapacitanceMatrix (object.c:301-366)
+ *
+ * The checker is oracle/orc_obj.c, with the same three corrections of
+ * reference defects (pCut's index, the re-test of the swapped-in particle,
+ * the unit-charge reset); tests/test_gpu_objects.py.
+ */
+#define _GNU_SOURCE
+#include "pinc_internal.h"
+#include <math.h>
+
+void pinc_pop_grow_ws(Population *pop, int s, long n);
+
+struct PincObj {
+	long nSurf;          /* surface nodes (one object) */
+	long *surfNode;      /* host: padded reference-layout node indices */
+	long *dSurf;         /* device: slab-storage indices of the surface nodes */
+	unsigned char *dInside; /* device: interior byte per padded node */
+	long nNodes, sy, sz;
+	double *dM;          /* device: inverse response matrix, row-major nSurf^2 */
+	double *wRow;        /* host: sum_i M[j][i] per j (eq. 7) */
+	double capSum;       /* 1 / sum M */
+	double *dPhiS;       /* device: phi at the surface nodes */
+	double rhoObjVal;    /* rhoObj at every surface node (accumulated) */
+	double collected;
+	int haveCap;
+};
+
+static void invert(double *A, double *inv, long n) {
+	for (long i = 0; i < n; i++)
+		for (long j = 0; j < n; j++) inv[i * n + j] = i == j;
+	for (long c = 0; c < n; c++) {
+		long p = c;
+		for (long r = c + 1; r < n; r++)
+			if (fabs(A[r * n + c]) > fabs(A[p * n + c])) p = r;
+		if (A[p * n + c] == 0.0) msg(ERROR, "capacitance matrix is singular");
+		if (p != c)
+			for (long j = 0; j < n; j++) {
+				double t = A[c * n + j];
+				A[c * n + j] = A[p * n + j];
+				A[p * n + j] = t;
+				t = inv[c * n + j];
+				inv[c * n + j] = inv[p * n + j];
+				inv[p * n + j] = t;
+			}
+		double d = 1.0 / A[c * n + c];
+		for (long j = 0; j < n; j++) {
+			A[c * n + j] *= d;
+			inv[c * n + j] *= d;
+		}
+		for (long r = 0; r < n; r++) {
+			if (r == c) continue;
+			double f = A[r * n + c];
+			if (f == 0.0) continue;
+			for (long j = 0; j < n; j++) {
+				A[r * n + j] -= f * A[c * n + j];
+				inv[r * n + j] -= f * inv[c * n + j];
+			}
+		}
+	}
+}
+
+PincObj *pinc_obj_create(const dictionary *ini, const Grid *rho) {
+	if (!iniHas(ini, "objects:sphere")) return NULL;
+	if (g_pinc.nranks > 1) msg(ERROR, "objects: one subdomain only on the device path");
+	if (rho->rank != 4) msg(ERROR, "objects are 3-D (object.c)");
+	double *sp = iniGetDoubleArr(ini, "objects:sphere", 4);
+	PincObj *o = calloc(1, sizeof(*o));
+	const int *ts = rho->trueSize;
+	int T[3] = {ts[1], ts[2], ts[3]}, S[3] = {T[0] + 2, T[1] + 2, T[2] + 2};
+	o->sy = S[0];
+	o->sz = (long)S[0] * S[1];
+	o->nNodes = o->sz * S[2];
+	/* node mask with periodic ghosts: object id 1 inside the sphere */
+	unsigned char *m = calloc(o->nNodes, 1), *inside = calloc(o->nNodes, 1);
+	for (long node = 0; node < o->nNodes; node++) {
+		int c[3] = {(int)(node % S[0]), (int)((node / o->sy) % S[1]), (int)(node / o->sz)};
+		double r2 = 0;
+		int ghost = 0;
+		for (int d = 0; d < 3; d++) {
+			int t = c[d] - 1;
+			if (t < 0 || t >= T[d]) ghost = 1;
+			t = (t + T[d]) % T[d];
+			r2 += (t - sp[d]) * (t - sp[d]);
+		}
+		m[node] = r2 <= sp[3] * sp[3];
+		inside[node] = m[node] && !ghost;
+	}
+	free(sp);
+	/* surface: true nodes with 1..7 of the 8 nodes at offsets {0,-1}^3 */
+	const long nb[8] = {0, -o->sz, -1, -1 - o->sz, -o->sy, -o->sy - o->sz, -o->sy - 1, -o->sy - 1 - o->sz};
+	o->surfNode = malloc(o->nNodes * sizeof(long));
+	long *dIdx = malloc(o->nNodes * sizeof(long));
+	long ps = (long)T[0] * T[1];
+	for (long node = 0; node < o->nNodes; node++) {
+		int c[3] = {(int)(node % S[0]), (int)((node / o->sy) % S[1]), (int)(node / o->sz)};
+		if (c[0] < 1 || c[0] > T[0] || c[1] < 1 || c[1] > T[1] || c[2] < 1 || c[2] > T[2]) continue;
+		int d = 0;
+		for (int q = 0; q < 8; q++) d += m[node + nb[q]];
+		if (d > 0 && d < 8) {
+			o->surfNode[o->nSurf] = node;
+			dIdx[o->nSurf] = (long)c[2] * ps + (long)(c[1] - 1) * T[0] + (c[0] - 1);
+			o->nSurf++;
+		}
+	}
+	if (!o->nSurf) msg(ERROR, "objects:sphere has no surface nodes");
+	pinc_check(pinc_hip_malloc((void **)&o->dInside, o->nNodes), "objects");
+	pinc_check(pinc_hip_h2d(o->dInside, inside, o->nNodes, g_pinc.stream), "objects");
+	pinc_check(pinc_hip_malloc((void **)&o->dSurf, o->nSurf * sizeof(long)), "objects");
+	pinc_check(pinc_hip_h2d(o->dSurf, dIdx, o->nSurf * sizeof(long), g_pinc.stream), "objects");
+	pinc_check(pinc_hip_malloc((void **)&o->dPhiS, o->nSurf * sizeof(double)), "objects");
+	pinc_check(pinc_hip_stream_sync(g_pinc.stream), "objects");
+	free(m);
+	free(inside);
+	free(dIdx);
+	return o;
+}
+
+void pinc_obj_free(PincObj *o) {
+	if (!o) return;
+	pinc_hip_free(o->dInside);
+	pinc_hip_free(o->dSurf);
+	pinc_hip_free(o->dPhiS);
+	pinc_hip_free(o->dM);
+	free(o->surfNode);
+	free(o->wRow);
+	free(o);
+}
+
+long pinc_obj_nsurface(const PincObj *o) { return o ? o->nSurf : 0; }
+double pinc_obj_collected(const PincObj *o) { return o ? o->collected : 0.0; }
+
+/* object.c:163-298: column i = phi at the surface nodes for a unit charge
+ * at surface node i (solver warm-started column to column, as the
+ * reference's); rho and phi are restored afterwards */
+void pinc_obj_capacitance(PincObj *o, Grid *rho, Grid *phi, void *solver,
+                          void (*solve)(void *, Grid *, Grid *, const MpiInfo *), const MpiInfo *mpi) {
+	long n = o->nSurf, N = rho->dev->n;
+	double *saveR = NULL, *saveP = NULL;
+	pinc_check(pinc_hip_malloc((void **)&saveR, N * sizeof(double)), "cap save");
+	pinc_check(pinc_hip_malloc((void **)&saveP, N * sizeof(double)), "cap save");
+	pinc_check(pinc_hip_d2d(saveR, rho->dev->d, N * sizeof(double), g_pinc.stream), "cap save");
+	pinc_check(pinc_hip_d2d(saveP, phi->dev->d, N * sizeof(double), g_pinc.stream), "cap save");
+	pinc_check(pinc_hip_memset(phi->dev->d, 0, N * sizeof(double), g_pinc.stream), "cap");
+	double *P = malloc(n * n * sizeof(double)), *col = malloc(n * sizeof(double));
+	for (long i = 0; i < n; i++) {
+		pinc_check(pinc_hip_memset(rho->dev->d, 0, N * sizeof(double), g_pinc.stream), "cap");
+		pinc_check(pinc_hip_obj_add(rho->dev->d, o->dSurf + i, 1, 1.0, g_pinc.stream), "cap unit charge");
+		solve(solver, rho, phi, mpi);
+		pinc_check(pinc_hip_obj_gather(phi->dev->d, o->dSurf, n, o->dPhiS, g_pinc.stream), "cap gather");
+		pinc_check(pinc_hip_d2h(col, o->dPhiS, n * sizeof(double), g_pinc.stream), "cap gather");
+		for (long k = 0; k < n; k++) P[k * n + i] = col[k];
+	}
+	double *M = malloc(n * n * sizeof(double));
+	invert(P, M, n);
+	double s = 0;
+	o->wRow = calloc(n, sizeof(double));
+	for (long j = 0; j < n; j++)
+		for (long i = 0; i < n; i++) {
+			s += M[j * n + i];
+			o->wRow[j] += M[j * n + i];
+		}
+	o->capSum = 1.0 / s;
+	pinc_check(pinc_hip_malloc((void **)&o->dM, n * n * sizeof(double)), "cap matrix");
+	pinc_check(pinc_hip_h2d(o->dM, M, n * n * sizeof(double), g_pinc.stream), "cap matrix");
+	pinc_check(pinc_hip_d2d(rho->dev->d, saveR, N * sizeof(double), g_pinc.stream), "cap restore");
+	pinc_check(pinc_hip_d2d(phi->dev->d, saveP, N * sizeof(double), g_pinc.stream), "cap restore");
+	pinc_check(pinc_hip_stream_sync(g_pinc.stream), "cap");
+	pinc_hip_free(saveR);
+	pinc_hip_free(saveP);
+	free(P);
+	free(M);
+	free(col);
+	rho->dev->ghostsValid = phi->dev->ghostsValid = 0;
+	o->haveCap = 1;
+}
+
+/* object.c:460-515 (corrected): remove the particles whose cell's lower
+ * node is interior, with the emigrant back-fill order; their charge goes
+ * to rhoObj's surface nodes.  discard: main.c:163-166 (charge dropped). */
+void pinc_obj_collect(PincObj *o, Population *pop, int discard) {
+	PincDevPop *dv = pop->dev;
+	if (dv->fused || dv->tiled) msg(ERROR, "objects need population:fused=0 and the reference layout");
+	double cnt = 0;
+	for (int s = 0; s < pop->nSpecies; s++) {
+		long n = pop->iStop[s] - pop->iStart[s];
+		if (n <= 0) continue;
+		long nb = (n + PINC_CHUNK - 1) / PINC_CHUNK;
+		for (int attempt = 0;; attempt++) {
+			pinc_pop_t p = pinc_devpop(pop);
+			pinc_check(pinc_hip_obj_flag(p, s, o->dInside, o->sy, o->sz, o->nNodes, dv->flags,
+			                             dv->chunkCount + dv->chunkBase[s], g_pinc.stream),
+			           "object flag");
+			(void)nb;
+			long nRem = 0;
+			long neCount[PINC_NNE];
+			int rc = pinc_hip_extract(p, s, dv->flags, dv->chunkCount + dv->chunkBase[s], 13, PINC_NNE, dv->ws[s],
+			                          &nRem, neCount, g_pinc.stream);
+			if (rc == PINC_ERR_CAPACITY && attempt == 0) {
+				pinc_pop_grow_ws(pop, s, nRem);
+				continue;
+			}
+			pinc_check(rc, "object collect");
+			pop->iStop[s] -= nRem;
+			cnt += pop->charge[s] * (double)nRem;
+			break;
+		}
+	}
+	dv->flagsValid = 0;
+	if (discard) return;
+	/* object.c:508-513: chargeCounter * invNrSurfNod added per surface node */
+	o->collected += cnt;
+	o->rhoObjVal += cnt * (1.0 / (double)o->nSurf);
+}
+
+/* gAddTo(rho, rhoObj) (main.c:230): rhoObj is rhoObjVal at every surface
+ * node and zero elsewhere */
+void pinc_obj_add_rho(PincObj *o, Grid *rho) {
+	if (o->rhoObjVal != 0.0)
+		pinc_check(pinc_hip_obj_add(rho->dev->d, o->dSurf, o->nSurf, o->rhoObjVal, g_pinc.stream), "rho += rhoObj");
+}
+
+/* object.c:301-366; returns phi_c */
+double pinc_obj_apply(PincObj *o, Grid *rho, const Grid *phi) {
+	if (!o->haveCap) msg(ERROR, "objects: capacitance matrix not computed");
+	long n = o->nSurf;
+	pinc_check(pinc_hip_obj_gather(phi->dev->d, o->dSurf, n, o->dPhiS, g_pinc.stream), "object gather");
+	double *ph = malloc(n * sizeof(double));
+	pinc_check(pinc_hip_d2h(ph, o->dPhiS, n * sizeof(double), g_pinc.stream), "object gather");
+	/* eq. 7 through the row sums of M (summed once at init) */
+	double pc = 0;
+	for (long j = 0; j < n; j++) pc += o->wRow[j] * ph[j];
+	pc *= o->capSum;
+	free(ph);
+	pinc_check(pinc_hip_obj_correct(o->dM, o->dPhiS, n, pc, o->dSurf, rho->dev->d, g_pinc.stream), "object correct");
+	rho->dev->ghostsValid = 0;
+	return pc;
+}

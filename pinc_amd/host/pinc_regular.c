@@ -37,6 +37,7 @@ struct PincSim {
 	PincSimOpts opts;
 	int initialised;
 	long steps;
+	PincObj *obj;      /* immersed object (objects:sphere), or NULL */
 	int output;        /* pinc_sim_open_output ran: files below are open */
 	long long history;
 };
@@ -91,6 +92,7 @@ static PincSim *sim_build(dictionary *ini, const PincSimOpts *opts) {
 	S->solve = (void (*)(void *, Grid *, Grid *, const MpiInfo *))solve;
 	S->solverFree = (void (*)(void *))solverFree;
 	S->spectral = solve == (void (*)())sSolve;
+	S->obj = pinc_obj_create(ini, S->rho);
 	if (S->opts.literal) {
 		/* main.c:226,232 fold rho's ghosts twice; see literal_ghost_weights */
 		S->pop->dev->geom.literal = 1;
@@ -115,6 +117,14 @@ static void sim_init(PincSim *S) {
 	}
 	S->extractEmigrants(pop, S->mpi);
 	puMigrate(pop, S->mpi, S->rho);
+	if (S->obj) {
+		/* capacitance matrix, then main.c:163-166: particles that start
+		 * inside the object are removed, their charge dropped */
+		pinc_phase_begin(4);
+		pinc_obj_capacitance(S->obj, S->rho, S->phi, S->solver, S->solve, S->mpi);
+		pinc_phase_end(4);
+		pinc_obj_collect(S->obj, pop, 1);
+	}
 }
 
 static void sim_fields(PincSim *S) {
@@ -143,9 +153,17 @@ static void sim_step(PincSim *S) {
 	puMove(pop, NULL);
 	S->extractEmigrants(pop, S->mpi);
 	puMigrate(pop, S->mpi, S->rho);
+	if (S->obj) pinc_obj_collect(S->obj, pop, 0); /* main.c:222 */
 	S->distr(pop, S->rho);
 	gHaloOp((funPtr)addSlice, S->rho, S->mpi, FROMHALO);
-	if (S->opts.literal) {
+	if (S->obj) {
+		/* main.c:230-238: rho += rhoObj (folded again in the literal
+		 * loop), solve, capacitance correction, solve */
+		pinc_obj_add_rho(S->obj, S->rho);
+		if (S->opts.literal) gHaloOp((funPtr)addSlice, S->rho, S->mpi, FROMHALO);
+		S->solve(S->solver, S->rho, S->phi, S->mpi);
+		pinc_obj_apply(S->obj, S->rho, S->phi);
+	} else if (S->opts.literal) {
 		gHaloOp((funPtr)addSlice, S->rho, S->mpi, FROMHALO);
 		S->solve(S->solver, S->rho, S->phi, S->mpi);
 	}
@@ -200,6 +218,7 @@ static void output_write(PincSim *S, double n) {
 static void sim_free(PincSim *S) {
 	if (!S) return;
 	output_close(S);
+	pinc_obj_free(S->obj);
 	if (S->solverFree) S->solverFree(S->solver);
 	gFree(S->E);
 	gFree(S->rho);
