@@ -96,9 +96,11 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="c4", choices=["c4", "c3"],
+    ap.add_argument("--workload", default="c4", choices=["c4", "c3", "c5"],
                     help="c4: warm 3-D plasma, 256^3, 64 ppc, multigrid (BASELINE.json metric, default); "
-                         "c3: Maxwellian 128^3, 32 ppc, spectral (rocFFT) Poisson solve")
+                         "c3: Maxwellian 128^3, 32 ppc, spectral (rocFFT) Poisson solve; "
+                         "c5: c4 plus an immersed sphere (object.c: charge collection, capacitance "
+                         "correction, second solve), one GPU, unfused operators")
     ap.add_argument("--size", type=int, default=None, help="global cells per dimension (c4: 256, c3: 128)")
     ap.add_argument("--ppc", type=int, default=None, help="particles per cell per species (c4: 64, c3: 32)")
     ap.add_argument("--mg", default="native", choices=["native", "reference"],
@@ -159,6 +161,10 @@ def main() -> int:
         comm_id = obj[0]
 
     c3 = args.workload == "c3"
+    c5 = args.workload == "c5"
+    if c5:
+        if world > 1:
+            raise SystemExit("c5: the device object path runs on one subdomain")
     if args.size is None:
         args.size = 128 if c3 else 256
     if args.ppc is None:
@@ -170,6 +176,11 @@ def main() -> int:
                          nalloc_pc=args.ppc + 8)
     if args.mg == "native":
         cfg["multigrid"]["native"] = "1"
+    if c5:
+        # a generated sphere (the reference's bepiColombo object file is not
+        # available): centre of the grid, radius S/32
+        cfg["objects"] = {"sphere": f"{S / 2},{S / 2},{S / 2},{S / 32}"}
+        cfg["population"]["fused"] = "0"
     if args.layout == "tiled":
         cfg["population"]["layout"] = "tiled"
         cfg["population"]["sortInterval"] = str(args.sort_interval)
@@ -272,7 +283,9 @@ def main() -> int:
         "dtype": "f64",
         "data": "synthetic (lattice positions, Maxwellian velocities from a seeded counter RNG)",
         "config": {
-            "workload": (f"C3 Maxwellian 3-D two-species plasma" if c3 else "C4 warm 3-D two-species plasma")
+            "workload": ("C3 Maxwellian 3-D two-species plasma" if c3 else
+                         f"C5 warm 3-D two-species plasma around an immersed sphere (radius {S / 32:g} cells)"
+                         if c5 else "C4 warm 3-D two-species plasma")
                         + f", {S}^3 grid, {args.ppc} ppc per species "
                         f"({n_total} particles), 1D slab decomposition 1,1,{world}",
             "grid": [S, S, S],

@@ -1,6 +1,8 @@
 /*
  * pinc_obj.c -- immersed objects (object.c, config C5) on the device path,
- * one subdomain (P = 1), reference particle layout, unfused operators.
+ * one subdomain (P = 1), unfused operators (either particle layout: with
+ * the tiled one the back-filled slots are deposited individually until the
+ * next sort, as after a migration).
  *
  *   pinc_obj_create       oFillLookupTables (object.c:111-160) and
  *                         oFindObjectSurfaceNodes (object.c:368-458) on the
@@ -198,7 +200,7 @@ void pinc_obj_capacitance(PincObj *o, Grid *rho, Grid *phi, void *solver,
  * to rhoObj's surface nodes.  discard: main.c:163-166 (charge dropped). */
 void pinc_obj_collect(PincObj *o, Population *pop, int discard) {
 	PincDevPop *dv = pop->dev;
-	if (dv->fused || dv->tiled) msg(ERROR, "objects need population:fused=0 and the reference layout");
+	if (dv->fused) msg(ERROR, "objects need population:fused=0 (collection runs between migrate and deposit)");
 	double cnt = 0;
 	for (int s = 0; s < pop->nSpecies; s++) {
 		long n = pop->iStop[s] - pop->iStart[s];

@@ -26,14 +26,20 @@ def _sphere(T, c, r):
     return (((x - c[0]) ** 2 + (y - c[1]) ** 2 + (z - c[2]) ** 2) <= r * r).astype(float)
 
 
-@pytest.mark.parametrize("T,sphere", [((16, 16, 16), (8.0, 8.0, 8.0, 2.5)), ((32, 16, 16), (20.3, 7.6, 9.1, 3.2))])
-def test_object_steps_match_checker(built, T, sphere):
+@pytest.mark.parametrize("T,sphere,layout", [((16, 16, 16), (8.0, 8.0, 8.0, 2.5), "reference"),
+                                             ((32, 16, 16), (20.3, 7.6, 9.1, 3.2), "reference"),
+                                             ((32, 16, 16), (20.3, 7.6, 9.1, 3.2), "tiled")])
+def test_object_steps_match_checker(built, T, sphere, layout):
     from pinc_amd import Sim
     cfg = configs.config("cold3d", true_size=T, nsub=(1, 1, 1))
     cfg["multigrid"]["mgLevels"] = "3"
     cfg["population"]["fused"] = "0"
     cfg["objects"] = {"sphere": ",".join(map(str, sphere))}
     ini = configs.write_ini(cfg)
+    if layout == "tiled":
+        cfg["population"]["layout"] = "tiled"
+        cfg["population"]["sortInterval"] = "2"
+    ini_dev = configs.write_ini(cfg)
     w = orc.World(ini)
     w.init()
     ob = orc.Objects(w, _sphere(T, sphere[:3], sphere[3]))
@@ -41,7 +47,7 @@ def test_object_steps_match_checker(built, T, sphere):
     ob.init_collect()
     w.init_fields()
     steps = 3
-    with Sim(ini) as s:
+    with Sim(ini_dev) as s:
         s.init()
         for sp in range(2):
             assert s.count(sp) == w.count(sp)
@@ -57,6 +63,13 @@ def test_object_steps_match_checker(built, T, sphere):
         for sp in range(2):
             pg, vg = s.particles(sp)
             po, vo, _ = w.particles(sp)
+            if layout == "tiled":
+                # sorted by tile: compare as sets (positions to 1e-9)
+                def order(p, v):
+                    k = np.lexsort(np.round(p * 1e6).T[::-1])
+                    return p[k], v[k]
+                pg, vg = order(pg, vg)
+                po, vo = order(po, vo)
             assert np.max(np.abs(pg - po)) <= 1e-9
             assert np.max(np.abs(vg - vo)) <= 1e-9 * max(1.0, np.abs(vo).max())
         phi_g = s.grid(1)[1:-1, 1:-1, 1:-1]
