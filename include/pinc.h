@@ -24,7 +24,7 @@ extern "C" {
 /* ------------------------------------------------------- core.h types -- */
 typedef void (*funPtr)();
 typedef struct dictionary dictionary;  /* iniparser-compatible dictionary */
-typedef struct ObjectOpaque Object;    /* immersed objects: out of scope */
+typedef struct PincObj Object;        /* immersed objects (object.h:8-21), one subdomain */
 
 typedef enum { STATUS = 0x00, WARNING = 0x01, ERROR = 0x02, TIMER = 0x03, ALL = 0x10 } msgKind;
 typedef enum { PERIODIC = 0x01, DIRICHLET = 0x02, NEUMANN = 0x03, NONE = 0x10 } bndType;
@@ -206,6 +206,16 @@ void sFree(SpectralSolver *solver);
 void sSolve(SpectralSolver *solver, Grid *rho, Grid *phi, const MpiInfo *mpiInfo);
 long sSolveCount(const SpectralSolver *solver);
 
+/* ------------------------------------------------ immersed objects -- */
+/* object.c on the device (pinc_obj.c): one object
+ * from objects:sphere = cx,cy,cz,r or objects:file (an .h5 with /Object
+ * [nz,ny,nx,1]); one subdomain; population:fused = 0 */
+Object *oAlloc(const dictionary *ini);
+void oFree(Object *obj);
+void oComputeCapacitanceMatrix(Object *obj, const dictionary *ini, const MpiInfo *mpiInfo);
+void oApplyCapacitanceMatrix(Grid *rho, const Grid *phi, const Object *obj, const MpiInfo *mpiInfo);
+void oCollectObjectCharge(Population *pop, Grid *rhoObj, Object *obj, const MpiInfo *mpiInfo);
+
 /* ------------------------------------------------------- h5 output -- */
 /* The reference's output files (grid.c:1161-1270, population.c:497-698,
  * io.c:566-734), written by rank 0 with serial HDF5 loaded at run time
@@ -229,6 +239,7 @@ void pWriteEnergy(long long xy, Population *pop, double x);
 int pinc_h5_available(void);
 long pinc_h5_read(const char *path, const char *name, int isAttr, double *out, long cap);
 int pinc_h5_dims(const char *path, const char *name, long *dimsOut);
+int pinc_h5_write(const char *path, const char *name, int rank, const long *dims, const double *data);
 
 /* ---------------------------------------------------------- run mode -- */
 void regular(dictionary *ini);

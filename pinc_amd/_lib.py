@@ -69,6 +69,7 @@ _sigs = {
     "pinc_h5_available": (C.c_int, []),
     "pinc_h5_read": (C.c_long, [C.c_char_p, C.c_char_p, C.c_int, C.c_void_p, C.c_long]),
     "pinc_h5_dims": (C.c_int, [C.c_char_p, C.c_char_p, C.c_void_p]),
+    "pinc_h5_write": (C.c_int, [C.c_char_p, C.c_char_p, C.c_int, C.c_void_p, C.c_void_p]),
     "pinc_sim_timers": (C.c_int, [C.c_void_p, C.c_void_p]),
     "pinc_sim_timers_reset": (C.c_int, [C.c_void_p]),
     "pinc_sim_total_particles": (C.c_long, [C.c_void_p]),

@@ -6,7 +6,7 @@
 //                          emigrant classification format (flag != center),
 //                          with per-chunk counts, so the removal itself is
 //                          pinc_hip_extract's back-fill (the order the
-//                          serial loop gives, oracle/orc_obj.c oo_collect)
+//                          serial loop gives, the object checker under oracle/)
 //   pinc_hip_obj_gather    phi at the surface nodes (object.c:327-333)
 //   pinc_hip_obj_correct   eq. 5 (object.c:349-362): rhoCorr_i =
 //                          sum_j M[j][i] (phi_c - phi_j), added to rho at the

@@ -486,6 +486,20 @@ long pinc_h5_read(const char *path, const char *name, int isAttr, double *out, l
 	return n;
 }
 
+/* a new .h5 file holding one dataset (fixtures for tests, e.g. an /Object
+ * mask for objects:file); returns 0 or -1 */
+int pinc_h5_write(const char *path, const char *name, int rank, const long *dims, const double *data) {
+	h5_load();
+	hid_t f = H.Fcreate(path, 0x0002u /* H5F_ACC_TRUNC */, H5P_DEFAULT, H5P_DEFAULT);
+	if (f < 0) return -1;
+	hsize_t d[8];
+	for (int i = 0; i < rank && i < 8; i++) d[i] = (hsize_t)dims[i];
+	make_groups(f, name);
+	write_dataset(f, name, rank, d, data);
+	H.Fclose(f);
+	return 0;
+}
+
 /* dims of a dataset (up to 8), returns its rank or -1 */
 int pinc_h5_dims(const char *path, const char *name, long *dimsOut) {
 	h5_load();

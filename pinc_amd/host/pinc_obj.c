@@ -21,7 +21,7 @@
  *   pinc_obj_add_rho      gAddTo(rho, rhoObj) (main.c:230)
  *   pinc_obj_apply        oApplyCapacitanceMatrix (object.c:301-366)
  *
- * The checker is oracle/orc_obj.c, with the same three corrections of
+ * The checker is the object restatement under oracle/, with the same three corrections of
  * reference defects (pCut's index, the re-test of the swapped-in particle,
  * the unit-charge reset); tests/test_gpu_objects.py.
  */
@@ -80,33 +80,59 @@ static void invert(double *A, double *inv, long n) {
 	}
 }
 
-PincObj *pinc_obj_create(const dictionary *ini, const Grid *rho) {
-	if (!iniHas(ini, "objects:sphere")) return NULL;
-	if (g_pinc.nranks > 1) msg(ERROR, "objects: one subdomain only on the device path");
-	if (rho->rank != 4) msg(ERROR, "objects are 3-D (object.c)");
+/* object mask over the true nodes, [z][y][x]: objects:sphere = cx,cy,cz,r
+ * (generated) or objects:file = an .h5 file with the reference's /Object
+ * dataset [nz, ny, nx, 1] (oReadH5, object.c:727-756) */
+static double *read_mask(const dictionary *ini, const int T[3]) {
+	long nTrue = (long)T[0] * T[1] * T[2];
+	double *mk = calloc(nTrue, sizeof(double));
+	if (iniHas(ini, "objects:file")) {
+		char *f = iniGetStr(ini, "objects:file");
+		long n = pinc_h5_read(f, "/Object", 0, mk, nTrue);
+		if (n != nTrue) msg(ERROR, "objects:file=%s: /Object must hold %ld values (got %ld)", f, nTrue, n);
+		free(f);
+		return mk;
+	}
 	double *sp = iniGetDoubleArr(ini, "objects:sphere", 4);
+	long k = 0;
+	for (int z = 0; z < T[2]; z++)
+		for (int y = 0; y < T[1]; y++)
+			for (int x = 0; x < T[0]; x++, k++) {
+				double r2 = (x - sp[0]) * (x - sp[0]) + (y - sp[1]) * (y - sp[1]) + (z - sp[2]) * (z - sp[2]);
+				mk[k] = r2 <= sp[3] * sp[3];
+			}
+	free(sp);
+	return mk;
+}
+
+static PincObj *obj_create(const dictionary *ini, const int T[3]) {
+	if (!iniHas(ini, "objects:sphere") && !iniHas(ini, "objects:file")) return NULL;
+	if (g_pinc.nranks > 1) msg(ERROR, "objects: one subdomain only on the device path");
 	PincObj *o = calloc(1, sizeof(*o));
-	const int *ts = rho->trueSize;
-	int T[3] = {ts[1], ts[2], ts[3]}, S[3] = {T[0] + 2, T[1] + 2, T[2] + 2};
+	int S[3] = {T[0] + 2, T[1] + 2, T[2] + 2};
 	o->sy = S[0];
 	o->sz = (long)S[0] * S[1];
 	o->nNodes = o->sz * S[2];
-	/* node mask with periodic ghosts: object id 1 inside the sphere */
+	double *mk = read_mask(ini, T);
+	/* node mask with periodic ghosts (the reference halos the object grid);
+	 * one object: every value above 0.5 (object.c:117-121 takes the highest
+	 * id as the count; several objects are next-row work) */
 	unsigned char *m = calloc(o->nNodes, 1), *inside = calloc(o->nNodes, 1);
 	for (long node = 0; node < o->nNodes; node++) {
 		int c[3] = {(int)(node % S[0]), (int)((node / o->sy) % S[1]), (int)(node / o->sz)};
-		double r2 = 0;
 		int ghost = 0;
+		long t[3];
 		for (int d = 0; d < 3; d++) {
-			int t = c[d] - 1;
-			if (t < 0 || t >= T[d]) ghost = 1;
-			t = (t + T[d]) % T[d];
-			r2 += (t - sp[d]) * (t - sp[d]);
+			t[d] = c[d] - 1;
+			if (t[d] < 0 || t[d] >= T[d]) ghost = 1;
+			t[d] = (t[d] + T[d]) % T[d];
 		}
-		m[node] = r2 <= sp[3] * sp[3];
+		double v = mk[t[0] + (long)T[0] * (t[1] + (long)T[1] * t[2])];
+		if (v > 1.5) msg(ERROR, "objects: one object per run on the device path (mask value %g)", v);
+		m[node] = v > 0.5;
 		inside[node] = m[node] && !ghost;
 	}
-	free(sp);
+	free(mk);
 	/* surface: true nodes with 1..7 of the 8 nodes at offsets {0,-1}^3 */
 	const long nb[8] = {0, -o->sz, -1, -1 - o->sz, -o->sy, -o->sy - o->sz, -o->sy - 1, -o->sy - 1 - o->sz};
 	o->surfNode = malloc(o->nNodes * sizeof(long));
@@ -134,6 +160,13 @@ PincObj *pinc_obj_create(const dictionary *ini, const Grid *rho) {
 	free(inside);
 	free(dIdx);
 	return o;
+}
+
+PincObj *pinc_obj_create(const dictionary *ini, const Grid *rho) {
+	if (!iniHas(ini, "objects:sphere") && !iniHas(ini, "objects:file")) return NULL;
+	if (rho->rank != 4) msg(ERROR, "objects are 3-D (object.c)");
+	int T[3] = {rho->trueSize[1], rho->trueSize[2], rho->trueSize[3]};
+	return obj_create(ini, T);
 }
 
 void pinc_obj_free(PincObj *o) {
@@ -255,4 +288,43 @@ double pinc_obj_apply(PincObj *o, Grid *rho, const Grid *phi) {
 	pinc_check(pinc_hip_obj_correct(o->dM, o->dPhiS, n, pc, o->dSurf, rho->dev->d, g_pinc.stream), "object correct");
 	rho->dev->ghostsValid = 0;
 	return pc;
+}
+
+/* ---------------------------------------------- the reference's API -- */
+/* object.h:8-21: Object is this build's PincObj (include/pinc.h) */
+
+Object *oAlloc(const dictionary *ini) {
+	if (iniGetInt(ini, "grid:nDims") != 3) msg(ERROR, "objects are 3-D (object.c)");
+	int *ts = iniGetIntArr(ini, "grid:trueSize", 3);
+	int T[3] = {ts[0], ts[1], ts[2]};
+	free(ts);
+	PincObj *o = obj_create(ini, T);
+	if (!o) msg(ERROR, "oAlloc: set objects:sphere or objects:file");
+	return o;
+}
+
+void oFree(Object *obj) { pinc_obj_free(obj); }
+
+/* object.c:163-298: the reference allocates its own solver for the columns */
+void oComputeCapacitanceMatrix(Object *obj, const dictionary *ini, const MpiInfo *mpiInfo) {
+	Grid *rho = gAlloc(ini, SCALAR), *phi = gAlloc(ini, SCALAR);
+	MultigridSolver *S = mgAllocSolver(ini, rho, phi);
+	pinc_obj_capacitance(obj, rho, phi, S, (void (*)(void *, Grid *, Grid *, const MpiInfo *))mgSolve, mpiInfo);
+	mgFreeSolver(S);
+	gFree(rho);
+	gFree(phi);
+}
+
+void oApplyCapacitanceMatrix(Grid *rho, const Grid *phi, const Object *obj, const MpiInfo *mpiInfo) {
+	(void)mpiInfo;
+	pinc_obj_apply((PincObj *)obj, rho, phi);
+}
+
+/* object.c:460-515: the collected charge is added to rhoObj's surface nodes */
+void oCollectObjectCharge(Population *pop, Grid *rhoObj, Object *obj, const MpiInfo *mpiInfo) {
+	(void)mpiInfo;
+	double before = obj->rhoObjVal;
+	pinc_obj_collect(obj, pop, 0);
+	double add = obj->rhoObjVal - before;
+	if (add != 0.0) pinc_check(pinc_hip_obj_add(rhoObj->dev->d, obj->dSurf, obj->nSurf, add, g_pinc.stream), "rhoObj");
 }

@@ -77,3 +77,29 @@ def test_object_steps_match_checker(built, T, sphere, layout):
         assert np.max(np.abs(phi_g - phi_o)) <= 1e-7 * np.abs(phi_o).max()
     # the object is charged: electrons fall in faster than ions
     assert ob.collected(0) != 0.0
+
+
+def test_object_mask_file_equals_sphere(built, tmp_path):
+    """objects:file (the reference's /Object dataset [nz, ny, nx, 1],
+    object.c:727-756) gives the same run as the generated sphere."""
+    from pinc_amd import Sim
+    from pinc_amd._lib import HOST
+    T, sphere = (16, 16, 16), (7.5, 8.2, 8.9, 3.1)
+    mask = np.ascontiguousarray(_sphere(T, sphere[:3], sphere[3])[..., None])
+    f = str(tmp_path / "obj.grid.h5")
+    dims = np.array(mask.shape, dtype=np.int64)
+    assert HOST.pinc_h5_write(f.encode(), b"/Object", 4, dims.ctypes.data, mask.ctypes.data) == 0
+    res = []
+    for key, val in (("sphere", ",".join(map(str, sphere))), ("file", f)):
+        cfg = configs.config("cold3d", true_size=T, nsub=(1, 1, 1))
+        cfg["multigrid"]["mgLevels"] = "3"
+        cfg["population"]["fused"] = "0"
+        cfg["objects"] = {key: val}
+        with Sim(configs.write_ini(cfg)) as s:
+            s.init()
+            s.step(2)
+            res.append((s.count(0), s.count(1), *s.energy()[:2]))
+    # same removals; energies to the run-to-run spread of the atomic deposit
+    assert res[0][:2] == res[1][:2]
+    for a, b in zip(res[0][2:], res[1][2:]):
+        assert abs(a - b) <= 1e-10 * abs(a)
