@@ -100,7 +100,7 @@ def main() -> int:
                     help="c4: warm 3-D plasma, 256^3, 64 ppc, multigrid (BASELINE.json metric, default); "
                          "c3: Maxwellian 128^3, 32 ppc, spectral (rocFFT) Poisson solve; "
                          "c5: c4 plus an immersed sphere (object.c: charge collection, capacitance "
-                         "correction, second solve), one GPU, unfused operators")
+                         "correction, second solve), unfused operators")
     ap.add_argument("--size", type=int, default=None, help="global cells per dimension (c4: 256, c3: 128)")
     ap.add_argument("--ppc", type=int, default=None, help="particles per cell per species (c4: 64, c3: 32)")
     ap.add_argument("--mg", default="native", choices=["native", "reference"],
@@ -162,9 +162,6 @@ def main() -> int:
 
     c3 = args.workload == "c3"
     c5 = args.workload == "c5"
-    if c5:
-        if world > 1:
-            raise SystemExit("c5: the device object path runs on one subdomain")
     if args.size is None:
         args.size = 128 if c3 else 256
     if args.ppc is None:

@@ -63,13 +63,14 @@ __global__ void k_obj_correct(const double *__restrict__ M, const double *__rest
 	const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
 	if (i >= n) return;
 	double c = 0.0;
+	if (idx[i] < 0) return;  // surface node of another rank's slab
 	for (long j = 0; j < n; j++) c += M[n * j + i] * (phiC - phiS[j]);
 	rho[idx[i]] += c;
 }
 
 __global__ void k_obj_add(double *__restrict__ grid, const long *__restrict__ idx, long n, double v) {
 	const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-	if (i < n) grid[idx[i]] += v;
+	if (i < n && idx[i] >= 0) grid[idx[i]] += v;
 }
 
 int check(const char *what) { return pinc::check_launch(what); }

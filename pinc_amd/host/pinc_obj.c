@@ -1,6 +1,8 @@
 /*
  * pinc_obj.c -- immersed objects (object.c, config C5) on the device path,
- * one subdomain (P = 1), unfused operators (either particle layout: with
+ * any number of z-slabs (the solve is replicated, so phi is read from its
+ * global view and the charge corrections go to the owning slab), unfused
+ * operators (either particle layout: with
  * the tiled one the back-filled slots are deposited individually until the
  * next sort, as after a migration).
  *
@@ -34,7 +36,10 @@ void pinc_pop_grow_ws(Population *pop, int s, long n);
 struct PincObj {
 	long nSurf;          /* surface nodes (one object) */
 	long *surfNode;      /* host: padded reference-layout node indices */
-	long *dSurf;         /* device: slab-storage indices of the surface nodes */
+	long *dSurf;         /* device: this rank's slab-storage index of each surface
+	                        node, -1 where another rank owns it */
+	long *dSurfG;        /* device: index of each surface node in the global
+	                        periodic grid the solver works on (phi global view) */
 	unsigned char *dInside; /* device: interior byte per padded node */
 	long nNodes, sy, sz;
 	double *dM;          /* device: inverse response matrix, row-major nSurf^2 */
@@ -105,74 +110,76 @@ static double *read_mask(const dictionary *ini, const int T[3]) {
 	return mk;
 }
 
-static PincObj *obj_create(const dictionary *ini, const int T[3]) {
+static PincObj *obj_create(const dictionary *ini, const pinc_geom_t *g) {
 	if (!iniHas(ini, "objects:sphere") && !iniHas(ini, "objects:file")) return NULL;
-	if (g_pinc.nranks > 1) msg(ERROR, "objects: one subdomain only on the device path");
+	if (g->nd != 3) msg(ERROR, "objects are 3-D (object.c)");
 	PincObj *o = calloc(1, sizeof(*o));
-	int S[3] = {T[0] + 2, T[1] + 2, T[2] + 2};
+	const int T[3] = {g->T[0], g->T[1], g->T[2]};
+	/* this rank's padded nodes: z covers its slab [off, off+nloc) */
+	int S[3] = {T[0] + 2, T[1] + 2, g->nloc + 2};
 	o->sy = S[0];
 	o->sz = (long)S[0] * S[1];
 	o->nNodes = o->sz * S[2];
 	double *mk = read_mask(ini, T);
-	/* node mask with periodic ghosts (the reference halos the object grid);
-	 * one object: every value above 0.5 (object.c:117-121 takes the highest
-	 * id as the count; several objects are next-row work) */
-	unsigned char *m = calloc(o->nNodes, 1), *inside = calloc(o->nNodes, 1);
+	for (long k = 0; k < (long)T[0] * T[1] * T[2]; k++)
+		if (mk[k] > 1.5) msg(ERROR, "objects: one object per run on the device path (mask value %g)", mk[k]);
+#define MK(x, y, z) (mk[((x) + T[0]) % T[0] + (long)T[0] * (((y) + T[1]) % T[1] + (long)T[1] * (((z) + T[2]) % T[2]))] > 0.5)
+	/* interior bytes of the local padded nodes (ghosts excluded, as the
+	 * reference's lookup skips ghost nodes) */
+	unsigned char *inside = calloc(o->nNodes, 1);
 	for (long node = 0; node < o->nNodes; node++) {
 		int c[3] = {(int)(node % S[0]), (int)((node / o->sy) % S[1]), (int)(node / o->sz)};
-		int ghost = 0;
-		long t[3];
-		for (int d = 0; d < 3; d++) {
-			t[d] = c[d] - 1;
-			if (t[d] < 0 || t[d] >= T[d]) ghost = 1;
-			t[d] = (t[d] + T[d]) % T[d];
-		}
-		double v = mk[t[0] + (long)T[0] * (t[1] + (long)T[1] * t[2])];
-		if (v > 1.5) msg(ERROR, "objects: one object per run on the device path (mask value %g)", v);
-		m[node] = v > 0.5;
-		inside[node] = m[node] && !ghost;
+		if (c[0] < 1 || c[0] > T[0] || c[1] < 1 || c[1] > T[1] || c[2] < 1 || c[2] > g->nloc) continue;
+		inside[node] = MK(c[0] - 1, c[1] - 1, g->off + c[2] - 1);
 	}
-	free(mk);
-	/* surface: true nodes with 1..7 of the 8 nodes at offsets {0,-1}^3 */
-	const long nb[8] = {0, -o->sz, -1, -1 - o->sz, -o->sy, -o->sy - o->sz, -o->sy - 1, -o->sy - 1 - o->sz};
-	o->surfNode = malloc(o->nNodes * sizeof(long));
-	long *dIdx = malloc(o->nNodes * sizeof(long));
+	/* surface (object.c:368-458): global true nodes with 1..7 of the 8
+	 * nodes at offsets {0,-1}^3 in the object, in global z,y,x order (for
+	 * z-slabs the reference's rank-then-local order) */
+	long nMax = (long)T[0] * T[1] * T[2];
+	long *dIdx = malloc(nMax * sizeof(long)), *gIdx = malloc(nMax * sizeof(long));
+	o->surfNode = malloc(nMax * sizeof(long));
 	long ps = (long)T[0] * T[1];
-	for (long node = 0; node < o->nNodes; node++) {
-		int c[3] = {(int)(node % S[0]), (int)((node / o->sy) % S[1]), (int)(node / o->sz)};
-		if (c[0] < 1 || c[0] > T[0] || c[1] < 1 || c[1] > T[1] || c[2] < 1 || c[2] > T[2]) continue;
-		int d = 0;
-		for (int q = 0; q < 8; q++) d += m[node + nb[q]];
-		if (d > 0 && d < 8) {
-			o->surfNode[o->nSurf] = node;
-			dIdx[o->nSurf] = (long)c[2] * ps + (long)(c[1] - 1) * T[0] + (c[0] - 1);
-			o->nSurf++;
-		}
-	}
+	for (int z = 0; z < T[2]; z++)
+		for (int y = 0; y < T[1]; y++)
+			for (int x = 0; x < T[0]; x++) {
+				int d = 0;
+				for (int q = 0; q < 8; q++) d += MK(x - (q & 1), y - ((q >> 1) & 1), z - (q >> 2));
+				if (d > 0 && d < 8) {
+					o->surfNode[o->nSurf] = x + (long)T[0] * (y + (long)T[1] * z);
+					gIdx[o->nSurf] = (long)z * ps + (long)y * T[0] + x;
+					int zl = z - g->off;
+					dIdx[o->nSurf] = (zl >= 0 && zl < g->nloc) ? (long)(zl + 1) * ps + (long)y * T[0] + x : -1;
+					o->nSurf++;
+				}
+			}
+#undef MK
+	free(mk);
 	if (!o->nSurf) msg(ERROR, "objects:sphere has no surface nodes");
 	pinc_check(pinc_hip_malloc((void **)&o->dInside, o->nNodes), "objects");
 	pinc_check(pinc_hip_h2d(o->dInside, inside, o->nNodes, g_pinc.stream), "objects");
 	pinc_check(pinc_hip_malloc((void **)&o->dSurf, o->nSurf * sizeof(long)), "objects");
 	pinc_check(pinc_hip_h2d(o->dSurf, dIdx, o->nSurf * sizeof(long), g_pinc.stream), "objects");
+	pinc_check(pinc_hip_malloc((void **)&o->dSurfG, o->nSurf * sizeof(long)), "objects");
+	pinc_check(pinc_hip_h2d(o->dSurfG, gIdx, o->nSurf * sizeof(long), g_pinc.stream), "objects");
 	pinc_check(pinc_hip_malloc((void **)&o->dPhiS, o->nSurf * sizeof(double)), "objects");
 	pinc_check(pinc_hip_stream_sync(g_pinc.stream), "objects");
-	free(m);
 	free(inside);
 	free(dIdx);
+	free(gIdx);
 	return o;
 }
 
 PincObj *pinc_obj_create(const dictionary *ini, const Grid *rho) {
 	if (!iniHas(ini, "objects:sphere") && !iniHas(ini, "objects:file")) return NULL;
 	if (rho->rank != 4) msg(ERROR, "objects are 3-D (object.c)");
-	int T[3] = {rho->trueSize[1], rho->trueSize[2], rho->trueSize[3]};
-	return obj_create(ini, T);
+	return obj_create(ini, &rho->dev->geom);
 }
 
 void pinc_obj_free(PincObj *o) {
 	if (!o) return;
 	pinc_hip_free(o->dInside);
 	pinc_hip_free(o->dSurf);
+	pinc_hip_free(o->dSurfG);
 	pinc_hip_free(o->dPhiS);
 	pinc_hip_free(o->dM);
 	free(o->surfNode);
@@ -195,12 +202,20 @@ void pinc_obj_capacitance(PincObj *o, Grid *rho, Grid *phi, void *solver,
 	pinc_check(pinc_hip_d2d(saveR, rho->dev->d, N * sizeof(double), g_pinc.stream), "cap save");
 	pinc_check(pinc_hip_d2d(saveP, phi->dev->d, N * sizeof(double), g_pinc.stream), "cap save");
 	pinc_check(pinc_hip_memset(phi->dev->d, 0, N * sizeof(double), g_pinc.stream), "cap");
+	/* several ranks: the solver's global phi is a buffer of its own */
+	double *saveG = NULL;
+	long NG = (long)phi->dev->geom.T[0] * phi->dev->geom.T[1] * phi->dev->geom.T[2];
+	if (phi->dev->ownsGlobal) {
+		pinc_check(pinc_hip_malloc((void **)&saveG, NG * sizeof(double)), "cap save");
+		pinc_check(pinc_hip_d2d(saveG, phi->dev->global, NG * sizeof(double), g_pinc.stream), "cap save");
+		pinc_check(pinc_hip_memset(phi->dev->global, 0, NG * sizeof(double), g_pinc.stream), "cap");
+	}
 	double *P = malloc(n * n * sizeof(double)), *col = malloc(n * sizeof(double));
 	for (long i = 0; i < n; i++) {
 		pinc_check(pinc_hip_memset(rho->dev->d, 0, N * sizeof(double), g_pinc.stream), "cap");
 		pinc_check(pinc_hip_obj_add(rho->dev->d, o->dSurf + i, 1, 1.0, g_pinc.stream), "cap unit charge");
 		solve(solver, rho, phi, mpi);
-		pinc_check(pinc_hip_obj_gather(phi->dev->d, o->dSurf, n, o->dPhiS, g_pinc.stream), "cap gather");
+		pinc_check(pinc_hip_obj_gather(phi->dev->global, o->dSurfG, n, o->dPhiS, g_pinc.stream), "cap gather");
 		pinc_check(pinc_hip_d2h(col, o->dPhiS, n * sizeof(double), g_pinc.stream), "cap gather");
 		for (long k = 0; k < n; k++) P[k * n + i] = col[k];
 	}
@@ -218,9 +233,11 @@ void pinc_obj_capacitance(PincObj *o, Grid *rho, Grid *phi, void *solver,
 	pinc_check(pinc_hip_h2d(o->dM, M, n * n * sizeof(double), g_pinc.stream), "cap matrix");
 	pinc_check(pinc_hip_d2d(rho->dev->d, saveR, N * sizeof(double), g_pinc.stream), "cap restore");
 	pinc_check(pinc_hip_d2d(phi->dev->d, saveP, N * sizeof(double), g_pinc.stream), "cap restore");
+	if (saveG) pinc_check(pinc_hip_d2d(phi->dev->global, saveG, NG * sizeof(double), g_pinc.stream), "cap restore");
 	pinc_check(pinc_hip_stream_sync(g_pinc.stream), "cap");
 	pinc_hip_free(saveR);
 	pinc_hip_free(saveP);
+	pinc_hip_free(saveG);
 	free(P);
 	free(M);
 	free(col);
@@ -260,6 +277,14 @@ void pinc_obj_collect(PincObj *o, Population *pop, int discard) {
 		}
 	}
 	dv->flagsValid = 0;
+	if (g_pinc.nranks > 1) {
+		/* the object's charge is global (MPI_Allreduce-free in the
+		 * reference only because one rank owns the object) */
+		double *d = PINC_SLOT(120);
+		pinc_check(pinc_hip_h2d(d, &cnt, sizeof(double), g_pinc.stream), "collect sum");
+		pinc_comm_allreduce_sum(d, 1, "collect sum");
+		pinc_check(pinc_hip_d2h(&cnt, d, sizeof(double), g_pinc.stream), "collect sum");
+	}
 	if (discard) return;
 	/* object.c:508-513: chargeCounter * invNrSurfNod added per surface node */
 	o->collected += cnt;
@@ -277,7 +302,7 @@ void pinc_obj_add_rho(PincObj *o, Grid *rho) {
 double pinc_obj_apply(PincObj *o, Grid *rho, const Grid *phi) {
 	if (!o->haveCap) msg(ERROR, "objects: capacitance matrix not computed");
 	long n = o->nSurf;
-	pinc_check(pinc_hip_obj_gather(phi->dev->d, o->dSurf, n, o->dPhiS, g_pinc.stream), "object gather");
+	pinc_check(pinc_hip_obj_gather(phi->dev->global, o->dSurfG, n, o->dPhiS, g_pinc.stream), "object gather");
 	double *ph = malloc(n * sizeof(double));
 	pinc_check(pinc_hip_d2h(ph, o->dPhiS, n * sizeof(double), g_pinc.stream), "object gather");
 	/* eq. 7 through the row sums of M (summed once at init) */
@@ -294,11 +319,8 @@ double pinc_obj_apply(PincObj *o, Grid *rho, const Grid *phi) {
 /* object.h:8-21: Object is this build's PincObj (include/pinc.h) */
 
 Object *oAlloc(const dictionary *ini) {
-	if (iniGetInt(ini, "grid:nDims") != 3) msg(ERROR, "objects are 3-D (object.c)");
-	int *ts = iniGetIntArr(ini, "grid:trueSize", 3);
-	int T[3] = {ts[0], ts[1], ts[2]};
-	free(ts);
-	PincObj *o = obj_create(ini, T);
+	pinc_geom_t g = pinc_geom_current();
+	PincObj *o = obj_create(ini, &g);
 	if (!o) msg(ERROR, "oAlloc: set objects:sphere or objects:file");
 	return o;
 }

@@ -103,3 +103,50 @@ def test_object_mask_file_equals_sphere(built, tmp_path):
     assert res[0][:2] == res[1][:2]
     for a, b in zip(res[0][2:], res[1][2:]):
         assert abs(a - b) <= 1e-10 * abs(a)
+
+
+def test_object_two_slabs_match_one(built, tmp_path):
+    """Two z-slabs (host transport, one GPU): the object's lookups are
+    global, phi is read from the replicated solve's global view, charge
+    corrections land in the owning slab and the collected charge is summed
+    over the ranks; counts and energies match a one-rank run."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+    from pathlib import Path
+    from pinc_amd import Sim
+    root = Path(__file__).resolve().parent.parent
+    sphere = "8.2,7.7,8.4,3.3"   # straddles the slab boundary at z = 8
+    steps = 3
+
+    def cfg(nsub, T):
+        c = configs.config("cold3d", true_size=T, nsub=nsub)
+        c["multigrid"]["mgLevels"] = "3"
+        c["population"]["fused"] = "0"
+        c["objects"] = {"sphere": sphere}
+        return configs.write_ini(c)
+
+    one = {"energy": [], "counts": []}
+    with Sim(cfg((1, 1, 1), (16, 16, 16))) as s:
+        s.init()
+        for _ in range(steps):
+            s.step()
+            ke, pe, _ = s.energy()
+            one["energy"].append([ke, pe])
+            one["counts"].append([s.count(0), s.count(1)])
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    out = tmp_path / "two.json"
+    env = dict(os.environ, PYTHONPATH=str(root))
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                        "--master-addr=127.0.0.1", f"--master-port={port}", str(root / "tests" / "obj_worker.py"),
+                        "--ini", cfg((1, 1, 2), (16, 16, 8)), "--out", str(out), "--steps", str(steps)],
+                       env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    two = json.loads(out.read_text())
+    assert two["counts"] == one["counts"]
+    for a, b in zip(one["energy"], two["energy"]):
+        assert abs(a[0] - b[0]) <= 1e-7 * abs(a[0]) and abs(a[1] - b[1]) <= 1e-7 * abs(a[1]), (a, b)
