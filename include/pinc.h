@@ -24,7 +24,7 @@ extern "C" {
 /* ------------------------------------------------------- core.h types -- */
 typedef void (*funPtr)();
 typedef struct dictionary dictionary;  /* iniparser-compatible dictionary */
-typedef struct PincObj Object;        /* immersed objects (object.h:8-21), one subdomain */
+typedef struct PincObj Object;        /* immersed objects (object.h:8-21) */
 
 typedef enum { STATUS = 0x00, WARNING = 0x01, ERROR = 0x02, TIMER = 0x03, ALL = 0x10 } msgKind;
 typedef enum { PERIODIC = 0x01, DIRICHLET = 0x02, NEUMANN = 0x03, NONE = 0x10 } bndType;
@@ -209,7 +209,7 @@ long sSolveCount(const SpectralSolver *solver);
 /* ------------------------------------------------ immersed objects -- */
 /* object.c on the device (pinc_obj.c): one object
  * from objects:sphere = cx,cy,cz,r or objects:file (an .h5 with /Object
- * [nz,ny,nx,1]); one subdomain; population:fused = 0 */
+ * [nz,ny,nx,1]); one object; population:fused = 0 */
 Object *oAlloc(const dictionary *ini);
 void oFree(Object *obj);
 void oComputeCapacitanceMatrix(Object *obj, const dictionary *ini, const MpiInfo *mpiInfo);
