@@ -207,9 +207,9 @@ void sSolve(SpectralSolver *solver, Grid *rho, Grid *phi, const MpiInfo *mpiInfo
 long sSolveCount(const SpectralSolver *solver);
 
 /* ------------------------------------------------ immersed objects -- */
-/* object.c on the device (pinc_obj.c): one object
+/* object.c on the device (pinc_obj.c): objects
  * from objects:sphere = cx,cy,cz,r or objects:file (an .h5 with /Object
- * [nz,ny,nx,1]); one object; population:fused = 0 */
+ * [nz,ny,nx,1], values 1..K); population:fused = 0 */
 Object *oAlloc(const dictionary *ini);
 void oFree(Object *obj);
 void oComputeCapacitanceMatrix(Object *obj, const dictionary *ini, const MpiInfo *mpiInfo);

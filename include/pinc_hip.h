@@ -201,13 +201,14 @@ int pinc_hip_extract(pinc_pop_t pop, int s, const unsigned char *flags, int *chu
 
 /* immersed objects (k_objects.hip; object.c, config C5).  inside: one byte
  * per node of the padded reference layout (strides 1, sy, sz; nNodes
- * nodes), 1 for interior nodes of an object.  obj_flag writes flags/chunk
- * counts in pinc_hip_extract's format (flag 0 = remove, 13 = keep) for
- * oCollectObjectCharge (object.c:460-515).  idx: device indices of the
+ * nodes), the object id of interior nodes (0: none).  obj_flag writes
+ * flags/chunk counts in pinc_hip_extract's format (flag 0 = remove, 13 =
+ * keep) for oCollectObjectCharge (object.c:460-515) and adds the flagged
+ * particles per object to objCount[id-1].  idx: device indices of the
  * surface nodes in a grid's slab storage.  obj_correct adds
  * sum_j M[j*n+i] (phiC - phiS[j]) to rho[idx[i]] (object.c:349-362). */
 int pinc_hip_obj_flag(pinc_pop_t pop, int s, const unsigned char *inside, long sy, long sz, long nNodes,
-                      unsigned char *flags, int *chunkCount, void *stream);
+                      unsigned char *flags, int *chunkCount, int *objCount, void *stream);
 int pinc_hip_obj_gather(const double *grid, const long *idx, long n, double *out, void *stream);
 int pinc_hip_obj_correct(const double *M, const double *phiS, long n, double phiC, const long *idx, double *rho,
                          void *stream);

@@ -28,7 +28,8 @@ __global__ __launch_bounds__(kObjThreads) void k_obj_flag(const double *__restri
                                                           const unsigned char *__restrict__ inside, long sy,
                                                           long sz, long nNodes, int center,
                                                           unsigned char *__restrict__ flags,
-                                                          int *__restrict__ chunkCount) {
+                                                          int *__restrict__ chunkCount,
+                                                          int *__restrict__ objCount) {
 	__shared__ int wcnt[kObjThreads / 64];
 	const long base = (long)blockIdx.x * PINC_CHUNK;
 	int cnt = 0;
@@ -37,9 +38,10 @@ __global__ __launch_bounds__(kObjThreads) void k_obj_flag(const double *__restri
 		if (i >= n) break;
 		// object.c:489-494: p = j + k*sizeProd[2] + l*sizeProd[3]
 		const long node = (long)(int)x0[i] + (long)(int)x1[i] * sy + (long)(int)x2[i] * sz;
-		const bool in = node >= 0 && node < nNodes && inside[node];
-		flags[i] = (unsigned char)(in ? 0 : center);
-		cnt += in;
+		const int id = (node >= 0 && node < nNodes) ? inside[node] : 0;
+		flags[i] = (unsigned char)(id ? 0 : center);
+		cnt += id != 0;
+		if (id) atomicAdd(&objCount[id - 1], 1);  // rare: particles entering an object
 	}
 	int wsum = cnt;
 	for (int o = 32; o > 0; o >>= 1) wsum += __shfl_xor(wsum, o);
@@ -78,7 +80,7 @@ int check(const char *what) { return pinc::check_launch(what); }
 }  // namespace
 
 extern "C" int pinc_hip_obj_flag(pinc_pop_t pop, int s, const unsigned char *inside, long sy, long sz, long nNodes,
-                                 unsigned char *flags, int *chunkCount, void *stream) {
+                                 unsigned char *flags, int *chunkCount, int *objCount, void *stream) {
 	const long n = pop.iStop[s] - pop.iStart[s];
 	if (n <= 0) return 0;
 	if (pop.nd != 3) return pinc::set_error(hipErrorInvalidValue, "objects are 3-D (object.c)");
@@ -86,7 +88,7 @@ extern "C" int pinc_hip_obj_flag(pinc_pop_t pop, int s, const unsigned char *ins
 	int center = 13;
 	hipLaunchKernelGGL(k_obj_flag, dim3((unsigned)((n + PINC_CHUNK - 1) / PINC_CHUNK)), dim3(kObjThreads), 0,
 	                   (hipStream_t)stream, pop.x[0] + b0, pop.x[1] + b0, pop.x[2] + b0, n, inside, sy, sz, nNodes,
-	                   center, flags + b0, chunkCount);
+	                   center, flags + b0, chunkCount, objCount);
 	return check("obj flag");
 }
 

@@ -34,20 +34,24 @@
 void pinc_pop_grow_ws(Population *pop, int s, long n);
 
 struct PincObj {
-	long nSurf;          /* surface nodes (one object) */
-	long *surfNode;      /* host: padded reference-layout node indices */
+	int nObj;            /* objects: mask values 1..nObj */
+	long nSurf;          /* surface nodes of all objects, grouped by object */
+	long *surfOff;       /* nObj+1: object a owns surface entries [surfOff[a], surfOff[a+1]) */
+	long *surfNode;      /* host: global node index x + T0*(y + T1*z) */
 	long *dSurf;         /* device: this rank's slab-storage index of each surface
 	                        node, -1 where another rank owns it */
 	long *dSurfG;        /* device: index of each surface node in the global
 	                        periodic grid the solver works on (phi global view) */
-	unsigned char *dInside; /* device: interior byte per padded node */
+	unsigned char *dInside; /* device: object id per local padded node (0: none) */
+	int *dCount;         /* device: particles flagged per object (one species) */
 	long nNodes, sy, sz;
-	double *dM;          /* device: inverse response matrix, row-major nSurf^2 */
-	double *wRow;        /* host: sum_i M[j][i] per j (eq. 7) */
-	double capSum;       /* 1 / sum M */
+	double *dM;          /* device: per object the inverse response matrix, row-major */
+	long *capOff;        /* nObj+1 offsets into dM */
+	double *wRow;        /* host: sum_i M[j][i] per surface entry j (eq. 7) */
+	double *capSum;      /* per object: 1 / sum M */
 	double *dPhiS;       /* device: phi at the surface nodes */
-	double rhoObjVal;    /* rhoObj at every surface node (accumulated) */
-	double collected;
+	double *rhoObjVal;   /* per object: rhoObj at each of its surface nodes */
+	double *collected;   /* per object */
 	int haveCap;
 };
 
@@ -121,29 +125,37 @@ static PincObj *obj_create(const dictionary *ini, const pinc_geom_t *g) {
 	o->sz = (long)S[0] * S[1];
 	o->nNodes = o->sz * S[2];
 	double *mk = read_mask(ini, T);
+	/* object ids (oFillLookupTables, object.c:117-121: the highest value is
+	 * the object count) */
+	int nObj = 0;
 	for (long k = 0; k < (long)T[0] * T[1] * T[2]; k++)
-		if (mk[k] > 1.5) msg(ERROR, "objects: one object per run on the device path (mask value %g)", mk[k]);
-#define MK(x, y, z) (mk[((x) + T[0]) % T[0] + (long)T[0] * (((y) + T[1]) % T[1] + (long)T[1] * (((z) + T[2]) % T[2]))] > 0.5)
+		if (mk[k] > nObj) nObj = (int)(mk[k] + 0.5);
+	if (nObj > 255) msg(ERROR, "objects: at most 255 objects");
+	o->nObj = nObj;
+#define ID(x, y, z) ((int)(mk[((x) + T[0]) % T[0] + (long)T[0] * (((y) + T[1]) % T[1] + (long)T[1] * (((z) + T[2]) % T[2]))] + 0.5))
 	/* interior bytes of the local padded nodes (ghosts excluded, as the
 	 * reference's lookup skips ghost nodes) */
 	unsigned char *inside = calloc(o->nNodes, 1);
 	for (long node = 0; node < o->nNodes; node++) {
 		int c[3] = {(int)(node % S[0]), (int)((node / o->sy) % S[1]), (int)(node / o->sz)};
 		if (c[0] < 1 || c[0] > T[0] || c[1] < 1 || c[1] > T[1] || c[2] < 1 || c[2] > g->nloc) continue;
-		inside[node] = MK(c[0] - 1, c[1] - 1, g->off + c[2] - 1);
+		int id = ID(c[0] - 1, c[1] - 1, g->off + c[2] - 1);
+		inside[node] = (unsigned char)(id > 0 ? id : 0);
 	}
 	/* surface (object.c:368-458): global true nodes with 1..7 of the 8
 	 * nodes at offsets {0,-1}^3 in the object, in global z,y,x order (for
 	 * z-slabs the reference's rank-then-local order) */
-	long nMax = (long)T[0] * T[1] * T[2];
+	long nMax = (long)T[0] * T[1] * T[2] * (nObj > 0 ? nObj : 1);
 	long *dIdx = malloc(nMax * sizeof(long)), *gIdx = malloc(nMax * sizeof(long));
 	o->surfNode = malloc(nMax * sizeof(long));
+	o->surfOff = calloc(nObj + 1, sizeof(long));
 	long ps = (long)T[0] * T[1];
+	for (int a = 1; a <= nObj; a++) {
 	for (int z = 0; z < T[2]; z++)
 		for (int y = 0; y < T[1]; y++)
 			for (int x = 0; x < T[0]; x++) {
 				int d = 0;
-				for (int q = 0; q < 8; q++) d += MK(x - (q & 1), y - ((q >> 1) & 1), z - (q >> 2));
+				for (int q = 0; q < 8; q++) d += ID(x - (q & 1), y - ((q >> 1) & 1), z - (q >> 2)) == a;
 				if (d > 0 && d < 8) {
 					o->surfNode[o->nSurf] = x + (long)T[0] * (y + (long)T[1] * z);
 					gIdx[o->nSurf] = (long)z * ps + (long)y * T[0] + x;
@@ -152,9 +164,11 @@ static PincObj *obj_create(const dictionary *ini, const pinc_geom_t *g) {
 					o->nSurf++;
 				}
 			}
-#undef MK
+		o->surfOff[a] = o->nSurf;
+	}
+#undef ID
 	free(mk);
-	if (!o->nSurf) msg(ERROR, "objects:sphere has no surface nodes");
+	if (!o->nSurf) msg(ERROR, "objects: the mask has no surface nodes");
 	pinc_check(pinc_hip_malloc((void **)&o->dInside, o->nNodes), "objects");
 	pinc_check(pinc_hip_h2d(o->dInside, inside, o->nNodes, g_pinc.stream), "objects");
 	pinc_check(pinc_hip_malloc((void **)&o->dSurf, o->nSurf * sizeof(long)), "objects");
@@ -162,6 +176,13 @@ static PincObj *obj_create(const dictionary *ini, const pinc_geom_t *g) {
 	pinc_check(pinc_hip_malloc((void **)&o->dSurfG, o->nSurf * sizeof(long)), "objects");
 	pinc_check(pinc_hip_h2d(o->dSurfG, gIdx, o->nSurf * sizeof(long), g_pinc.stream), "objects");
 	pinc_check(pinc_hip_malloc((void **)&o->dPhiS, o->nSurf * sizeof(double)), "objects");
+	pinc_check(pinc_hip_malloc((void **)&o->dCount, (nObj + 1) * sizeof(int)), "objects");
+	o->capOff = calloc(nObj + 1, sizeof(long));
+	o->capSum = calloc(nObj + 1, sizeof(double));
+	o->rhoObjVal = calloc(nObj + 1, sizeof(double));
+	o->collected = calloc(nObj + 1, sizeof(double));
+	for (int a = 0; a < nObj; a++)
+		if (o->surfOff[a + 1] == o->surfOff[a]) msg(ERROR, "object %d has no surface nodes", a + 1);
 	pinc_check(pinc_hip_stream_sync(g_pinc.stream), "objects");
 	free(inside);
 	free(dIdx);
@@ -182,13 +203,23 @@ void pinc_obj_free(PincObj *o) {
 	pinc_hip_free(o->dSurfG);
 	pinc_hip_free(o->dPhiS);
 	pinc_hip_free(o->dM);
+	pinc_hip_free(o->dCount);
 	free(o->surfNode);
+	free(o->surfOff);
+	free(o->capOff);
+	free(o->capSum);
+	free(o->rhoObjVal);
+	free(o->collected);
 	free(o->wRow);
 	free(o);
 }
 
 long pinc_obj_nsurface(const PincObj *o) { return o ? o->nSurf : 0; }
-double pinc_obj_collected(const PincObj *o) { return o ? o->collected : 0.0; }
+double pinc_obj_collected(const PincObj *o) {
+	double t = 0;
+	for (int a = 0; o && a < o->nObj; a++) t += o->collected[a];
+	return t;
+}
 
 /* object.c:163-298: column i = phi at the surface nodes for a unit charge
  * at surface node i (solver warm-started column to column, as the
@@ -210,27 +241,38 @@ void pinc_obj_capacitance(PincObj *o, Grid *rho, Grid *phi, void *solver,
 		pinc_check(pinc_hip_d2d(saveG, phi->dev->global, NG * sizeof(double), g_pinc.stream), "cap save");
 		pinc_check(pinc_hip_memset(phi->dev->global, 0, NG * sizeof(double), g_pinc.stream), "cap");
 	}
-	double *P = malloc(n * n * sizeof(double)), *col = malloc(n * sizeof(double));
-	for (long i = 0; i < n; i++) {
-		pinc_check(pinc_hip_memset(rho->dev->d, 0, N * sizeof(double), g_pinc.stream), "cap");
-		pinc_check(pinc_hip_obj_add(rho->dev->d, o->dSurf + i, 1, 1.0, g_pinc.stream), "cap unit charge");
-		solve(solver, rho, phi, mpi);
-		pinc_check(pinc_hip_obj_gather(phi->dev->global, o->dSurfG, n, o->dPhiS, g_pinc.stream), "cap gather");
-		pinc_check(pinc_hip_d2h(col, o->dPhiS, n * sizeof(double), g_pinc.stream), "cap gather");
-		for (long k = 0; k < n; k++) P[k * n + i] = col[k];
+	double *col = malloc(n * sizeof(double));
+	for (int a = 0; a < o->nObj; a++) {
+		long na = o->surfOff[a + 1] - o->surfOff[a];
+		o->capOff[a + 1] = o->capOff[a] + na * na;
 	}
-	double *M = malloc(n * n * sizeof(double));
-	invert(P, M, n);
-	double s = 0;
+	pinc_check(pinc_hip_malloc((void **)&o->dM, o->capOff[o->nObj] * sizeof(double)), "cap matrix");
 	o->wRow = calloc(n, sizeof(double));
-	for (long j = 0; j < n; j++)
-		for (long i = 0; i < n; i++) {
-			s += M[j * n + i];
-			o->wRow[j] += M[j * n + i];
+	for (int a = 0; a < o->nObj; a++) {
+		long s0 = o->surfOff[a], na = o->surfOff[a + 1] - s0;
+		double *P = malloc(na * na * sizeof(double)), *M = malloc(na * na * sizeof(double));
+		for (long i = 0; i < na; i++) {
+			pinc_check(pinc_hip_memset(rho->dev->d, 0, N * sizeof(double), g_pinc.stream), "cap");
+			pinc_check(pinc_hip_obj_add(rho->dev->d, o->dSurf + s0 + i, 1, 1.0, g_pinc.stream), "cap unit charge");
+			solve(solver, rho, phi, mpi);
+			pinc_check(pinc_hip_obj_gather(phi->dev->global, o->dSurfG + s0, na, o->dPhiS, g_pinc.stream),
+			           "cap gather");
+			pinc_check(pinc_hip_d2h(col, o->dPhiS, na * sizeof(double), g_pinc.stream), "cap gather");
+			for (long k = 0; k < na; k++) P[k * na + i] = col[k];
 		}
-	o->capSum = 1.0 / s;
-	pinc_check(pinc_hip_malloc((void **)&o->dM, n * n * sizeof(double)), "cap matrix");
-	pinc_check(pinc_hip_h2d(o->dM, M, n * n * sizeof(double), g_pinc.stream), "cap matrix");
+		invert(P, M, na);
+		double sum = 0;
+		for (long j = 0; j < na; j++)
+			for (long i = 0; i < na; i++) {
+				sum += M[j * na + i];
+				o->wRow[s0 + j] += M[j * na + i];
+			}
+		o->capSum[a] = 1.0 / sum;
+		pinc_check(pinc_hip_h2d(o->dM + o->capOff[a], M, na * na * sizeof(double), g_pinc.stream), "cap matrix");
+		pinc_check(pinc_hip_stream_sync(g_pinc.stream), "cap matrix");
+		free(P);
+		free(M);
+	}
 	pinc_check(pinc_hip_d2d(rho->dev->d, saveR, N * sizeof(double), g_pinc.stream), "cap restore");
 	pinc_check(pinc_hip_d2d(phi->dev->d, saveP, N * sizeof(double), g_pinc.stream), "cap restore");
 	if (saveG) pinc_check(pinc_hip_d2d(phi->dev->global, saveG, NG * sizeof(double), g_pinc.stream), "cap restore");
@@ -238,8 +280,6 @@ void pinc_obj_capacitance(PincObj *o, Grid *rho, Grid *phi, void *solver,
 	pinc_hip_free(saveR);
 	pinc_hip_free(saveP);
 	pinc_hip_free(saveG);
-	free(P);
-	free(M);
 	free(col);
 	rho->dev->ghostsValid = phi->dev->ghostsValid = 0;
 	o->haveCap = 1;
@@ -251,17 +291,18 @@ void pinc_obj_capacitance(PincObj *o, Grid *rho, Grid *phi, void *solver,
 void pinc_obj_collect(PincObj *o, Population *pop, int discard) {
 	PincDevPop *dv = pop->dev;
 	if (dv->fused) msg(ERROR, "objects need population:fused=0 (collection runs between migrate and deposit)");
-	double cnt = 0;
+	int K = o->nObj;
+	double *cnt = calloc(K + 1, sizeof(double));
+	int *hc = calloc(K + 1, sizeof(int));
 	for (int s = 0; s < pop->nSpecies; s++) {
 		long n = pop->iStop[s] - pop->iStart[s];
 		if (n <= 0) continue;
-		long nb = (n + PINC_CHUNK - 1) / PINC_CHUNK;
 		for (int attempt = 0;; attempt++) {
 			pinc_pop_t p = pinc_devpop(pop);
+			pinc_check(pinc_hip_memset(o->dCount, 0, (K + 1) * sizeof(int), g_pinc.stream), "object count");
 			pinc_check(pinc_hip_obj_flag(p, s, o->dInside, o->sy, o->sz, o->nNodes, dv->flags,
-			                             dv->chunkCount + dv->chunkBase[s], g_pinc.stream),
+			                             dv->chunkCount + dv->chunkBase[s], o->dCount, g_pinc.stream),
 			           "object flag");
-			(void)nb;
 			long nRem = 0;
 			long neCount[PINC_NNE];
 			int rc = pinc_hip_extract(p, s, dv->flags, dv->chunkCount + dv->chunkBase[s], 13, PINC_NNE, dv->ws[s],
@@ -271,46 +312,63 @@ void pinc_obj_collect(PincObj *o, Population *pop, int discard) {
 				continue;
 			}
 			pinc_check(rc, "object collect");
+			pinc_check(pinc_hip_d2h(hc, o->dCount, K * sizeof(int), g_pinc.stream), "object count");
 			pop->iStop[s] -= nRem;
-			cnt += pop->charge[s] * (double)nRem;
+			/* chargeCounter[a] += charge[s] per particle (object.c:497) */
+			for (int a = 0; a < K; a++) cnt[a] += pop->charge[s] * (double)hc[a];
 			break;
 		}
 	}
 	dv->flagsValid = 0;
-	if (g_pinc.nranks > 1) {
-		/* the object's charge is global (MPI_Allreduce-free in the
-		 * reference only because one rank owns the object) */
+	if (g_pinc.nranks > 1 && K > 0) {
+		/* every rank collects in its slab; the object's charge is global */
 		double *d = PINC_SLOT(120);
-		pinc_check(pinc_hip_h2d(d, &cnt, sizeof(double), g_pinc.stream), "collect sum");
-		pinc_comm_allreduce_sum(d, 1, "collect sum");
-		pinc_check(pinc_hip_d2h(&cnt, d, sizeof(double), g_pinc.stream), "collect sum");
+		if (K > 64) msg(ERROR, "objects: at most 64 objects with several ranks");
+		pinc_check(pinc_hip_h2d(d, cnt, K * sizeof(double), g_pinc.stream), "collect sum");
+		pinc_comm_allreduce_sum(d, K, "collect sum");
+		pinc_check(pinc_hip_d2h(cnt, d, K * sizeof(double), g_pinc.stream), "collect sum");
 	}
-	if (discard) return;
-	/* object.c:508-513: chargeCounter * invNrSurfNod added per surface node */
-	o->collected += cnt;
-	o->rhoObjVal += cnt * (1.0 / (double)o->nSurf);
+	if (!discard)
+		/* object.c:508-513: chargeCounter * invNrSurfNod added per surface node */
+		for (int a = 0; a < K; a++) {
+			o->collected[a] += cnt[a];
+			o->rhoObjVal[a] += cnt[a] * (1.0 / (double)(o->surfOff[a + 1] - o->surfOff[a]));
+		}
+	free(cnt);
+	free(hc);
 }
 
 /* gAddTo(rho, rhoObj) (main.c:230): rhoObj is rhoObjVal at every surface
  * node and zero elsewhere */
 void pinc_obj_add_rho(PincObj *o, Grid *rho) {
-	if (o->rhoObjVal != 0.0)
-		pinc_check(pinc_hip_obj_add(rho->dev->d, o->dSurf, o->nSurf, o->rhoObjVal, g_pinc.stream), "rho += rhoObj");
+	for (int a = 0; a < o->nObj; a++)
+		if (o->rhoObjVal[a] != 0.0)
+			pinc_check(pinc_hip_obj_add(rho->dev->d, o->dSurf + o->surfOff[a], o->surfOff[a + 1] - o->surfOff[a],
+			                            o->rhoObjVal[a], g_pinc.stream),
+			           "rho += rhoObj");
 }
 
 /* object.c:301-366; returns phi_c */
 double pinc_obj_apply(PincObj *o, Grid *rho, const Grid *phi) {
 	if (!o->haveCap) msg(ERROR, "objects: capacitance matrix not computed");
 	long n = o->nSurf;
+	/* phi at every object's surface first: the corrections do not change
+	 * phi until the next solve (object.c:313-363 loops the objects) */
 	pinc_check(pinc_hip_obj_gather(phi->dev->global, o->dSurfG, n, o->dPhiS, g_pinc.stream), "object gather");
 	double *ph = malloc(n * sizeof(double));
 	pinc_check(pinc_hip_d2h(ph, o->dPhiS, n * sizeof(double), g_pinc.stream), "object gather");
-	/* eq. 7 through the row sums of M (summed once at init) */
 	double pc = 0;
-	for (long j = 0; j < n; j++) pc += o->wRow[j] * ph[j];
-	pc *= o->capSum;
+	for (int a = 0; a < o->nObj; a++) {
+		long s0 = o->surfOff[a], na = o->surfOff[a + 1] - s0;
+		/* eq. 7 through the row sums of M (summed once at init) */
+		pc = 0;
+		for (long j = 0; j < na; j++) pc += o->wRow[s0 + j] * ph[s0 + j];
+		pc *= o->capSum[a];
+		pinc_check(pinc_hip_obj_correct(o->dM + o->capOff[a], o->dPhiS + s0, na, pc, o->dSurf + s0, rho->dev->d,
+		                                g_pinc.stream),
+		           "object correct");
+	}
 	free(ph);
-	pinc_check(pinc_hip_obj_correct(o->dM, o->dPhiS, n, pc, o->dSurf, rho->dev->d, g_pinc.stream), "object correct");
 	rho->dev->ghostsValid = 0;
 	return pc;
 }
@@ -345,8 +403,14 @@ void oApplyCapacitanceMatrix(Grid *rho, const Grid *phi, const Object *obj, cons
 /* object.c:460-515: the collected charge is added to rhoObj's surface nodes */
 void oCollectObjectCharge(Population *pop, Grid *rhoObj, Object *obj, const MpiInfo *mpiInfo) {
 	(void)mpiInfo;
-	double before = obj->rhoObjVal;
+	double before[256];
+	for (int a = 0; a < obj->nObj; a++) before[a] = obj->rhoObjVal[a];
 	pinc_obj_collect(obj, pop, 0);
-	double add = obj->rhoObjVal - before;
-	if (add != 0.0) pinc_check(pinc_hip_obj_add(rhoObj->dev->d, obj->dSurf, obj->nSurf, add, g_pinc.stream), "rhoObj");
+	for (int a = 0; a < obj->nObj; a++) {
+		double add = obj->rhoObjVal[a] - before[a];
+		if (add != 0.0)
+			pinc_check(pinc_hip_obj_add(rhoObj->dev->d, obj->dSurf + obj->surfOff[a],
+			                            obj->surfOff[a + 1] - obj->surfOff[a], add, g_pinc.stream),
+			           "rhoObj");
+	}
 }

@@ -150,3 +150,45 @@ def test_object_two_slabs_match_one(built, tmp_path):
     assert two["counts"] == one["counts"]
     for a, b in zip(one["energy"], two["energy"]):
         assert abs(a[0] - b[0]) <= 1e-7 * abs(a[0]) and abs(a[1] - b[1]) <= 1e-7 * abs(a[1]), (a, b)
+
+
+def test_two_objects_match_checker(built, tmp_path):
+    """Two objects (mask values 1 and 2, from an objects:file mask): one
+    capacitance matrix each, per-object charge collection and correction,
+    against the checker's multi-object restatement."""
+    from pinc_amd import Sim
+    from pinc_amd._lib import HOST
+    T = (32, 16, 16)
+    mask = _sphere(T, (8.2, 7.9, 8.1), 2.6) + 2 * _sphere(T, (23.4, 8.3, 7.6), 3.1)
+    assert mask.max() == 2
+    f = str(tmp_path / "two.grid.h5")
+    m4 = np.ascontiguousarray(mask[..., None])
+    dims = np.array(m4.shape, dtype=np.int64)
+    assert HOST.pinc_h5_write(f.encode(), b"/Object", 4, dims.ctypes.data, m4.ctypes.data) == 0
+    cfg = configs.config("cold3d", true_size=T, nsub=(1, 1, 1))
+    cfg["multigrid"]["mgLevels"] = "3"
+    cfg["population"]["fused"] = "0"
+    cfg["objects"] = {"file": f}
+    ini = configs.write_ini(cfg)
+    w = orc.World(ini)
+    w.init()
+    ob = orc.Objects(w, mask)
+    assert ob.n == 2
+    ob.capacitance()
+    ob.init_collect()
+    w.init_fields()
+    with Sim(ini) as s:
+        s.init()
+        for k in range(3):
+            ob.step()
+            s.step()
+            ke_o, pe_o = w.energy()
+            ke, pe, _ = s.energy()
+            for sp in range(2):
+                assert s.count(sp) == w.count(sp), (k, sp)
+            assert abs(ke - ke_o) <= 1e-7 * abs(ke_o), (k, ke, ke_o)
+            assert abs(pe - pe_o) <= 1e-7 * abs(pe_o), (k, pe, pe_o)
+        phi_g = s.grid(1)[1:-1, 1:-1, 1:-1]
+        phi_o = w.grid(1)[1:-1, 1:-1, 1:-1]
+        assert np.max(np.abs(phi_g - phi_o)) <= 1e-7 * np.abs(phi_o).max()
+    assert ob.collected(0) != 0.0 and ob.collected(1) != 0.0
