@@ -110,6 +110,9 @@ def main() -> int:
     ap.add_argument("--layout", default="tiled", choices=["tiled", "reference"],
                     help="tiled: particles re-sorted by 4^3-cell tile every --sort-interval moves (default); "
                          "reference: the reference's particle order (bit-exact indices)")
+    ap.add_argument("--obj-capacitance", default="solve", choices=["solve", "green"],
+                    help="c5: capacitance matrix by one solve per surface node (the reference's, default) or "
+                         "by translating one periodic response (objects:capacitance = green)")
     ap.add_argument("--sort-interval", type=int, default=8)
     ap.add_argument("--sort-fraction", type=float, default=0.0,
                     help="> 0: sort each species once this fraction of its particles left their cell since its "
@@ -176,7 +179,7 @@ def main() -> int:
     if c5:
         # a generated sphere (the reference's bepiColombo object file is not
         # available): centre of the grid, radius S/32
-        cfg["objects"] = {"sphere": f"{S / 2},{S / 2},{S / 2},{S / 32}"}
+        cfg["objects"] = {"sphere": f"{S / 2},{S / 2},{S / 2},{S / 32}", "capacitance": args.obj_capacitance}
         cfg["population"]["fused"] = "0"
     if args.layout == "tiled":
         cfg["population"]["layout"] = "tiled"

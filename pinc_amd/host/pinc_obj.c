@@ -53,6 +53,8 @@ struct PincObj {
 	double *rhoObjVal;   /* per object: rhoObj at each of its surface nodes */
 	double *collected;   /* per object */
 	int haveCap;
+	int green;           /* objects:capacitance = green: columns by translation */
+	int T[3];
 };
 
 static void invert(double *A, double *inv, long n) {
@@ -132,6 +134,13 @@ static PincObj *obj_create(const dictionary *ini, const pinc_geom_t *g) {
 		if (mk[k] > nObj) nObj = (int)(mk[k] + 0.5);
 	if (nObj > 255) msg(ERROR, "objects: at most 255 objects");
 	o->nObj = nObj;
+	for (int d = 0; d < 3; d++) o->T[d] = T[d];
+	if (iniHas(ini, "objects:capacitance")) {
+		char *c = iniGetStr(ini, "objects:capacitance");
+		if (!strcmp(c, "green")) o->green = 1;
+		else if (strcmp(c, "solve")) msg(ERROR, "objects:capacitance=%s (solve or green)", c);
+		free(c);
+	}
 #define ID(x, y, z) ((int)(mk[((x) + T[0]) % T[0] + (long)T[0] * (((y) + T[1]) % T[1] + (long)T[1] * (((z) + T[2]) % T[2]))] + 0.5))
 	/* interior bytes of the local padded nodes (ghosts excluded, as the
 	 * reference's lookup skips ghost nodes) */
@@ -248,10 +257,39 @@ void pinc_obj_capacitance(PincObj *o, Grid *rho, Grid *phi, void *solver,
 	}
 	pinc_check(pinc_hip_malloc((void **)&o->dM, o->capOff[o->nObj] * sizeof(double)), "cap matrix");
 	o->wRow = calloc(n, sizeof(double));
+	/* objects:capacitance = green (extension): the periodic, neutralised
+	 * problem is translation invariant, so the response at node k to a unit
+	 * charge at node i is G(r_k - r_i) for the response G to a unit charge
+	 * at the origin: one solve instead of one per surface node.  Equal to
+	 * the reference's columns to the solver tolerance. */
+	double *G = NULL;
+	const long TX = o->T[0], TY = o->T[1], TZ = o->T[2];
+	if (o->green) {
+		long NG = TX * TY * TZ;
+		G = malloc(NG * sizeof(double));
+		pinc_check(pinc_hip_memset(rho->dev->d, 0, N * sizeof(double), g_pinc.stream), "cap");
+		if (phi->dev->geom.off == 0) {
+			long i0 = rho->dev->planeSize; /* global (0,0,0) in the slab of rank 0 */
+			double one = 1.0;
+			pinc_check(pinc_hip_h2d(rho->dev->d + i0, &one, sizeof(double), g_pinc.stream), "cap unit charge");
+		}
+		solve(solver, rho, phi, mpi);
+		pinc_check(pinc_hip_d2h(G, phi->dev->global, NG * sizeof(double), g_pinc.stream), "cap green");
+	}
 	for (int a = 0; a < o->nObj; a++) {
 		long s0 = o->surfOff[a], na = o->surfOff[a + 1] - s0;
 		double *P = malloc(na * na * sizeof(double)), *M = malloc(na * na * sizeof(double));
-		for (long i = 0; i < na; i++) {
+		for (long i = 0; i < na && G; i++) {
+			long ni = o->surfNode[s0 + i];
+			long xi = ni % TX, yi = (ni / TX) % TY, zi = ni / (TX * TY);
+			for (long k = 0; k < na; k++) {
+				long nk = o->surfNode[s0 + k];
+				long dx = (nk % TX - xi + TX) % TX, dy = ((nk / TX) % TY - yi + TY) % TY,
+				     dz = (nk / (TX * TY) - zi + TZ) % TZ;
+				P[k * na + i] = G[dx + TX * (dy + TY * dz)];
+			}
+		}
+		for (long i = 0; i < na && !G; i++) {
 			pinc_check(pinc_hip_memset(rho->dev->d, 0, N * sizeof(double), g_pinc.stream), "cap");
 			pinc_check(pinc_hip_obj_add(rho->dev->d, o->dSurf + s0 + i, 1, 1.0, g_pinc.stream), "cap unit charge");
 			solve(solver, rho, phi, mpi);
@@ -281,6 +319,7 @@ void pinc_obj_capacitance(PincObj *o, Grid *rho, Grid *phi, void *solver,
 	pinc_hip_free(saveP);
 	pinc_hip_free(saveG);
 	free(col);
+	free(G);
 	rho->dev->ghostsValid = phi->dev->ghostsValid = 0;
 	o->haveCap = 1;
 }

@@ -192,3 +192,24 @@ def test_two_objects_match_checker(built, tmp_path):
         phi_o = w.grid(1)[1:-1, 1:-1, 1:-1]
         assert np.max(np.abs(phi_g - phi_o)) <= 1e-7 * np.abs(phi_o).max()
     assert ob.collected(0) != 0.0 and ob.collected(1) != 0.0
+
+
+def test_green_capacitance_matches_solves(built):
+    """objects:capacitance = green (one solve, columns by translation of the
+    periodic response) gives the run of the reference's one-solve-per-node
+    matrix, to the solver tolerance."""
+    from pinc_amd import Sim
+    res = []
+    for mode in ("solve", "green"):
+        cfg = configs.config("cold3d", true_size=(32, 16, 16), nsub=(1, 1, 1))
+        cfg["multigrid"]["mgLevels"] = "3"
+        cfg["population"]["fused"] = "0"
+        cfg["objects"] = {"sphere": "20.3,7.6,9.1,3.2", "capacitance": mode}
+        with Sim(configs.write_ini(cfg)) as s:
+            s.init()
+            s.step(3)
+            res.append((s.count(0), s.count(1), *s.energy()[:2], s.grid(1)[1:-1, 1:-1, 1:-1].copy()))
+    (a0, a1, ka, pa, fa), (b0, b1, kb, pb, fb) = res
+    assert (a0, a1) == (b0, b1)
+    assert abs(ka - kb) <= 1e-7 * abs(ka) and abs(pa - pb) <= 1e-7 * abs(pa)
+    assert np.max(np.abs(fa - fb)) <= 1e-6 * np.abs(fa).max()
