@@ -142,13 +142,14 @@ def main() -> int:
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
+        # control plane only (barriers, the communicator id, max-over-ranks
+        # timing): gloo over TCP.  The data path is the library's own RCCL
+        # communicator (pinc_hip_comm_init), so torch's bundled RCCL is never
+        # brought up next to it.
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if args.host_transport:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    red_dev = "cpu" if args.host_transport else "cuda"
+        dist.init_process_group("gloo")
+    red_dev = "cpu"
 
     from pinc_amd import configs, _lib
     from pinc_amd.sim import Sim

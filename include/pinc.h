@@ -195,6 +195,12 @@ MultigridSolver *mgAllocSolver(const dictionary *ini, Grid *rho, Grid *phi);
 void mgFreeSolver(MultigridSolver *solver);
 void mgSolve(MultigridSolver *solver, Grid *rho, Grid *phi, const MpiInfo *mpiInfo);
 long mgCycleCount(const MultigridSolver *solver);
+/* diagnostics (not in the reference): cap the V-cycles of one solve
+ * (0 = until converged, as multigrid.c:1698) and record the RMS residual
+ * after each cycle of the last solve into a buffer of histCap entries;
+ * mgHistory copies it out and returns the cycle count of that solve */
+void mgSetLimit(MultigridSolver *solver, long maxCycles, long histCap);
+long mgHistory(const MultigridSolver *solver, double *out, long cap);
 
 /* ---------------------------------------------------------- spectral -- */
 /* spectral.c:14-115; N-D extension of the reference's 1-D solver on rocFFT */
@@ -270,6 +276,10 @@ int pinc_sim_step(PincSim *sim);            /* one iteration of main.c:197-274 *
 int pinc_sim_op(PincSim *sim, const char *op);
 int pinc_sim_energy(PincSim *sim, double *ke, double *pe, double *keSpecies); /* rank-summed */
 long pinc_sim_cycles(const PincSim *sim);
+/* mgSetLimit / mgHistory of the simulation's multigrid solver (-1 if the
+ * Poisson solver is spectral) */
+int pinc_sim_mg_limit(PincSim *sim, long maxCycles, long histCap);
+long pinc_sim_mg_history(PincSim *sim, double *out, long cap);
 int pinc_sim_nspecies(const PincSim *sim);
 int pinc_sim_ndims(const PincSim *sim);
 long pinc_sim_pop_count(PincSim *sim, int s);

@@ -51,6 +51,11 @@ void oini_scaledouble(OIni *ini, const char *key, double factor);
 void oini_applysuffix(OIni *ini, const char *key, const char *suffix,
                       const double *mul, int mullen);
 void orc_die(const char *fmt, ...);
+/* OpenMP threads of the oracle's stencil and per-rank loops (ORC_THREADS,
+ * default 1).  Only loops whose result does not depend on the visiting
+ * order are parallel, so every output is bit-identical for any count. */
+extern int orc_nthreads;
+#define ORC_PAR_MIN 32768
 
 /* ---------------------------------------------------------------- types -- */
 typedef struct {
@@ -119,6 +124,9 @@ typedef struct {
 	double maxVel;
 	/* diagnostics */
 	long cycles;        /* V-cycles run so far */
+	long mgCap;         /* 0: loop until converged (multigrid.c:1698); else cycles per solve */
+	double *mgHist;     /* RMS residual after each cycle of the last solve */
+	long mgHistCap, mgHistN;
 	int verbose;        /* ORC_VERBOSE=n: MG progress every n cycles (stderr) */
 	long solves;
 	double lastKE, lastPE;

@@ -49,6 +49,9 @@ def _load() -> C.CDLL:
         "orc_kat_reciprocal": (C.c_int, [C.c_int, C.c_int]),
         "orc_kat_neighborhood": (None, [C.c_char_p, vp, vp]),
         "orc_world_ndims": (C.c_int, [vp]),
+        "orc_world_mg_limit": (None, [vp, C.c_long, C.c_long]),
+        "orc_world_mg_history": (C.c_long, [vp, vp, C.c_long]),
+        "orc_set_threads": (None, [C.c_int]),
         "orc_world_nspecies": (C.c_int, [vp]),
         "oo_create": (vp, [vp, vp]),
         "oo_free": (None, [vp]),
@@ -107,6 +110,18 @@ class World:
     @property
     def cycles(self):
         return LIB.orc_world_cycles(self._h)
+
+    def mg_limit(self, max_cycles: int = 0, hist_cap: int = 0):
+        """Cap the V-cycles of one solve (0: until converged) and record up
+        to hist_cap per-cycle RMS residuals."""
+        LIB.orc_world_mg_limit(self._h, max_cycles, hist_cap)
+
+    def mg_history(self) -> np.ndarray:
+        n = LIB.orc_world_mg_history(self._h, None, 0)
+        out = np.zeros(n)
+        if n:
+            LIB.orc_world_mg_history(self._h, out.ctypes.data, n)
+        return out
 
     def energy(self):
         ke, pe = C.c_double(), C.c_double()

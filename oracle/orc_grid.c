@@ -59,23 +59,29 @@ void og_free(OGrid *g){ free(g->val); g->val = NULL; }
 
 void og_zero(OGrid *g){ memset(g->val, 0, g->sizeProd[g->rank]*sizeof(double)); }
 
+int orc_nthreads = 1;
+
 void og_mul(OGrid *g, double num){
 	long n = g->sizeProd[g->rank];
+	#pragma omp parallel for num_threads(orc_nthreads) if(n > ORC_PAR_MIN)
 	for(long p = 0; p < n; p++) g->val[p] *= num;
 }
 
 void og_sub(OGrid *g, double num){
 	long n = g->sizeProd[g->rank];
+	#pragma omp parallel for num_threads(orc_nthreads) if(n > ORC_PAR_MIN)
 	for(long p = 0; p < n; p++) g->val[p] -= num;
 }
 
 void og_addto(OGrid *res, const OGrid *add){
 	long n = res->sizeProd[res->rank];
+	#pragma omp parallel for num_threads(orc_nthreads) if(n > ORC_PAR_MIN)
 	for(long p = 0; p < n; p++) res->val[p] += add->val[p];
 }
 
 void og_square(OGrid *g){
 	long n = g->sizeProd[g->rank];
+	#pragma omp parallel for num_threads(orc_nthreads) if(n > ORC_PAR_MIN)
 	for(long p = 0; p < n; p++) g->val[p] = g->val[p]*g->val[p];
 }
 
@@ -127,6 +133,7 @@ void og_findiff1st(const OGrid *scalar, OGrid *field){
 	for(int d = 1; d < rank; d++) start += sp[d];
 	long end = sp[rank] - start;
 	for(int d = 1; d < rank; d++){
+		#pragma omp parallel for num_threads(orc_nthreads) if(end - start > ORC_PAR_MIN)
 		for(long g = start; g < end; g++)
 			field->val[g*fstride + (d-1)] = 0.5*(scalar->val[g + sp[d]] - scalar->val[g - sp[d]]);
 	}
@@ -142,6 +149,7 @@ void og_findiff2nd(OGrid *res, const OGrid *phi){
 	for(int d = 1; d < rank; d++) g0 += sp[d];
 	if(rank == 4){
 		long end = sp[rank] - 2*g0;
+		#pragma omp parallel for num_threads(orc_nthreads) if(end > ORC_PAR_MIN)
 		for(long q = 0; q < end; q++){
 			long g = g0 + q;
 			double r = -6.*p[g];
@@ -151,6 +159,7 @@ void og_findiff2nd(OGrid *res, const OGrid *phi){
 	} else {
 		long end = sp[rank] - 2*g0;
 		double coeff = 2.*(rank-1);
+		#pragma omp parallel for num_threads(orc_nthreads) if(end > ORC_PAR_MIN)
 		for(long q = 0; q < end + 1; q++){
 			long g = g0 + q;
 			double r = -coeff*p[g];

@@ -57,6 +57,9 @@ void omg_gs_pass(OGrid *phi, const OGrid *rho, int pass, int nd3){
 	if(nd3){
 		double coeff = 1./6.;
 		int parity = (pass == 0) ? 1 : 0; /* red: j+k+l odd */
+		/* points of one colour only read the other colour: any visiting
+		 * order gives the same values */
+		#pragma omp parallel for num_threads(orc_nthreads) if(sp[4] > ORC_PAR_MIN)
 		for(int l = 1; l <= phi->trueSize[3]; l++)
 			for(int k = 0; k < phi->size[2]; k++)
 				for(int j = (k + l + parity) & 1; j < phi->size[1]; j += 2){
@@ -71,6 +74,7 @@ void omg_gs_pass(OGrid *phi, const OGrid *rho, int pass, int nd3){
 	int want = (nd + pass) & 1; /* parity of the coordinate sum */
 	int T[3] = {1, 1, 1};
 	for(int d = 0; d < nd; d++) T[d] = phi->trueSize[d+1];
+	#pragma omp parallel for num_threads(orc_nthreads) if(sp[rank] > ORC_PAR_MIN)
 	for(int z = 1; z <= (nd > 2 ? T[2] : 1); z++)
 		for(int y = 1; y <= (nd > 1 ? T[1] : 1); y++)
 			for(int x = 1; x <= T[0]; x++){
@@ -100,6 +104,7 @@ void omg_restrict(const OGrid *fine, OGrid *coarse, int nd3){
 	for(int d = 0; d < nd; d++) T[d] = coarse->trueSize[d+1];
 	if(nd3){
 		double coeff = 1./12.;
+		#pragma omp parallel for num_threads(orc_nthreads) if(cs[rank] > ORC_PAR_MIN)
 		for(int l = 1; l <= T[2]; l++)
 			for(int k = 1; k <= T[1]; k++)
 				for(int j = 1; j <= T[0]; j++){
@@ -111,6 +116,7 @@ void omg_restrict(const OGrid *fine, OGrid *coarse, int nd3){
 		return;
 	}
 	double c0 = 2.*nd;
+	#pragma omp parallel for num_threads(orc_nthreads) if(cs[rank] > ORC_PAR_MIN)
 	for(int l = 1; l <= (nd > 2 ? T[2] : 1); l++)
 		for(int k = 1; k <= (nd > 1 ? T[1] : 1); k++)
 			for(int j = 1; j <= T[0]; j++){
@@ -130,6 +136,7 @@ void omg_inject(OGrid *fine, const OGrid *coarse){
 	int nd = fine->rank - 1;
 	int T[3] = {1, 1, 1};
 	for(int d = 0; d < nd; d++) T[d] = coarse->trueSize[d+1];
+	#pragma omp parallel for num_threads(orc_nthreads) if(cs[fine->rank] > ORC_PAR_MIN)
 	for(int l = 1; l <= T[2]; l++)
 		for(int k = 1; k <= T[1]; k++)
 			for(int j = 1; j <= T[0]; j++){
@@ -147,10 +154,12 @@ void omg_prolong_dim(OGrid *fine, int r){
 	int nd = fine->rank - 1;
 	int T[3] = {1, 1, 1};
 	for(int d = 0; d < nd; d++) T[d] = fine->trueSize[d+1];
-	int c[4];
-	for(c[3] = 1; c[3] <= T[2]; c[3]++)
-		for(c[2] = 1; c[2] <= T[1]; c[2]++)
-			for(c[1] = 1; c[1] <= T[0]; c[1]++){
+	/* written points are even along r and read odd neighbours along r only */
+	#pragma omp parallel for num_threads(orc_nthreads) if(fs[fine->rank] > ORC_PAR_MIN)
+	for(int z = 1; z <= T[2]; z++)
+		for(int y = 1; y <= T[1]; y++)
+			for(int x = 1; x <= T[0]; x++){
+				int c[4] = {0, x, y, z};
 				int ok = 1;
 				for(int d = 1; d <= nd; d++){
 					if(d == r && (c[d] & 1)) ok = 0;
@@ -236,6 +245,8 @@ void ow_mg_solve(OWorld *w){
 		collect(w, selPhi, 0, phi);
 		collect(w, selRes, 0, res);
 		long N = og_tot_truesize(rho[0], &w->r[0].mpi);
+		long c = 0;
+		w->mgHistN = 0;
 		while(barRes > 1.E-10){
 			vrec(w, 0, bottom, 0);
 			w->cycles++;
@@ -244,6 +255,9 @@ void ow_mg_solve(OWorld *w){
 			double sum = 0;
 			for(int r = 0; r < w->P; r++){ og_square(res[r]); sum += og_sum_true(res[r]); }
 			barRes = sqrt(sum/N);
+			if(w->mgHistN < w->mgHistCap) w->mgHist[w->mgHistN] = barRes;
+			w->mgHistN++;
+			if(w->mgCap > 0 && ++c >= w->mgCap) break;
 			if(w->verbose && w->cycles % w->verbose == 0)
 				fprintf(stderr, "[orc] cycle %ld residual %.3e\n", (long)w->cycles, barRes);
 		}

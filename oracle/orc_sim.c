@@ -181,6 +181,7 @@ static void select_methods(OWorld *w){
 OWorld *ow_create(OIni *ini, int literal){
 	OWorld *w = calloc(1, sizeof(*w));
 	{ const char *ev = getenv("ORC_VERBOSE"); w->verbose = ev ? atoi(ev) : 0; }
+	{ const char *ev = getenv("ORC_THREADS"); if(ev && atoi(ev) > 0) orc_nthreads = atoi(ev); }
 	w->ini = ini;
 	w->literal = literal;
 	select_methods(w);
@@ -258,7 +259,7 @@ void ow_free(OWorld *w){
 		free(mp->emigrants); free(mp->emigrantIds);
 		free(mp->nEmigrants); free(mp->nImmigrants); free(mp->nEmigrantsAlloc);
 	}
-	free(w->r); free(w->keSpecies); free(w->spectralFactor);
+	free(w->r); free(w->keSpecies); free(w->spectralFactor); free(w->mgHist);
 	oini_free(w->ini);
 	free(w);
 }
@@ -617,4 +618,20 @@ void orc_kat_neighborhood(const char *iniText, double *thr, long *alloc){
 }
 
 int orc_world_ndims(const OWorld *w){ return w->nDims; }
+
+/* multigrid diagnostics: cycles per solve (0 = until converged) and the
+ * per-cycle RMS residual of the last solve */
+void orc_world_mg_limit(OWorld *w, long maxCycles, long histCap){
+	w->mgCap = maxCycles > 0 ? maxCycles : 0;
+	free(w->mgHist);
+	w->mgHist = histCap > 0 ? calloc(histCap, sizeof(double)) : NULL;
+	w->mgHistCap = histCap > 0 ? histCap : 0;
+	w->mgHistN = 0;
+}
+long orc_world_mg_history(const OWorld *w, double *out, long cap){
+	long n = w->mgHistN < w->mgHistCap ? w->mgHistN : w->mgHistCap;
+	if(out) for(long i = 0; i < n && i < cap; i++) out[i] = w->mgHist[i];
+	return w->mgHistN;
+}
+void orc_set_threads(int n){ if(n > 0) orc_nthreads = n; }
 int orc_world_nspecies(const OWorld *w){ return w->nSpecies; }

@@ -37,8 +37,15 @@ def _load() -> tuple[C.CDLL, C.CDLL]:
     host_path = LIBDIR / "libpinc.so"
     if not hip_path.exists() or not host_path.exists():
         raise ImportError(f"native PINC libraries not built ({LIBDIR}); run python -m pinc_amd.build")
-    hip = C.CDLL(str(hip_path), mode=C.RTLD_GLOBAL)
-    host = C.CDLL(str(host_path), mode=C.RTLD_GLOBAL)
+    # RTLD_LOCAL: libpinc_hip links the system ROCm runtime (/opt/rocm), torch
+    # ships its own copies under other file names.  Loaded RTLD_GLOBAL, the
+    # system runtime's symbols would interpose on the libraries torch loads
+    # afterwards, so torch would run on a mix of two HIP/HSA runtimes and
+    # abort in their teardown at exit (a double free, seen in round 1 when
+    # pinc_amd was imported before torch).  Local scope keeps each stack
+    # bound to its own runtime; libpinc finds libpinc_hip through its rpath.
+    hip = C.CDLL(str(hip_path), mode=C.RTLD_LOCAL)
+    host = C.CDLL(str(host_path), mode=C.RTLD_LOCAL)
     return hip, host
 
 
@@ -53,6 +60,8 @@ _sigs = {
     "pinc_sim_op": (C.c_int, [C.c_void_p, C.c_char_p]),
     "pinc_sim_energy": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "pinc_sim_cycles": (C.c_long, [C.c_void_p]),
+    "pinc_sim_mg_limit": (C.c_int, [C.c_void_p, C.c_long, C.c_long]),
+    "pinc_sim_mg_history": (C.c_long, [C.c_void_p, C.c_void_p, C.c_long]),
     "pinc_sim_nspecies": (C.c_int, [C.c_void_p]),
     "pinc_sim_ndims": (C.c_int, [C.c_void_p]),
     "pinc_sim_pop_count": (C.c_long, [C.c_void_p, C.c_int]),

@@ -1759,17 +1759,23 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 		}
 		// neighbour digit per dimension, as k_move_classify
 		int ne = 0;
+		bool outside = false;
 #pragma unroll
 		for (int d = ND - 1; d >= 0; d--) {
 			int dig = 1 - (p[k][d] < a.thr.lo[d]) + (p[k][d] >= a.thr.up[d]);
 			double q = p[k][d] - (double)(dig - 1) * (a.thr.hi[d] - 1.0);
-			bad |= (q < 0.0 || q > a.thr.hi[d]) << 1;
+			outside |= (q < 0.0 || q > a.thr.hi[d]);
 			if ((a.wrapMask >> d) & 1) {
 				if (dig != 1) p[k][d] = p[k][d] + (double)((1 - dig) * a.thr.T[d]);
 				dig = 1;
 			}
 			ne = ne * 3 + dig;
 		}
+		// pPosAssertInLocalFrame fails for this particle (the host stops the
+		// run with msg(ERROR) before the next deposit): route it to the
+		// emigrant path so that nothing indexes the grid with it
+		bad |= (int)outside << 1;
+		if (outside) ne = 0;
 		if (SORT) {
 			// flag staged by block slot (outside the box: by item position)
 			const int r = rlL[k * kPushThreads + threadIdx.x];

@@ -34,6 +34,7 @@ struct pinc_fft_s {
 namespace {
 
 bool g_rocfft_ready = false;
+int g_rocfft_plans = 0;  // live plans (pinc_hip_fft_create / _destroy)
 
 int fft_error(rocfft_status s, const char *where) {
 	if (s == rocfft_status_success) return 0;
@@ -83,6 +84,7 @@ extern "C" int pinc_hip_fft_create(pinc_fft_t **out, int nd, const int *T, void 
 		g_rocfft_ready = true;
 	}
 	pinc_fft_t *f = (pinc_fft_t *)calloc(1, sizeof(pinc_fft_t));
+	g_rocfft_plans++;
 	f->nd = nd;
 	f->nReal = 1;
 	for (int d = 0; d < 3; d++) {
@@ -156,4 +158,11 @@ extern "C" void pinc_hip_fft_destroy(pinc_fft_t *f) {
 	if (f->rin) (void)hipFree(f->rin);
 	if (f->spec) (void)hipFree(f->spec);
 	free(f);
+	// rocfft_setup is paired with rocfft_cleanup once the last plan is gone,
+	// so rocFFT's state is released while the HIP runtime is still up
+	// instead of by static destructors after it
+	if (--g_rocfft_plans == 0 && g_rocfft_ready) {
+		(void)rocfft_cleanup();
+		g_rocfft_ready = false;
+	}
 }

@@ -35,7 +35,10 @@ void msg(msgKind kind, const char *format, ...) {
 	}
 	if ((kind & 0x0F) == ERROR) snprintf(g_lastError, sizeof(g_lastError), "%s", buf);
 	if ((kind & ALL) || g_pinc.rank == 0) {
-		if ((kind & 0x0F) != STATUS || getenv("PINC_VERBOSE")) fprintf(stream, "%s: %s\n", prefix, buf);
+		/* STATUS lines print as in the reference (only regular() emits them);
+		 * PINC_QUIET silences them */
+		if ((kind & 0x0F) != STATUS || !getenv("PINC_QUIET")) fprintf(stream, "%s: %s\n", prefix, buf);
+		fflush(stream);
 	}
 	if ((kind & 0x0F) == ERROR) exit(EXIT_FAILURE);
 }

@@ -150,6 +150,10 @@ struct MultigridSolver {
 	int native;
 	int useGraph;      /* multigrid:graph: replay one captured V-cycle */
 	void *cycleGraph;  /* instantiated graph of vrec(S, 0) */
+	/* diagnostics: RMS residual after each V-cycle of the last solve, and an
+	 * optional cap on the cycles of one solve (0 = loop until converged) */
+	double *hist;
+	long histCap, histN, maxCycles;
 };
 
 /* collectives over RCCL or the host transport (pinc_comm.c) */

@@ -133,6 +133,7 @@ MultigridSolver *mgAllocSolver(const dictionary *ini, Grid *rho, Grid *phi) {
 void mgFreeSolver(MultigridSolver *S) {
 	if (!S) return;
 	pinc_hip_graph_destroy(S->cycleGraph);
+	free(S->hist);
 	for (int q = 0; q < S->nLevels; q++) {
 		if (q > 0) {
 			pinc_hip_free(S->rho[q]);
@@ -144,6 +145,21 @@ void mgFreeSolver(MultigridSolver *S) {
 }
 
 long mgCycleCount(const MultigridSolver *S) { return S->cycles; }
+
+void mgSetLimit(MultigridSolver *S, long maxCycles, long histCap) {
+	S->maxCycles = maxCycles > 0 ? maxCycles : 0;
+	free(S->hist);
+	S->hist = histCap > 0 ? calloc(histCap, sizeof(double)) : NULL;
+	S->histCap = histCap > 0 ? histCap : 0;
+	S->histN = 0;
+}
+
+long mgHistory(const MultigridSolver *S, double *out, long cap) {
+	long n = S->histN < S->histCap ? S->histN : S->histCap;
+	if (out)
+		for (long i = 0; i < n && i < cap; i++) out[i] = S->hist[i];
+	return S->histN;
+}
 
 /* gNeutralizeGrid on a level of the global grid */
 static void neutralize(double *a, long N) {
@@ -278,9 +294,10 @@ void mgSolve(MultigridSolver *S, Grid *rho, Grid *phi, const MpiInfo *mpiInfo) {
 		 * caps a solve for diagnostics (stops with a warning) */
 		const long maxCycles = 1000000;
 		const char *capEnv = getenv("PINC_MG_MAX_CYCLES");
-		long cap = capEnv ? atol(capEnv) : 0;
+		long cap = S->maxCycles ? S->maxCycles : (capEnv ? atol(capEnv) : 0);
 		double barRes = 2.;
 		long c = 0;
+		S->histN = 0;
 		while (barRes > 1.E-10) {
 			if (S->useGraph) {
 				/* the V-cycle is a fixed launch sequence on fixed buffers:
@@ -308,6 +325,13 @@ void mgSolve(MultigridSolver *S, Grid *rho, Grid *phi, const MpiInfo *mpiInfo) {
 			double sum = 0;
 			pinc_check(pinc_hip_d2h(&sum, PINC_SLOT(TMP_SLOT + 1), sizeof(double), g_pinc.stream), "norm");
 			barRes = sqrt(sum / S->N[0]);
+			if (S->histN < S->histCap) S->hist[S->histN] = barRes;
+			S->histN++;
+			if (S->maxCycles && !isfinite(barRes)) {
+				/* diagnostic run (mgSetLimit): keep the history, stop */
+				fprintf(stderr, "[pinc] rank %d solve stopped: residual %g after %ld cycles\n", g_pinc.rank, barRes, c + 1);
+				break;
+			}
 			if (++c > maxCycles || isnan(barRes)) msg(ERROR, "multigrid did not converge (residual %g)", barRes);
 			if (g_pinc.verbose && (c % g_pinc.verbose == 0)) {
 				fprintf(stderr, "[pinc] rank %d solve cycle %ld residual %.3e\n", g_pinc.rank, c, barRes);

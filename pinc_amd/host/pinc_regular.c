@@ -153,6 +153,10 @@ static void sim_step(PincSim *S) {
 	puMove(pop, NULL);
 	S->extractEmigrants(pop, S->mpi);
 	puMigrate(pop, S->mpi, S->rho);
+	/* pPosAssertInLocalFrame (main.c:219) before anything deposits an
+	 * immigrant: a particle outside the local frame must not reach the
+	 * deposit's grid indexing */
+	check_errors();
 	if (S->obj) pinc_obj_collect(S->obj, pop, 0); /* main.c:222 */
 	S->distr(pop, S->rho);
 	gHaloOp((funPtr)addSlice, S->rho, S->mpi, FROMHALO);
@@ -337,6 +341,17 @@ int pinc_sim_energy(PincSim *S, double *ke, double *pe, double *keSpecies) {
 long pinc_sim_cycles(const PincSim *S) {
 	return S->spectral ? sSolveCount(S->solver) : mgCycleCount(S->solver);
 }
+int pinc_sim_mg_limit(PincSim *S, long maxCycles, long histCap) {
+	if (S->spectral) return -1;
+	mgSetLimit(S->solver, maxCycles, histCap);
+	return 0;
+}
+
+long pinc_sim_mg_history(PincSim *S, double *out, long cap) {
+	if (S->spectral) return -1;
+	return mgHistory(S->solver, out, cap);
+}
+
 int pinc_sim_nspecies(const PincSim *S) { return S->pop->nSpecies; }
 int pinc_sim_ndims(const PincSim *S) { return S->pop->nDims; }
 long pinc_sim_pop_count(PincSim *S, int s) { return S->pop->iStop[s] - S->pop->iStart[s]; }

@@ -96,6 +96,20 @@ class Sim:
     def cycles(self) -> int:
         return HOST.pinc_sim_cycles(self._h)
 
+    def mg_limit(self, max_cycles: int = 0, hist_cap: int = 0) -> None:
+        """Cap the V-cycles of one multigrid solve (0: until converged) and
+        record up to hist_cap per-cycle RMS residuals (mgSetLimit)."""
+        if HOST.pinc_sim_mg_limit(self._h, max_cycles, hist_cap):
+            raise RuntimeError("mg_limit: the Poisson solver is not multigrid")
+
+    def mg_history(self) -> np.ndarray:
+        """RMS residual after each V-cycle of the last solve (mgHistory)."""
+        n = HOST.pinc_sim_mg_history(self._h, None, 0)
+        out = np.zeros(max(n, 0))
+        if n > 0:
+            HOST.pinc_sim_mg_history(self._h, out.ctypes.data, n)
+        return out
+
     def count(self, s: int) -> int:
         return HOST.pinc_sim_pop_count(self._h, s)
 

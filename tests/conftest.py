@@ -22,11 +22,9 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def built():
     import subprocess
-    # torch (device memory for the kernel-level tests) brings up the HIP
-    # runtime first, whichever test file runs first: with the native
-    # library initialised before it, the process aborted at exit in the
-    # runtimes' teardown (a double free after all tests had passed)
-    import torch  # noqa: F401
+    # no import-order workaround: pinc_amd loads its libraries RTLD_LOCAL
+    # (pinc_amd/_lib.py), and tests/test_abi_gpu.py checks that a process
+    # importing pinc_amd before torch exits cleanly
     from pinc_amd.build import build
     subprocess.run(["make", "-s", "-C", str(ROOT / "oracle"), "-j4"], check=True)
     return build()
