@@ -37,13 +37,22 @@ def _load() -> tuple[C.CDLL, C.CDLL]:
     host_path = LIBDIR / "libpinc.so"
     if not hip_path.exists() or not host_path.exists():
         raise ImportError(f"native PINC libraries not built ({LIBDIR}); run python -m pinc_amd.build")
-    # RTLD_LOCAL: libpinc_hip links the system ROCm runtime (/opt/rocm), torch
-    # ships its own copies under other file names.  Loaded RTLD_GLOBAL, the
-    # system runtime's symbols would interpose on the libraries torch loads
-    # afterwards, so torch would run on a mix of two HIP/HSA runtimes and
-    # abort in their teardown at exit (a double free, seen in round 1 when
-    # pinc_amd was imported before torch).  Local scope keeps each stack
-    # bound to its own runtime; libpinc finds libpinc_hip through its rpath.
+    # One ROCm stack per process.  libpinc_hip.so needs libamdhip64.so.7,
+    # librocfft.so.0 and librccl.so.1; torch bundles its own copies with the
+    # same sonames but links them under unversioned names.  Loaded first, the
+    # system (/opt/rocm) copies do not satisfy torch's names, so torch brings
+    # a second HIP/HSA runtime into the process: the second one to touch the
+    # GPU finds no device (KFD serves one runtime per process), and in round
+    # 1 the two copies aborted at exit in their teardown (a double free) --
+    # that was the import-order dependence.  Loading torch first makes the
+    # loader satisfy our sonames with torch's already-loaded stack, whichever
+    # module the caller imported first; a process without torch (the C
+    # driver, tests/c_driver) runs on /opt/rocm.  RTLD_LOCAL keeps our
+    # symbols out of the global scope; libpinc finds libpinc_hip by rpath.
+    try:
+        import torch  # noqa: F401  (see above: binds our libraries to torch's ROCm stack)
+    except ImportError:
+        pass
     hip = C.CDLL(str(hip_path), mode=C.RTLD_LOCAL)
     host = C.CDLL(str(host_path), mode=C.RTLD_LOCAL)
     return hip, host

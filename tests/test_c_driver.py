@@ -7,7 +7,8 @@
   "KE .. PE .." STATUS lines (regular(), main.c:197-274) must match the
   oracle's energy history, and it must exit 0.
 * Python processes that import pinc_amd before or after torch must exit 0
-  (round 1 hid an abort at exit behind the import order).
+  (round 1 hid an abort at exit behind the import order, ADVICE r01: two
+  ROCm stacks in one process, see pinc_amd/_lib.py).
 """
 import os
 import re

