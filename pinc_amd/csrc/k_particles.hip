@@ -1898,21 +1898,46 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 
 	PUSH_TS(6);
 	// ---- phase E: deposit of the particles that stay
-	auto add_corner = [&](const int *j, int c, double w) {
-		int cc[3] = {0, 0, 0};
+	// global fallback of one corner (nodes outside the LDS box: far movers,
+	// wrapped particles, a block whose box did not fit)
+	auto add_corner_global = [&](const int *j, int c, double w) {
+		int off = 0;
 #pragma unroll
-		for (int d = 0; d < ND; d++) cc[d] = j[d] + ((c >> d) & 1);
-		if (rB.inside(cc, ND)) {
-			atomicAdd(&rhoL[rB.index(cc, ND)], w);
+		for (int d = 0; d < ND; d++) {
+			int o0, o1;
+			node_pair(G, d, j[d], o0, o1);
+			off += ((c >> d) & 1) ? o1 : o0;
+		}
+		unsafeAtomicAdd(&a.rho[(unsigned)off], w);
+	};
+	// LDS offsets of the 2^ND corners relative to the cell's lower node
+	// (block-uniform: scalar registers)
+	int coff[NC];
+#pragma unroll
+	for (int c = 0; c < NC; c++) {
+		int o = 0, st = 1;
+#pragma unroll
+		for (int d = 0; d < ND; d++) {
+			o += ((c >> d) & 1) ? st : 0;
+			st *= rB.n[d];
+		}
+		coff[c] = o;
+	}
+	// LDS index of the cell's lower node if all 2^ND corners lie in the box,
+	// else -1 (one test per particle instead of one per corner)
+	auto box_cell = [&](const int *j) -> int {
+		bool in = rB.vol > 0;
+#pragma unroll
+		for (int d = 0; d < ND; d++) in = in && j[d] >= rB.lo[d] && j[d] + 1 < rB.lo[d] + rB.n[d];
+		return in ? rB.index(j, ND) : -1;
+	};
+	auto add8 = [&](const int *j, int l0, const double *w) {
+		if (l0 >= 0) {
+#pragma unroll
+			for (int c = 0; c < NC; c++) atomicAdd(&rhoL[l0 + coff[c]], w[c]);
 		} else {
-			int off = 0;
 #pragma unroll
-			for (int d = 0; d < ND; d++) {
-				int o0, o1;
-				node_pair(G, d, j[d], o0, o1);
-				off += ((c >> d) & 1) ? o1 : o0;
-			}
-			unsafeAtomicAdd(&a.rho[(unsigned)off], w);
+			for (int c = 0; c < NC; c++) add_corner_global(j, c, w[c]);
 		}
 	};
 	const int keyMul[3] = {1, G.T[0] + 2, (G.T[0] + 2) * (G.T[1] + 2)};  // unique cell key
@@ -1934,7 +1959,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	// one wave pass: lanes sharing a cell (up to kPushGroups groups of at
 	// least kPushGroupMin lanes) are summed across the wave and added once,
 	// the others add their weights one by one
-	auto deposit_pass = [&](bool mine, const int *j, const double *w, int key) {
+	auto deposit_pass = [&](bool mine, const int *j, const double *w, int key, int l0) {
 		unsigned long long pend = __ballot(mine);
 		unsigned long long indiv = 0;
 #pragma unroll 1
@@ -1953,16 +1978,18 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 			for (int c = 0; c < 8; c++) r[c] = in ? w[c] : 0.0;
 			double sum = wave_reduce8(r);
 			const int corner = lane >> 3;
-			int jl[3] = {0, 0, 0};  // leader's cell (read with every lane active)
+			const int ll = __shfl(l0, leader, 64);  // leader's box cell (every lane active)
+			if (ll >= 0) {
+				if ((lane & 7) == 0 && corner < NC) atomicAdd(&rhoL[ll + coff[corner]], sum);
+			} else {
+				int jl[3] = {0, 0, 0};
 #pragma unroll
-			for (int d = 0; d < ND; d++) jl[d] = __shfl(j[d], leader, 64);
-			if ((lane & 7) == 0 && corner < NC) add_corner(jl, corner, sum);
+				for (int d = 0; d < ND; d++) jl[d] = __shfl(j[d], leader, 64);
+				if ((lane & 7) == 0 && corner < NC) add_corner_global(jl, corner, sum);
+			}
 		}
 		indiv |= pend;
-		if ((indiv >> lane) & 1ull) {
-#pragma unroll
-			for (int c = 0; c < NC; c++) add_corner(j, c, w[c]);
-		}
+		if ((indiv >> lane) & 1ull) add8(j, l0, w);
 	};
 	// the two particles of a lane's pair are neighbours in memory and mostly
 	// share a cell: their weights are summed in the lane first, so one wave
@@ -1989,11 +2016,9 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 			for (int c = 0; c < 8; c++) w[c] = w1[c];
 			key = key1;
 		}
-		deposit_pass(m0 || m1, j, w, key);
-		if (m0 && m1 && !merge) {
-#pragma unroll
-			for (int c = 0; c < NC; c++) add_corner(j1, c, w1[c]);
-		}
+		const int l0 = (m0 || m1) ? box_cell(j) : -1;
+		deposit_pass(m0 || m1, j, w, key, l0);
+		if (m0 && m1 && !merge) add8(j1, box_cell(j1), w1);
 	}
 
 	if (KICK) {
