@@ -66,29 +66,62 @@ def _pmc_traffic(prefix: str):
     return None
 
 
-def _cpu_baseline(size: int, ppc: int, steps: int) -> dict:
-    """The oracle (plain-C restatement of the reference, one core) on a
-    bounded sample of the same workload."""
+def _cpu_threads() -> int:
+    """Host threads the CPU baseline uses: the job's CPU share (the GPU box
+    sets OMP_NUM_THREADS to it), at most the CPUs this process may run on."""
+    aff = len(os.sched_getaffinity(0))
+    return max(1, min(aff, int(os.environ.get("OMP_NUM_THREADS", aff))))
+
+
+def _cpu_baseline(size: int, ppc: int, steps: int, native: bool) -> dict:
+    """The oracle (plain-C restatement of the reference) on the host cores,
+    on a bounded sample of the same workload: the warm plasma at size^3 with
+    ppc particles per cell per species, decomposed into one z-slab per
+    thread (grid:nSubdomains = 1,1,T, the reference's MPI decomposition,
+    emulated ranks in parallel with OpenMP), solving with the same multigrid
+    algorithm as the GPU line (native mode, orc_native.c, or the
+    reference's)."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import orc  # test/baseline infrastructure only
     from pinc_amd import configs
-    cfg = configs.config("warm", true_size=(size, size, size), nsub=(1, 1, 1), ppc=ppc, nalloc_pc=ppc + 8)
+    threads = _cpu_threads()
+    nsub = threads
+    while nsub > 1 and (size % nsub or (size // nsub) % 2):
+        nsub -= 1
+    orc.LIB.orc_set_threads(threads)
+    cfg = configs.config("warm", true_size=(size, size, size // nsub), nsub=(1, 1, nsub), ppc=ppc,
+                         nalloc_pc=ppc + 8, levels=1 if native else 5)
+    if native:
+        cfg["multigrid"]["native"] = "1"
     ini = configs.write_ini(cfg)
+    t_init = time.perf_counter()
     w = orc.World(ini)
     w.init(perturb=False, maxwell=True, seed=20260101)
     w.init_fields()
-    n = w.count(0) + w.count(1)
+    t_init = time.perf_counter() - t_init
+    n = sum(w.count(s, rank=r) for r in range(w.nranks) for s in range(2))
     c0 = w.cycles
+    ph0 = w.timers()
     t0 = time.perf_counter()
     w.step(steps)
     dt = time.perf_counter() - t0
+    ph = {k: (v - ph0[k]) * 1e3 / steps for k, v in w.timers().items()}
     cyc = (w.cycles - c0) / steps
+    levels = orc.LIB.orc_world_mg_levels(w._h)
     w.close()
     os.unlink(ini)
-    return {"value": n * steps / dt, "unit": "particle-updates/s", "cores": 1, "kind": "port",
-            "sample": f"oracle (C restatement, 1 thread) on the same warm 3-D workload at {size}^3, "
-                      f"{ppc} ppc x 2 species ({n} particles), {steps} steps; {cyc:.0f} V-cycles/solve",
-            "seconds": dt}
+    push_ms = ph["move"] + ph["migrate"] + ph["deposit"] + ph["accelerate"]
+    return {"value": n * steps / dt, "unit": "particle-updates/s", "cores": threads, "kind": "port",
+            "nproc": os.cpu_count(), "cpu_share": len(os.sched_getaffinity(0)),
+            "sample": f"oracle (C restatement of the reference, OpenMP over {nsub} emulated z-slab ranks, "
+                      f"{threads} threads) on the same warm 3-D workload at {size}^3, {ppc} ppc x 2 species "
+                      f"({n} particles), {steps} steps; multigrid "
+                      + ("native mode as the GPU line" if native else "reference algorithm")
+                      + f", {levels} levels, {cyc:.0f} V-cycles/solve",
+            "seconds": dt, "init_s": t_init,
+            "push_deposit_updates_per_s": n / (push_ms * 1e-3) if push_ms > 0 else None,
+            "poisson_ms_per_step": ph["solve"], "mg_cycles_per_solve": cyc,
+            "phase_ms_per_step": ph}
 
 
 def main() -> int:
@@ -122,8 +155,8 @@ def main() -> int:
     ap.add_argument("--sort-in-push", type=int, default=1,
                     help="1: the tile sort rides in every sort-interval-th push (default); 0: separate sort pass")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-size", type=int, default=64)
-    ap.add_argument("--cpu-steps", type=int, default=8)
+    ap.add_argument("--cpu-size", type=int, default=128)
+    ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--host-transport", action="store_true",
                     help="rehearsal only: N ranks share GPU 0 and the collectives go through the gloo host "
                          "transport (RCCL refuses two ranks on one device); never the measured configuration")
@@ -338,7 +371,7 @@ def main() -> int:
     os.unlink(ini)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = _cpu_baseline(args.cpu_size, args.ppc, args.cpu_steps)
+        result["cpu_baseline"] = _cpu_baseline(args.cpu_size, args.ppc, args.cpu_steps, args.mg == "native")
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist is not None:

@@ -111,6 +111,8 @@ enum { ORC_RESTR_3D, ORC_RESTR_ND };
 enum { ORC_PROL_3D, ORC_PROL_ND };
 enum { ORC_POISSON_MG, ORC_POISSON_SPECTRAL };
 
+typedef struct ONative ONative;  /* orc_native.c */
+
 typedef struct {
 	int P;              /* number of subdomains (emulated ranks) */
 	int nDims, nSpecies;
@@ -135,6 +137,8 @@ typedef struct {
 	double unitCharge, unitMass, unitLength, unitTime;
 	int literal;        /* 1: reproduce main.c double FROMHALO + 2nd solve */
 	double *spectralFactor; /* 1-D spectral solver (spectral.c:29-37) */
+	ONative *native;    /* multigrid:native = 1 (the device's native mode) */
+	double phaseT[7];   /* ow_step wall seconds per phase */
 } OWorld;
 
 /* ---------------------------------------------------------------- grid -- */
@@ -189,6 +193,12 @@ void om_create_neighborhood(OMpi *mpi, const OIni *ini, const OGrid *g);
 void ow_mg_alloc(OWorld *w);
 void ow_mg_solve(OWorld *w);
 void ow_spectral_solve(OWorld *w);
+/* native-mode multigrid of the MI355X build (orc_native.c; not the
+ * reference's algorithm): correction scheme with the coarse h^2 factor */
+ONative *on_alloc(int nd, const int *Tglobal, int nLevelsIni, int nd3);
+void on_free(ONative *S);
+int on_levels(const ONative *S);
+void ow_native_solve(OWorld *w);
 /* single-grid stencil primitives (exported for unit tests) */
 void omg_gs_pass(OGrid *phi, const OGrid *rho, int color, int nd3);
 void omg_residual(OGrid *res, const OGrid *rho, const OGrid *phi);

@@ -52,6 +52,8 @@ def _load() -> C.CDLL:
         "orc_world_mg_limit": (None, [vp, C.c_long, C.c_long]),
         "orc_world_mg_history": (C.c_long, [vp, vp, C.c_long]),
         "orc_set_threads": (None, [C.c_int]),
+        "orc_world_mg_levels": (C.c_int, [vp]),
+        "orc_world_timers": (None, [vp, vp]),
         "orc_world_nspecies": (C.c_int, [vp]),
         "oo_create": (vp, [vp, vp]),
         "oo_free": (None, [vp]),
@@ -115,6 +117,14 @@ class World:
         """Cap the V-cycles of one solve (0: until converged) and record up
         to hist_cap per-cycle RMS residuals."""
         LIB.orc_world_mg_limit(self._h, max_cycles, hist_cap)
+
+    PHASES = ["move", "migrate", "deposit", "solve", "efield", "accelerate", "energy"]
+
+    def timers(self) -> dict:
+        """Wall seconds per phase of ow_step since creation."""
+        out = np.zeros(7)
+        LIB.orc_world_timers(self._h, out.ctypes.data)
+        return dict(zip(self.PHASES, out.tolist()))
 
     def mg_history(self) -> np.ndarray:
         n = LIB.orc_world_mg_history(self._h, None, 0)

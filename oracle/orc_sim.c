@@ -19,6 +19,18 @@
  */
 #include "orc.h"
 #include <math.h>
+#include <time.h>
+
+/* per-rank loops run in parallel over the emulated ranks (OpenMP): every
+ * rank's state is private to it and cross-rank combination happens after
+ * the loop in rank order, so results are bit-identical to a serial run */
+#define PER_RANK _Pragma("omp parallel for num_threads(orc_nthreads) schedule(static) if(w->P > 1)")
+
+static double now_s(void){
+	struct timespec t;
+	clock_gettime(CLOCK_MONOTONIC, &t);
+	return t.tv_sec + 1e-9*t.tv_nsec;
+}
 
 static const double elementaryCharge = 1.60217733e-19;
 static const double electronMass = 9.10938188e-31;
@@ -230,6 +242,11 @@ OWorld *ow_create(OIni *ini, int literal){
 	}
 	free(nsub); free(ng); free(ts);
 	if(w->poisson == ORC_POISSON_MG) ow_mg_alloc(w);
+	if(w->poisson == ORC_POISSON_MG && oini_has(ini, "multigrid:native") && oini_int(ini, "multigrid:native")){
+		int Tg[3] = {1, 1, 1};
+		for(int d = 0; d < nd; d++) Tg[d] = w->r[0].rho.trueSize[d+1]*w->r[0].mpi.nSubdomains[d];
+		w->native = on_alloc(nd, Tg, w->nLevels, w->restrictor == ORC_RESTR_3D);
+	}
 	else if(nd == 1 && w->P == 1){
 		int N = w->r[0].rho.trueSize[1];
 		int M = N/2 + 1;
@@ -260,12 +277,14 @@ void ow_free(OWorld *w){
 		free(mp->nEmigrants); free(mp->nImmigrants); free(mp->nEmigrantsAlloc);
 	}
 	free(w->r); free(w->keSpecies); free(w->spectralFactor); free(w->mgHist);
+	on_free(w->native);
 	oini_free(w->ini);
 	free(w);
 }
 
 /* ---------------------------------------------------------- operators -- */
 static void do_extract(OWorld *w){
+	PER_RANK
 	for(int r = 0; r < w->P; r++){
 		if(w->migrate == ORC_MIG_3D) opu_extract3d(&w->r[r].pop, &w->r[r].mpi);
 		else opu_extractnd(&w->r[r].pop, &w->r[r].mpi);
@@ -274,6 +293,7 @@ static void do_extract(OWorld *w){
 
 static void do_distr(OWorld *w){
 	OGrid *rho[256];
+	PER_RANK
 	for(int r = 0; r < w->P; r++){
 		if(w->distr == ORC_DISTR_3D1) opu_distr3d1(&w->r[r].pop, &w->r[r].rho);
 		else opu_distrnd1(&w->r[r].pop, &w->r[r].rho);
@@ -283,7 +303,8 @@ static void do_distr(OWorld *w){
 }
 
 static void do_solve(OWorld *w){
-	if(w->poisson == ORC_POISSON_MG) ow_mg_solve(w);
+	if(w->native) ow_native_solve(w);
+	else if(w->poisson == ORC_POISSON_MG) ow_mg_solve(w);
 	else ow_spectral_solve(w);
 }
 
@@ -297,6 +318,7 @@ static void do_efield(OWorld *w, int haloPhi){
 }
 
 static void do_acc(OWorld *w){
+	PER_RANK
 	for(int r = 0; r < w->P; r++){
 		OPop *p = &w->r[r].pop;
 		OGrid *E = &w->r[r].E;
@@ -315,20 +337,24 @@ static void do_energy(OWorld *w){
 	int ns = w->nSpecies;
 	double ke = 0, pe = 0;
 	for(int s = 0; s < ns; s++) w->keSpecies[s] = 0;
+	PER_RANK
 	for(int r = 0; r < w->P; r++){
 		OPop *p = &w->r[r].pop;
 		op_sum_kin(p);
+		p->potEnergy[ns] = og_pot_energy_inner(&w->r[r].rho, &w->r[r].phi)*0.5;
+	}
+	for(int r = 0; r < w->P; r++){
+		OPop *p = &w->r[r].pop;
 		ke += p->kinEnergy[ns];
 		for(int s = 0; s < ns; s++) w->keSpecies[s] += p->kinEnergy[s];
-		double e = og_pot_energy_inner(&w->r[r].rho, &w->r[r].phi)*0.5;
-		p->potEnergy[ns] = e;
-		pe += e;
+		pe += p->potEnergy[ns];
 	}
 	w->lastKE = ke;
 	w->lastPE = pe;
 }
 
 void ow_init(OWorld *w, int perturb, int maxwell, unsigned long long seed){
+	PER_RANK
 	for(int r = 0; r < w->P; r++){
 		ORank *R = &w->r[r];
 		op_pos_lattice(&R->pop, w->ini, &R->mpi);
@@ -371,10 +397,17 @@ void ow_init_fields(OWorld *w){
 }
 
 void ow_step(OWorld *w){
+	/* per-phase wall times: move, extract+migrate, deposit (+fold), solve,
+	 * E field, accelerate, energies */
+	double t0 = now_s(), t;
+	PER_RANK
 	for(int r = 0; r < w->P; r++) opu_move(&w->r[r].pop);
+	t = now_s(); w->phaseT[0] += t - t0; t0 = t;
 	do_extract(w);
 	ow_migrate(w);
+	t = now_s(); w->phaseT[1] += t - t0; t0 = t;
 	do_distr(w);
+	t = now_s(); w->phaseT[2] += t - t0; t0 = t;
 	if(w->literal){
 		OGrid *rho[256];
 		for(int r = 0; r < w->P; r++) rho[r] = &w->r[r].rho;
@@ -382,9 +415,13 @@ void ow_step(OWorld *w){
 		do_solve(w);
 	}
 	do_solve(w);
+	t = now_s(); w->phaseT[3] += t - t0; t0 = t;
 	do_efield(w, 1);
+	t = now_s(); w->phaseT[4] += t - t0; t0 = t;
 	do_acc(w);
+	t = now_s(); w->phaseT[5] += t - t0; t0 = t;
 	do_energy(w);
+	t = now_s(); w->phaseT[6] += t - t0;
 }
 
 /* main.c:197-274 with the immersed-object calls (main.c:221-238):
@@ -634,4 +671,7 @@ long orc_world_mg_history(const OWorld *w, double *out, long cap){
 	return w->mgHistN;
 }
 void orc_set_threads(int n){ if(n > 0) orc_nthreads = n; }
+/* seconds per phase since creation (see ow_step) */
+void orc_world_timers(const OWorld *w, double *out){ memcpy(out, w->phaseT, 7*sizeof(double)); }
+int orc_world_mg_levels(const OWorld *w){ return w->native ? on_levels(w->native) : w->nLevels; }
 int orc_world_nspecies(const OWorld *w){ return w->nSpecies; }

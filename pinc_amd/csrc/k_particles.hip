@@ -1226,7 +1226,7 @@ struct PushArgs {
 };
 // phase timestamp of the block (thread 0, s_memrealtime at 100 MHz)
 #define PUSH_TS(slot) \
-	if (a.tstamp && threadIdx.x == 0) a.tstamp[(long)blockIdx.x * 8 + (slot)] = wall_clock64()
+	if (a.tstamp && threadIdx.x == 0) a.tstamp[(long)chunk * 8 + (slot)] = wall_clock64()
 
 // same-cell groups of at least kPushGroupMin lanes (at most kPushGroups of
 // them per wave and item) are summed across the wave before the LDS add
@@ -1239,6 +1239,26 @@ struct PushArgs {
 #define PINC_PUSH_GROUPS 4
 #endif
 constexpr int kPushGroupMin = PINC_PUSH_GROUP_MIN;
+// diagnostics only (timing by elimination, wrong results): bit 0 skips the
+// deposit, bit 1 the E staging and gather, bit 2 the flush
+#ifndef PINC_PUSH_SKIP
+#define PINC_PUSH_SKIP 0
+#endif
+// deposit into per-lane-group copies of the LDS charge box (lane & (nc-1)
+// picks the copy, nc <= PINC_PUSH_COPIES copies as the box allows) with
+// plain LDS atomics, instead of same-cell wave reductions (0).  Measured at
+// C4 (mean over the sort cycle): 0 copies 29.6 ms per species launch,
+// 2 copies 30.0, 4 copies 28.2, 8 copies 28.2 -- a sorted wave's lanes
+// mostly share one cell, and 8 copies cut the same-address conflicts of
+// each ds_add_f64 to 8-way for ~60 fewer VALU instructions per particle
+// than the reduction.  (Tried and rejected the same day: whole-chunk
+// launches without per-element conditions, 43 ms, spills; 2 items per
+// thread at 4-5 waves/SIMD, 31-32 ms; 512-thread blocks, 35.8 ms.)
+#ifndef PINC_PUSH_COPIES
+#define PINC_PUSH_COPIES 8
+#endif
+constexpr int kRhoLds = PINC_PUSH_COPIES ? 2048 : 1024;
+
 constexpr int kPushGroups = PINC_PUSH_GROUPS;
 // 8 waves x 4 particles per thread per PINC_CHUNK block: fewer live VGPRs
 // (px) than 4 waves x 8, so more waves per SIMD hide the gather latency
@@ -1469,7 +1489,7 @@ template <int ND, bool V3D, bool KICK, bool SORT>
 __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PINC_PUSH_WPE))) void k_push(PushArgs a) {
 	constexpr int NC = 1 << ND;
 	constexpr int NW = kPushThreads / 64;
-	__shared__ double rhoL[kRhoBoxCap];
+	__shared__ double rhoL[kRhoLds];
 	__shared__ double eL[KICK ? kEBoxCap * ND : 1];
 	__shared__ int cntIn[SORT ? kInCellCap : 1];
 	__shared__ int cntOut[kOutCellCap];
@@ -1595,11 +1615,17 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 
 	PUSH_TS(1);
 	// ---- phase B: LDS setup (zero the accumulators, stage E)
-	for (int t = threadIdx.x; t < rB.vol; t += kPushThreads) rhoL[t] = 0.0;
+	// copies of the charge box (PINC_PUSH_COPIES): odd stride, so that the
+	// copies of a node fall in different LDS banks
+	const int rStride = rB.vol | 1;
+	int nCopy = 1;
+	while (nCopy < PINC_PUSH_COPIES && 2 * nCopy * rStride <= kRhoLds) nCopy *= 2;
+	const int myCopy = (lane & (nCopy - 1)) * rStride;
+	for (int t = threadIdx.x; t < (PINC_PUSH_COPIES ? nCopy * rStride : rB.vol); t += kPushThreads) rhoL[t] = 0.0;
 	if (SORT)
 		for (int t = threadIdx.x; t < iB.vol; t += kPushThreads) cntIn[t] = 0;
 	for (int t = threadIdx.x; t < oB.vol; t += kPushThreads) cntOut[t] = 0;
-	if (KICK) {
+	if (KICK && !(PINC_PUSH_SKIP & 2)) {
 		for (int t = threadIdx.x; t < eB.vol; t += kPushThreads) {
 			int c[3] = {0, 0, 0};
 			eB.coords(t, c, ND);
@@ -1666,6 +1692,18 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 
 	PUSH_TS(3);
 	// ---- phase D: kick, drift, classify (unsorted: store)
+	// value offsets of the 2^ND corners in the staged E box (block-uniform)
+	int eoffs[NC];
+#pragma unroll
+	for (int c = 0; c < NC; c++) {
+		int o = 0, st = 1;
+#pragma unroll
+		for (int d = 0; d < ND; d++) {
+			o += ((c >> d) & 1) ? st : 0;
+			st *= eB.n[d];
+		}
+		eoffs[c] = o * ND;
+	}
 	double ke = 0.0;
 	int cnt = 0, bad = 0;
 	unsigned dep = 0;
@@ -1682,20 +1720,23 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 				dec[d] = p[k][d] - j[d];
 				comp[d] = 1 - dec[d];
 			}
+			// all 2^ND corners in the staged box: one unsigned compare per
+			// dimension, evaluated without short-circuit branches
 			bool inE = eB.vol > 0;
 #pragma unroll
-			for (int d = 0; d < ND; d++) inE = inE && j[d] >= eB.lo[d] && j[d] + 1 < eB.lo[d] + eB.n[d];
+			for (int d = 0; d < ND; d++) inE &= (unsigned)(j[d] - eB.lo[d]) < (unsigned)(eB.n[d] - 1);
 			double e[NC][ND];
-			if (inE) {
-				const int l0 = eB.index(j, ND);
+			if (PINC_PUSH_SKIP & 2) {
 #pragma unroll
-				for (int c = 0; c < NC; c++) {
-					int l = l0;
+				for (int c = 0; c < NC; c++)
 #pragma unroll
-					for (int d = 0; d < ND; d++) l += ((c >> d) & 1) ? (d == 0 ? 1 : (d == 1 ? eB.n[0] : eB.n[0] * eB.n[1])) : 0;
+					for (int q = 0; q < ND; q++) e[c][q] = 0.0;
+			} else if (inE) {
+				const double *eb = eL + mul24(eB.index(j, ND), ND);
 #pragma unroll
-					for (int q = 0; q < ND; q++) e[c][q] = eL[l * ND + q];
-				}
+				for (int c = 0; c < NC; c++)
+#pragma unroll
+					for (int q = 0; q < ND; q++) e[c][q] = eb[eoffs[c] + q];
 			} else {
 				int o[3][2];
 #pragma unroll
@@ -1928,11 +1969,12 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	auto box_cell = [&](const int *j) -> int {
 		bool in = rB.vol > 0;
 #pragma unroll
-		for (int d = 0; d < ND; d++) in = in && j[d] >= rB.lo[d] && j[d] + 1 < rB.lo[d] + rB.n[d];
+		for (int d = 0; d < ND; d++) in &= (unsigned)(j[d] - rB.lo[d]) < (unsigned)(rB.n[d] - 1);
 		return in ? rB.index(j, ND) : -1;
 	};
 	auto add8 = [&](const int *j, int l0, const double *w) {
 		if (l0 >= 0) {
+			if (PINC_PUSH_COPIES) l0 += myCopy;
 #pragma unroll
 			for (int c = 0; c < NC; c++) atomicAdd(&rhoL[l0 + coff[c]], w[c]);
 		} else {
@@ -1996,7 +2038,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	// pass covers the pair's 128 particles; the second particle of a pair
 	// that straddles a cell adds its weights one by one
 #pragma unroll
-	for (int k = 0; k < kPushItems; k += 2) {
+	for (int k = 0; k < ((PINC_PUSH_SKIP & 1) ? 0 : kPushItems); k += 2) {
 		const bool m0 = (dep >> k) & 1u, m1 = (dep >> (k + 1)) & 1u;
 		int j[3] = {0, 0, 0}, j1[3] = {0, 0, 0};
 		double w[8], w1[8];
@@ -2017,7 +2059,11 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 			key = key1;
 		}
 		const int l0 = (m0 || m1) ? box_cell(j) : -1;
-		deposit_pass(m0 || m1, j, w, key, l0);
+		if (PINC_PUSH_COPIES) {
+			if (m0 || m1) add8(j, l0, w);
+		} else {
+			deposit_pass(m0 || m1, j, w, key, l0);
+		}
 		if (m0 && m1 && !merge) add8(j1, box_cell(j1), w1);
 	}
 
@@ -2037,8 +2083,10 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 		if (t) atomicAdd(a.moved, (unsigned long long)t);
 	}
 	// flush: one global atomic per touched node / output cell
-	for (int t = threadIdx.x; t < rB.vol; t += kPushThreads) {
+	for (int t = threadIdx.x; t < ((PINC_PUSH_SKIP & 4) ? 0 : rB.vol); t += kPushThreads) {
 		double v = rhoL[t];
+		if (PINC_PUSH_COPIES)
+			for (int c = 1; c < nCopy; c++) v += rhoL[c * rStride + t];
 		if (v == 0.0) continue;
 		int c[3] = {0, 0, 0};
 		rB.coords(t, c, ND);
