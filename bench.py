@@ -266,6 +266,7 @@ def main() -> int:
     cycles = sim.cycles - c0
     n_local = sim.total_particles()
     ke, pe, _ = sim.energy()
+    mg_levels = sim.mg_levels
 
     dt_max = dt
     n_total = n_local
@@ -329,9 +330,10 @@ def main() -> int:
             "decomposition": f"1,1,{world}",
             "layout": args.layout + (f" (tile sort every {args.sort_interval} steps)" if args.layout == "tiled" else ""),
             "poisson": ("spectral (sSolver, rocFFT r2c/c2r, global grid)" if c3 else
-                        "multigrid mgVRecursive, 5 levels, RB Gauss-Seidel 10/10/10, "
-                        + ("native mode (correction scheme, coarse h^2 factor)" if args.mg == "native"
-                           else "reference algorithm (parity mode)")),
+                        f"multigrid mgVRecursive, {mg_levels} levels ({S}^3 down to {S >> (mg_levels - 1)}^3), "
+                        "RB Gauss-Seidel 10/10/10, "
+                        + ("native mode (correction scheme, coarse h^2 factor; the ini's 5 levels extended)"
+                           if args.mg == "native" else "reference algorithm (parity mode)")),
         },
         "poisson_ms_per_step": solve_ms,
         "push_deposit_ms_per_step": push_ms,

@@ -201,6 +201,7 @@ long mgCycleCount(const MultigridSolver *solver);
  * mgHistory copies it out and returns the cycle count of that solve */
 void mgSetLimit(MultigridSolver *solver, long maxCycles, long histCap);
 long mgHistory(const MultigridSolver *solver, double *out, long cap);
+int mgLevels(const MultigridSolver *solver);
 
 /* ---------------------------------------------------------- spectral -- */
 /* spectral.c:14-115; N-D extension of the reference's 1-D solver on rocFFT */
@@ -279,6 +280,7 @@ long pinc_sim_cycles(const PincSim *sim);
 /* mgSetLimit / mgHistory of the simulation's multigrid solver (-1 if the
  * Poisson solver is spectral) */
 int pinc_sim_mg_limit(PincSim *sim, long maxCycles, long histCap);
+int pinc_sim_mg_levels(PincSim *sim);  /* levels of the multigrid hierarchy in use */
 long pinc_sim_mg_history(PincSim *sim, double *out, long cap);
 int pinc_sim_nspecies(const PincSim *sim);
 int pinc_sim_ndims(const PincSim *sim);

@@ -1257,7 +1257,10 @@ constexpr int kPushGroupMin = PINC_PUSH_GROUP_MIN;
 #ifndef PINC_PUSH_COPIES
 #define PINC_PUSH_COPIES 8
 #endif
-constexpr int kRhoLds = PINC_PUSH_COPIES ? 2048 : 1024;
+#ifndef PINC_PUSH_RHO_LDS
+#define PINC_PUSH_RHO_LDS 2048
+#endif
+constexpr int kRhoLds = PINC_PUSH_COPIES ? PINC_PUSH_RHO_LDS : 1024;
 
 constexpr int kPushGroups = PINC_PUSH_GROUPS;
 // 8 waves x 4 particles per thread per PINC_CHUNK block: fewer live VGPRs
@@ -1489,7 +1492,9 @@ template <int ND, bool V3D, bool KICK, bool SORT>
 __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PINC_PUSH_WPE))) void k_push(PushArgs a) {
 	constexpr int NC = 1 << ND;
 	constexpr int NW = kPushThreads / 64;
-	__shared__ double rhoL[kRhoLds];
+	// the sorting push keeps its LDS at 40 KB (4 blocks per CU): fewer copies
+	constexpr int RL = SORT ? 1024 : kRhoLds;
+	__shared__ double rhoL[RL];
 	__shared__ double eL[KICK ? kEBoxCap * ND : 1];
 	__shared__ int cntIn[SORT ? kInCellCap : 1];
 	__shared__ int cntOut[kOutCellCap];
@@ -1619,7 +1624,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	// copies of a node fall in different LDS banks
 	const int rStride = rB.vol | 1;
 	int nCopy = 1;
-	while (nCopy < PINC_PUSH_COPIES && 2 * nCopy * rStride <= kRhoLds) nCopy *= 2;
+	while (nCopy < PINC_PUSH_COPIES && 2 * nCopy * rStride <= RL) nCopy *= 2;
 	const int myCopy = (lane & (nCopy - 1)) * rStride;
 	for (int t = threadIdx.x; t < (PINC_PUSH_COPIES ? nCopy * rStride : rB.vol); t += kPushThreads) rhoL[t] = 0.0;
 	if (SORT)

@@ -154,6 +154,8 @@ void mgSetLimit(MultigridSolver *S, long maxCycles, long histCap) {
 	S->histN = 0;
 }
 
+int mgLevels(const MultigridSolver *S) { return S->nLevels; }
+
 long mgHistory(const MultigridSolver *S, double *out, long cap) {
 	long n = S->histN < S->histCap ? S->histN : S->histCap;
 	if (out)

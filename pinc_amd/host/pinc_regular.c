@@ -347,6 +347,8 @@ int pinc_sim_mg_limit(PincSim *S, long maxCycles, long histCap) {
 	return 0;
 }
 
+int pinc_sim_mg_levels(PincSim *S) { return S->spectral ? 0 : mgLevels(S->solver); }
+
 long pinc_sim_mg_history(PincSim *S, double *out, long cap) {
 	if (S->spectral) return -1;
 	return mgHistory(S->solver, out, cap);

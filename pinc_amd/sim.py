@@ -102,6 +102,11 @@ class Sim:
         if HOST.pinc_sim_mg_limit(self._h, max_cycles, hist_cap):
             raise RuntimeError("mg_limit: the Poisson solver is not multigrid")
 
+    @property
+    def mg_levels(self) -> int:
+        """Levels of the multigrid hierarchy in use (0 for the spectral solver)."""
+        return HOST.pinc_sim_mg_levels(self._h)
+
     def mg_history(self) -> np.ndarray:
         """RMS residual after each V-cycle of the last solve (mgHistory)."""
         n = HOST.pinc_sim_mg_history(self._h, None, 0)

@@ -1,7 +1,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-O=gpurun_out/r02c
+O=gpurun_out/${1:-r02c}
 mkdir -p $O
 timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_WAVE_CYCLES \
 	-d $O/pmcA -o bench -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > $O/pmcA.json 2> $O/pmcA.err &&
