@@ -69,6 +69,7 @@ def _load() -> C.CDLL:
         "oo_interior_nodes": (None, [vp, C.c_int, vp]),
         "oo_collected": (C.c_double, [vp, C.c_int]),
         "oo_rho_obj": (None, [vp, vp]),
+        "oo_set_reference_divisor": (None, [vp, C.c_int]),
     }
     for n, (r, a) in sigs.items():
         f = getattr(lib, n)
@@ -249,6 +250,11 @@ class Objects:
 
     def collect(self):
         LIB.oo_collect(self._h, self.w._h)
+
+    def reference_divisor(self, on: bool = True):
+        """Spread collected charge with object.c:476-478's cumulative
+        divisor 1/lookupSurfaceOffset[a+1] (the reference's defect)."""
+        LIB.oo_set_reference_divisor(self._h, int(on))
 
     def init_collect(self):
         LIB.oo_init_collect(self._h, self.w._h)

@@ -23,7 +23,19 @@
  *   - the swapped-in last particle is re-tested (the reference's loop moves
  *     on, leaving it inside the object for a step);
  *   - object.c:243 resets mgRho at lookupSurf[inode] without the object's
- *     offset (wrong node for every object but the first).
+ *     offset (wrong node for every object but the first);
+ *   - object.c:476-478 spreads object a's collected charge with
+ *     invNrSurfNod[a] = 1/lookupSurfaceOffset[a+1], the CUMULATIVE surface
+ *     count of objects 0..a (the commented-out line above it divides by the
+ *     total), so every object after the first loses part of its charge;
+ *     here the divisor is object a's own surface count (the reference's
+ *     form is kept behind oo_set_reference_divisor for the test that pins
+ *     the difference, tests/test_oracle_objects.py);
+ *   - the reference spreads each rank's own count over that rank's own
+ *     surface nodes, with no reduction; the build sums the count over the
+ *     ranks and spreads it over all of the object's surface nodes (the same
+ *     for an object inside one subdomain; this checker has one).
+ * The spreading keeps the reference's expression, count * (1.0/divisor).
  * Parity of a build against this restatement is therefore parity against
  * the algorithm, pinned by its invariants (tests/test_oracle_objects.py):
  * after the correction the surface is an equipotential at phi_c, the
@@ -34,6 +46,7 @@
 
 struct OObj {
 	int nObjects;
+	int refDivisor;       /* 1: object.c:476-478's cumulative divisor (tests only) */
 	long nNodes;          /* nodes of the padded grid */
 	double *mask;         /* node values (object id, 0 = vacuum) */
 	int *objOfNode;       /* interior object of a true node (0 = none) */
@@ -276,12 +289,17 @@ void oo_collect(OObj *o, OWorld *w) {
 		}
 	}
 	for (int a = 0; a < o->nObjects; a++) {
-		long n = o->surfaceOff[a + 1] - o->surfaceOff[a];
+		long n = o->refDivisor ? o->surfaceOff[a + 1] : o->surfaceOff[a + 1] - o->surfaceOff[a];
+		double inv = 1.0 / (double)n;
 		o->collected[a] += cnt[a];
-		for (long b = o->surfaceOff[a]; b < o->surfaceOff[a + 1]; b++) o->rhoObj.val[o->surface[b]] += cnt[a] / n;
+		for (long b = o->surfaceOff[a]; b < o->surfaceOff[a + 1]; b++) o->rhoObj.val[o->surface[b]] += cnt[a] * inv;
 	}
 	free(cnt);
 }
+
+/* object.c's own divisor, 1/lookupSurfaceOffset[a+1] (the defect named in
+ * the header), for the test that pins the corrected one */
+void oo_set_reference_divisor(OObj *o, int on) { o->refDivisor = on; }
 
 /* ctypes accessors */
 int oo_nobjects(const OObj *o) { return o->nObjects; }

@@ -88,9 +88,13 @@ __global__ __launch_bounds__(kThreads) void k_gs_pass(double *__restrict__ phi,
 			v *= 1. / (2 * ND);
 		}
 		phi[g] = v;
-		long go = g + (xo - c[0]);
-		acc += v + (phi[go] - mu);
+		if (partial) {
+			long go = g + (xo - c[0]);
+			acc += v + (phi[go] - mu);
+		}
 	}
+	// native mode passes no partials: no neutralisation after each colour
+	if (!partial) return;
 	double t = block_sum(acc, red);
 	if (threadIdx.x == 0) partial[blockIdx.x] = t;
 }

@@ -154,6 +154,7 @@ struct MultigridSolver {
 	 * optional cap on the cycles of one solve (0 = loop until converged) */
 	double *hist;
 	long histCap, histN, maxCycles;
+	long fusedMin;     /* smallest level (points) smoothed by the fused sweeps */
 };
 
 /* collectives over RCCL or the host transport (pinc_comm.c) */

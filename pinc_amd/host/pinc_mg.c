@@ -79,6 +79,10 @@ MultigridSolver *mgAllocSolver(const dictionary *ini, Grid *rho, Grid *phi) {
 	 * C4, the gaps between dependent kernels are GPU-side) */
 	S->useGraph = S->native && iniHas(ini, "multigrid:graph") && iniGetInt(ini, "multigrid:graph");
 	S->cycleGraph = NULL;
+	/* native mode: levels of at least fusedMin points smooth with the
+	 * z-marching fused sweeps (two iterations per launch), smaller ones
+	 * colour by colour (PINC_MG_FUSED_MIN overrides, experiments) */
+	S->fusedMin = getenv("PINC_MG_FUSED_MIN") ? atol(getenv("PINC_MG_FUSED_MIN")) : (1L << 23);
 	for (int d = 1; d <= nd; d++)
 		if (rho->trueSize[d] % (1 << S->nLevels))
 			msg(ERROR, "All elements in grid:trueSize must be a multiple of 2^mgLevels=%d", 1 << S->nLevels);
@@ -181,7 +185,7 @@ static void smooth_native(MultigridSolver *S, int q, int nIter, int nd3) {
 	 * 256^3: 128^3 and below are as fast, launch-latency bound, as two
 	 * passes; rechecked with the 32x8 two-ahead sweep) */
 	int fused = nd3 && L.nd == 3 && L.T[0] % 16 == 0 && L.T[1] % 16 == 0 && L.T[2] % 16 == 0 &&
-	            S->N[q] >= (1L << 23);
+	            S->N[q] >= S->fusedMin;
 	int k = 0;
 	/* two iterations per launch (pinc_hip_gs_sweep2x) in pairs, so that the
 	 * ping-pong ends in phi */
@@ -207,7 +211,7 @@ static void smooth_native(MultigridSolver *S, int q, int nIter, int nd3) {
 	for (; k < nIter; k++) {
 		for (int pass = 0; pass < 2; pass++) {
 			int nb = 0;
-			pinc_check(pinc_hip_gs_pass(S->phi[q], S->rho[q], L, pass, nd3, NULL, g_pinc.dScratch, &nb, g_pinc.stream),
+			pinc_check(pinc_hip_gs_pass(S->phi[q], S->rho[q], L, pass, nd3, NULL, NULL, &nb, g_pinc.stream),
 			           "gs pass");
 		}
 	}

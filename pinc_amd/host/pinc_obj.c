@@ -23,9 +23,20 @@
  *   pinc_obj_add_rho      gAddTo(rho, rhoObj) (main.c:230)
  *   pinc_obj_apply        oApplyCapacitanceMatrix (object.c:301-366)
  *
- * The checker is the object restatement under oracle/, with the same three corrections of
- * reference defects (pCut's index, the re-test of the swapped-in particle,
- * the unit-charge reset); tests/test_gpu_objects.py.
+ * The checker is the object restatement under oracle/ (oracle/orc_obj.c),
+ * with the same five corrections of reference defects, named in its header:
+ *   1. pCut gets the particle, not the node index (object.c:499);
+ *   2. the particle swapped into a removed one's slot is re-tested;
+ *   3. the unit charge is reset at the object's own surface node
+ *      (object.c:243);
+ *   4. collected charge is spread with 1/(object a's surface nodes), not
+ *      object.c:476-478's 1/lookupSurfaceOffset[a+1] (cumulative: objects
+ *      after the first lose charge; tests/test_oracle_objects.py pins both);
+ *   5. with several ranks an object's count is summed over the ranks and
+ *      spread over all of its surface nodes (the reference spreads each
+ *      rank's count over that rank's surface nodes, no reduction: the same
+ *      for an object inside one subdomain).
+ * Device parity: tests/test_gpu_objects.py.
  */
 #define _GNU_SOURCE
 #include "pinc_internal.h"
@@ -154,7 +165,9 @@ static PincObj *obj_create(const dictionary *ini, const pinc_geom_t *g) {
 	/* surface (object.c:368-458): global true nodes with 1..7 of the 8
 	 * nodes at offsets {0,-1}^3 in the object, in global z,y,x order (for
 	 * z-slabs the reference's rank-then-local order) */
-	long nMax = (long)T[0] * T[1] * T[2] * (nObj > 0 ? nObj : 1);
+	/* the lists grow geometrically (a surface is a thin shell: sizing them
+	 * by the grid would hold GBs at 256^3 with several objects) */
+	long nMax = 4096;
 	long *dIdx = malloc(nMax * sizeof(long)), *gIdx = malloc(nMax * sizeof(long));
 	o->surfNode = malloc(nMax * sizeof(long));
 	o->surfOff = calloc(nObj + 1, sizeof(long));
@@ -166,6 +179,13 @@ static PincObj *obj_create(const dictionary *ini, const pinc_geom_t *g) {
 				int d = 0;
 				for (int q = 0; q < 8; q++) d += ID(x - (q & 1), y - ((q >> 1) & 1), z - (q >> 2)) == a;
 				if (d > 0 && d < 8) {
+					if (o->nSurf == nMax) {
+						nMax *= 2;
+						dIdx = realloc(dIdx, nMax * sizeof(long));
+						gIdx = realloc(gIdx, nMax * sizeof(long));
+						o->surfNode = realloc(o->surfNode, nMax * sizeof(long));
+						if (!dIdx || !gIdx || !o->surfNode) msg(ERROR, "objects: out of host memory");
+					}
 					o->surfNode[o->nSurf] = x + (long)T[0] * (y + (long)T[1] * z);
 					gIdx[o->nSurf] = (long)z * ps + (long)y * T[0] + x;
 					int zl = z - g->off;
@@ -178,6 +198,7 @@ static PincObj *obj_create(const dictionary *ini, const pinc_geom_t *g) {
 #undef ID
 	free(mk);
 	if (!o->nSurf) msg(ERROR, "objects: the mask has no surface nodes");
+	o->surfNode = realloc(o->surfNode, o->nSurf * sizeof(long));
 	pinc_check(pinc_hip_malloc((void **)&o->dInside, o->nNodes), "objects");
 	pinc_check(pinc_hip_h2d(o->dInside, inside, o->nNodes, g_pinc.stream), "objects");
 	pinc_check(pinc_hip_malloc((void **)&o->dSurf, o->nSurf * sizeof(long)), "objects");
@@ -255,6 +276,10 @@ void pinc_obj_capacitance(PincObj *o, Grid *rho, Grid *phi, void *solver,
 		long na = o->surfOff[a + 1] - o->surfOff[a];
 		o->capOff[a + 1] = o->capOff[a] + na * na;
 	}
+	/* a second call (oComputeCapacitanceMatrix again) replaces the matrix */
+	pinc_hip_free(o->dM);
+	o->dM = NULL;
+	free(o->wRow);
 	pinc_check(pinc_hip_malloc((void **)&o->dM, o->capOff[o->nObj] * sizeof(double)), "cap matrix");
 	o->wRow = calloc(n, sizeof(double));
 	/* objects:capacitance = green (extension): the periodic, neutralised

@@ -27,4 +27,9 @@ def built():
     # importing pinc_amd before torch exits cleanly
     from pinc_amd.build import build
     subprocess.run(["make", "-s", "-C", str(ROOT / "oracle"), "-j4"], check=True)
-    return build()
+    out = build()
+    # the checker's stencil and per-rank loops use the job's CPU share
+    # (results are bit-identical for any thread count, oracle/orc.h)
+    import orc
+    orc.LIB.orc_set_threads(max(1, min(16, len(os.sched_getaffinity(0)))))
+    return out

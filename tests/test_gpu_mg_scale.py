@@ -14,7 +14,6 @@ summation order of the neutralisation means and of the norm, so the
 histories agree to round-off until the residual itself approaches
 round-off.
 """
-import os
 import sys
 from pathlib import Path
 
@@ -28,10 +27,8 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(scope="module", autouse=True)
-def oracle_threads(built):
-    import orc
-    n = min(16, len(os.sched_getaffinity(0)))
-    orc.LIB.orc_set_threads(n)
+def _built(built):  # the checker's thread count is set there (conftest.py)
+    return built
 
 
 def _compare(g, o, rtol_hist, rtol_phi, tail_floor=1e-8):

@@ -213,3 +213,86 @@ def test_green_capacitance_matches_solves(built):
     assert (a0, a1) == (b0, b1)
     assert abs(ka - kb) <= 1e-7 * abs(ka) and abs(pa - pb) <= 1e-7 * abs(pa)
     assert np.max(np.abs(fa - fb)) <= 1e-6 * np.abs(fa).max()
+
+
+GOLD_MASKS = __import__("pathlib").Path(__file__).resolve().parent / "golden" / "masks"
+
+
+@pytest.mark.parametrize("name", ["sphere.grid.h5", "test_boxbox.h5_backup", "test_box_sphere.h5_backup",
+                                  "test_twobox32.h5_backup"])
+def test_reference_masks_match_checker(built, name):
+    """The object masks that ship with the reference (sphere.grid.h5 and the
+    32^3 test_*.h5_backup files, committed unchanged under
+    tests/golden/masks/), read by objects:file as oReadH5 reads them
+    (object.c:727-756: dataset /Object [nz, ny, nx, 1]): lookup tables,
+    capacitance matrices, collection and corrections against the checker
+    fed with the same mask, two steps."""
+    from pinc_amd import Sim
+    from pinc_amd.sim import h5_read
+    f = str(GOLD_MASKS / name)
+    mask = h5_read(f, "/Object")[..., 0]
+    T = tuple(reversed(mask.shape))
+    cfg = configs.config("cold3d", true_size=T, nsub=(1, 1, 1))
+    cfg["multigrid"]["mgLevels"] = "3"
+    cfg["population"]["fused"] = "0"
+    cfg["population"]["nParticles"] = "8 pc"
+    cfg["population"]["nAlloc"] = "12 pc"
+    cfg["objects"] = {"file": f}
+    ini = configs.write_ini(cfg)
+    w = orc.World(ini)
+    w.init()
+    ob = orc.Objects(w, mask)
+    assert ob.n == int(mask.max())
+    ob.capacitance()
+    ob.init_collect()
+    w.init_fields()
+    with Sim(ini) as s:
+        s.init()
+        for sp in range(2):
+            assert s.count(sp) == w.count(sp)
+        for k in range(2):
+            ob.step()
+            s.step()
+            ke_o, pe_o = w.energy()
+            ke, pe, _ = s.energy()
+            for sp in range(2):
+                assert s.count(sp) == w.count(sp), (k, sp)
+            assert abs(ke - ke_o) <= 1e-7 * abs(ke_o), (k, ke, ke_o)
+            assert abs(pe - pe_o) <= 1e-7 * abs(pe_o), (k, pe, pe_o)
+        phi_g = s.grid(1)[1:-1, 1:-1, 1:-1]
+        phi_o = w.grid(1)[1:-1, 1:-1, 1:-1]
+        assert np.max(np.abs(phi_g - phi_o)) <= 1e-7 * np.abs(phi_o).max()
+
+
+@pytest.mark.parametrize("name", ["test_box64.h5_backup", "test_twobox.h5_backup"])
+def test_reference_masks_64_green_equals_solve(built, name):
+    """The 64^3 reference masks on the device: the capacitance matrix by one
+    solve per surface node (the reference's method) and by translation
+    (objects:capacitance = green) give the same run (counts exact, energies
+    to the solver tolerance), and the particles inside the objects are gone."""
+    from pinc_amd import Sim
+    from pinc_amd.sim import h5_read
+    f = str(GOLD_MASKS / name)
+    mask = h5_read(f, "/Object")[..., 0]
+    T = tuple(reversed(mask.shape))
+    res = []
+    for mode in ("solve", "green"):
+        cfg = configs.config("cold3d", true_size=T, nsub=(1, 1, 1))
+        cfg["multigrid"]["mgLevels"] = "4"
+        cfg["population"]["fused"] = "0"
+        cfg["population"]["nParticles"] = "4 pc"
+        cfg["population"]["nAlloc"] = "6 pc"
+        cfg["objects"] = {"file": f, "capacitance": mode}
+        with Sim(configs.write_ini(cfg)) as s:
+            s.init()
+            s.step(2)
+            inside = 0
+            for sp in range(2):
+                p, _ = s.particles(sp)
+                j = p.astype(np.int64) - 1   # lower node, true-node coordinates
+                inside += int((mask[j[:, 2] % T[2], j[:, 1] % T[1], j[:, 0] % T[0]] > 0).sum())
+            res.append((s.count(0), s.count(1), *s.energy()[:2], inside))
+    (a0, a1, ka, pa, ia), (b0, b1, kb, pb, ib) = res
+    assert (a0, a1) == (b0, b1)
+    assert ia == 0 and ib == 0
+    assert abs(ka - kb) <= 1e-7 * abs(ka) and abs(pa - pb) <= 1e-7 * abs(pa)

@@ -128,3 +128,33 @@ def test_object_steps_run():
     ob.step(3)
     ke, pe = w.energy()
     assert np.isfinite(ke) and np.isfinite(pe)
+
+
+@pytest.mark.parametrize("reference", [False, True])
+def test_collected_charge_divisor(reference):
+    """object.c:476-478 spreads object a's collected charge with
+    1/lookupSurfaceOffset[a+1], the cumulative surface count of objects
+    0..a: object 0 keeps its charge, every later object loses the fraction
+    its predecessors' surfaces take.  The build (pinc_obj.c) and this
+    checker divide by the object's own surface count (a named correction,
+    DESIGN.md section 11): rhoObj over each object's surface sums to the
+    charge it collected."""
+    T = (24, 16, 16)
+    w = _world(T)
+    w.init()
+    mask = _sphere(T, (6.0, 8.0, 8.0), 3.0) + 2 * _sphere(T, (17.0, 8.0, 8.0), 3.5)
+    ob = orc.Objects(w, mask)
+    assert ob.n == 2
+    ob.reference_divisor(reference)
+    ob.collect()
+    ro = ob.rho_obj().ravel()
+    n0, n1 = len(ob.surface(0)), len(ob.surface(1))
+    s0, s1 = ro[ob.surface(0)].sum(), ro[ob.surface(1)].sum()
+    c0, c1 = ob.collected(0), ob.collected(1)
+    assert abs(c0) > 0 and abs(c1) > 0
+    assert s0 == pytest.approx(c0, rel=1e-12)
+    if reference:
+        assert s1 == pytest.approx(c1 * n1 / (n0 + n1), rel=1e-12)
+        assert abs(s1) < abs(c1)
+    else:
+        assert s1 == pytest.approx(c1, rel=1e-12)
