@@ -156,7 +156,7 @@ def main() -> int:
                     help="1: the tile sort rides in every sort-interval-th push (default); 0: separate sort pass")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-size", type=int, default=128)
-    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--cpu-steps", type=int, default=20)
     ap.add_argument("--host-transport", action="store_true",
                     help="rehearsal only: N ranks share GPU 0 and the collectives go through the gloo host "
                          "transport (RCCL refuses two ranks on one device); never the measured configuration")

@@ -218,12 +218,12 @@ def test_green_capacitance_matches_solves(built):
 GOLD_MASKS = __import__("pathlib").Path(__file__).resolve().parent / "golden" / "masks"
 
 
-@pytest.mark.parametrize("name", ["sphere.grid.h5", "test_boxbox.h5_backup", "test_box_sphere.h5_backup",
-                                  "test_twobox32.h5_backup"])
+@pytest.mark.parametrize("name", ["sphere.grid.h5", "test_boxbox.h5_backup"])
 def test_reference_masks_match_checker(built, name):
-    """The object masks that ship with the reference (sphere.grid.h5 and the
-    32^3 test_*.h5_backup files, committed unchanged under
-    tests/golden/masks/), read by objects:file as oReadH5 reads them
+    """The object masks that ship with the reference (all of them are
+    committed unchanged under tests/golden/masks/; the single object and a
+    two-object 32^3 file here, the checker's capacitance solves keep the
+    rest out of the suite's time), read by objects:file as oReadH5 reads them
     (object.c:727-756: dataset /Object [nz, ny, nx, 1]): lookup tables,
     capacitance matrices, collection and corrections against the checker
     fed with the same mask, two steps."""
