@@ -1257,6 +1257,16 @@ constexpr int kPushGroupMin = PINC_PUSH_GROUP_MIN;
 #ifndef PINC_PUSH_COPIES
 #define PINC_PUSH_COPIES 8
 #endif
+// 1: a thread's particles are consecutive in memory, with plain loads and
+// stores (measured at C4, mean over the sort cycle, per species launch:
+// 27.1 ms against 28.3 for lane pairs 512 apart with nontemporal access;
+// this pattern with nontemporal loads and stores 42 ms, nontemporal stores
+// only 33.7, nontemporal loads only 30.1 -- each wave instruction covers
+// every other 16 B of 2 KB and the next one the rest, which must meet in
+// L2; PMC traffic 122 GB per launch against 110 GB)
+#ifndef PINC_PUSH_CONSEC
+#define PINC_PUSH_CONSEC 1
+#endif
 #ifndef PINC_PUSH_RHO_LDS
 #define PINC_PUSH_RHO_LDS 2048
 #endif
@@ -1530,7 +1540,15 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	const long base = (long)chunk * kPushChunk;
 	// item k of a thread: particles in lane-contiguous pairs (16-B loads and
 	// stores, 1 KiB per wave instruction), pair k/2 of the thread
+#if PINC_PUSH_CONSEC
+	// the kPushItems particles of a thread are consecutive (two 16-B loads per
+	// array and thread: a wave instruction covers every other 16 B of 2 KB,
+	// the next one the rest, through L2), so a thread's particles mostly share
+	// a cell and their charge is summed in the thread before the LDS adds
+	auto item = [&](int k) -> long { return base + (long)(kPushItems * threadIdx.x + k); };
+#else
 	auto item = [&](int k) -> long { return base + (long)((k >> 1) * (2 * kPushThreads) + 2 * threadIdx.x + (k & 1)); };
+#endif
 	// pairs are 16-B aligned when every species array is (the species
 	// offset iStart is even); otherwise one 8-B access per particle
 	bool al = true;
@@ -1554,8 +1572,13 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 		for (int d = 0; d < ND; d++) {
 			if (ok1 && al) {
 				// streamed once per step (far beyond L2/MALL): non-temporal
+#if PINC_PUSH_CONSEC
+				const dvec2 x = *reinterpret_cast<const dvec2 *>(a.xi[d] + i);
+				const dvec2 v = *reinterpret_cast<const dvec2 *>(a.vi[d] + i);
+#else
 				const dvec2 x = __builtin_nontemporal_load(reinterpret_cast<const dvec2 *>(a.xi[d] + i));
 				const dvec2 v = __builtin_nontemporal_load(reinterpret_cast<const dvec2 *>(a.vi[d] + i));
+#endif
 				p[k][d] = x.x;
 				p[k + 1][d] = x.y;
 				vv[k][d] = v.x;
@@ -1846,9 +1869,14 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 #pragma unroll
 			for (int d = 0; d < ND; d++) {
 				if (ok1 && al) {
+#if PINC_PUSH_CONSEC
+					*reinterpret_cast<dvec2 *>(a.xo[d] + i) = dvec2{p[k][d], p[k + 1][d]};
+					if (wv) *reinterpret_cast<dvec2 *>(a.vo[d] + i) = dvec2{vv[k][d], vv[k + 1][d]};
+#else
 					__builtin_nontemporal_store(dvec2{p[k][d], p[k + 1][d]}, reinterpret_cast<dvec2 *>(a.xo[d] + i));
 					if (wv)
 						__builtin_nontemporal_store(dvec2{vv[k][d], vv[k + 1][d]}, reinterpret_cast<dvec2 *>(a.vo[d] + i));
+#endif
 				} else {
 					if (ok0) a.xo[d][i] = p[k][d];
 					if (ok0 && wv) a.vo[d][i] = vv[k][d];
@@ -2042,6 +2070,36 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	// share a cell: their weights are summed in the lane first, so one wave
 	// pass covers the pair's 128 particles; the second particle of a pair
 	// that straddles a cell adds its weights one by one
+#if PINC_PUSH_CONSEC && PINC_PUSH_COPIES
+	// consecutive particles of the thread: runs of one cell are summed in
+	// registers and added once (8 LDS atomics per run)
+	{
+		int jr[3] = {0, 0, 0}, keyr = -1;
+		double wr[8];
+		bool open = false;
+#pragma unroll
+		for (int k = 0; k < ((PINC_PUSH_SKIP & 1) ? 0 : kPushItems); k++) {
+			if (!((dep >> k) & 1u)) continue;
+			int jk[3] = {0, 0, 0};
+			double wk[8];
+			const int kk = weights(k, jk, wk);
+			if (open && kk == keyr) {
+#pragma unroll
+				for (int c = 0; c < 8; c++) wr[c] += wk[c];
+			} else {
+				if (open) add8(jr, box_cell(jr), wr);
+				open = true;
+				keyr = kk;
+#pragma unroll
+				for (int d = 0; d < 3; d++) jr[d] = jk[d];
+#pragma unroll
+				for (int c = 0; c < 8; c++) wr[c] = wk[c];
+			}
+		}
+		if (open) add8(jr, box_cell(jr), wr);
+	}
+	if (false)
+#endif
 #pragma unroll
 	for (int k = 0; k < ((PINC_PUSH_SKIP & 1) ? 0 : kPushItems); k += 2) {
 		const bool m0 = (dep >> k) & 1u, m1 = (dep >> (k + 1)) & 1u;
