@@ -73,7 +73,7 @@ def _cpu_threads() -> int:
     return max(1, min(aff, int(os.environ.get("OMP_NUM_THREADS", aff))))
 
 
-def _cpu_baseline(size: int, ppc: int, steps: int, native: bool) -> dict:
+def _cpu_baseline(size: int, ppc: int, steps: int, native: bool, workload: str = "c4") -> dict:
     """The oracle (plain-C restatement of the reference) on the host cores,
     on a bounded sample of the same workload: the warm plasma at size^3 with
     ppc particles per cell per species, decomposed into one z-slab per
@@ -89,14 +89,23 @@ def _cpu_baseline(size: int, ppc: int, steps: int, native: bool) -> dict:
     while nsub > 1 and (size % nsub or (size // nsub) % 2):
         nsub -= 1
     orc.LIB.orc_set_threads(threads)
-    cfg = configs.config("warm", true_size=(size, size, size // nsub), nsub=(1, 1, nsub), ppc=ppc,
-                         nalloc_pc=ppc + 8, levels=1 if native else 5)
-    if native:
+    nd = 2 if workload == "c2" else 3
+    if workload == "c2":
+        cfg = configs.config("c2")
+        cfg["grid"]["trueSize"] = f"{size},{size // nsub}"
+        cfg["grid"]["nSubdomains"] = f"1,{nsub}"
+        cfg["population"]["nParticles"] = f"{ppc} pc"
+        cfg["population"]["nAlloc"] = f"{ppc + 16} pc"
+        cfg["multigrid"]["mgLevels"] = "1" if native else cfg["multigrid"]["mgLevels"]
+    else:
+        cfg = configs.config("c3" if workload == "c3" else "warm", true_size=(size, size, size // nsub),
+                             nsub=(1, 1, nsub), ppc=ppc, nalloc_pc=ppc + 8, levels=1 if native else 5)
+    if native and cfg["methods"]["poisson"] == "mgSolver":
         cfg["multigrid"]["native"] = "1"
     ini = configs.write_ini(cfg)
     t_init = time.perf_counter()
     w = orc.World(ini)
-    w.init(perturb=False, maxwell=True, seed=20260101)
+    w.init(perturb=workload == "c2", maxwell=workload != "c2", seed=20260101)
     w.init_fields()
     t_init = time.perf_counter() - t_init
     n = sum(w.count(s, rank=r) for r in range(w.nranks) for s in range(2))
@@ -113,11 +122,12 @@ def _cpu_baseline(size: int, ppc: int, steps: int, native: bool) -> dict:
     push_ms = ph["move"] + ph["migrate"] + ph["deposit"] + ph["accelerate"]
     return {"value": n * steps / dt, "unit": "particle-updates/s", "cores": threads, "kind": "port",
             "nproc": os.cpu_count(), "cpu_share": len(os.sched_getaffinity(0)),
-            "sample": f"oracle (C restatement of the reference, OpenMP over {nsub} emulated z-slab ranks, "
-                      f"{threads} threads) on the same warm 3-D workload at {size}^3, {ppc} ppc x 2 species "
-                      f"({n} particles), {steps} steps; multigrid "
-                      + ("native mode as the GPU line" if native else "reference algorithm")
-                      + f", {levels} levels, {cyc:.0f} V-cycles/solve",
+            "sample": f"oracle (C restatement of the reference, OpenMP over {nsub} emulated slab ranks, "
+                      f"{threads} threads) on the same {workload.upper()} workload at {size}^{nd}, {ppc} ppc x 2 "
+                      f"species ({n} particles), {steps} steps; "
+                      + ("spectral solve (naive DFT restatement)" if cfg["methods"]["poisson"] == "sSolver" else
+                         "multigrid " + ("native mode as the GPU line" if native else "reference algorithm")
+                         + f", {levels} levels, {cyc:.0f} V-cycles/solve"),
             "seconds": dt, "init_s": t_init,
             "push_deposit_updates_per_s": n / (push_ms * 1e-3) if push_ms > 0 else None,
             "poisson_ms_per_step": ph["solve"], "mg_cycles_per_solve": cyc,
@@ -129,11 +139,12 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="c4", choices=["c4", "c3", "c5"],
+    ap.add_argument("--workload", default="c4", choices=["c4", "c3", "c5", "c2"],
                     help="c4: warm 3-D plasma, 256^3, 64 ppc, multigrid (BASELINE.json metric, default); "
                          "c3: Maxwellian 128^3, 32 ppc, spectral (rocFFT) Poisson solve; "
                          "c5: c4 plus an immersed sphere (object.c: charge collection, capacitance "
-                         "correction, second solve), unfused operators")
+                         "correction, second solve), unfused operators; "
+                         "c2: input/langmuir2D.ini at 128^2, 32 ppc (Langmuir perturbation, cold), multigrid")
     ap.add_argument("--size", type=int, default=None, help="global cells per dimension (c4: 256, c3: 128)")
     ap.add_argument("--ppc", type=int, default=None, help="particles per cell per species (c4: 64, c3: 32)")
     ap.add_argument("--mg", default="native", choices=["native", "reference"],
@@ -147,7 +158,7 @@ def main() -> int:
                     help="c5: capacitance matrix by one solve per surface node (the reference's, default) or "
                          "by translating one periodic response (objects:capacitance = green)")
     ap.add_argument("--sort-interval", type=int, default=8)
-    ap.add_argument("--sort-fraction", type=float, default=0.0,
+    ap.add_argument("--sort-fraction", type=float, default=0.8,
                     help="> 0: sort each species once this fraction of its particles left their cell since its "
                          "last sort (adaptive, per species; --sort-max pushes apart at most) instead of every "
                          "--sort-interval pushes")
@@ -199,15 +210,25 @@ def main() -> int:
 
     c3 = args.workload == "c3"
     c5 = args.workload == "c5"
+    c2 = args.workload == "c2"
     if args.size is None:
-        args.size = 128 if c3 else 256
+        args.size = 128 if (c3 or c2) else 256
     if args.ppc is None:
-        args.ppc = 32 if c3 else 64
+        args.ppc = 32 if (c3 or c2) else 64
     S = args.size
+    nd = 2 if c2 else 3
     if S % world:
         raise SystemExit("grid size must divide by the GPU count")
-    cfg = configs.config("c3" if c3 else "warm", true_size=(S, S, S // world), nsub=(1, 1, world), ppc=args.ppc,
-                         nalloc_pc=args.ppc + 8)
+    if c2:
+        # input/langmuir2D.ini + SURVEY.md 8(d)'s C2 overrides, slabs along y
+        cfg = configs.config("c2")
+        cfg["grid"]["trueSize"] = f"{S},{S // world}"
+        cfg["grid"]["nSubdomains"] = f"1,{world}"
+        cfg["population"]["nParticles"] = f"{args.ppc} pc"
+        cfg["population"]["nAlloc"] = f"{args.ppc + 16} pc"
+    else:
+        cfg = configs.config("c3" if c3 else "warm", true_size=(S, S, S // world), nsub=(1, 1, world), ppc=args.ppc,
+                             nalloc_pc=args.ppc + 8)
     if args.mg == "native":
         cfg["multigrid"]["native"] = "1"
     if c5:
@@ -231,8 +252,8 @@ def main() -> int:
         print(f"[bench rank {rank}] {msg}", file=sys.stderr, flush=True)
 
     t_init0 = time.perf_counter()
-    log(f"creating {S}^3 x {args.ppc} ppc on {world} GPU(s)")
-    sim = Sim(ini, rank=rank, nranks=world, device=local, comm_id=comm_id, maxwell=True, perturb=False,
+    log(f"creating {S}^{nd} x {args.ppc} ppc on {world} GPU(s)")
+    sim = Sim(ini, rank=rank, nranks=world, device=local, comm_id=comm_id, maxwell=not c2, perturb=c2,
               device_init=True, seed=20260101, timing=True, transport=transport)
     sim.init()
     sim.sync()
@@ -301,7 +322,8 @@ def main() -> int:
     dom = max(kernels, key=lambda k: kernels[k]["est_ms_per_step"])
     dk = kernels[dom]
     # push+deposit against SURVEY.md 8(d): 144 B per particle-update (3-D)
-    pd_bytes = 144.0 * n_local + 32.0 * S ** 3 / world
+    # 144 B per 3-D particle-update (96 B in 2-D) + 32 B per cell
+    pd_bytes = (96.0 if c2 else 144.0) * n_local + 32.0 * S ** nd / world
     pd_gbs = pd_bytes / (push_ms * 1e-3) / 1e9 if push_ms > 0 else 0.0
 
     result = {
@@ -318,19 +340,23 @@ def main() -> int:
         "dtype": "f64",
         "data": "synthetic (lattice positions, Maxwellian velocities from a seeded counter RNG)",
         "config": {
-            "workload": ("C3 Maxwellian 3-D two-species plasma" if c3 else
-                         f"C5 warm 3-D two-species plasma around an immersed sphere (radius {S / 32:g} cells)"
-                         if c5 else "C4 warm 3-D two-species plasma")
-                        + f", {S}^3 grid, {args.ppc} ppc per species "
-                        f"({n_total} particles), 1D slab decomposition 1,1,{world}",
-            "grid": [S, S, S],
+            "workload": (f"C2 Langmuir 2-D two-species plasma (input/langmuir2D.ini), {S}^2 grid, {args.ppc} ppc per "
+                         f"species ({n_total} particles), 1D slab decomposition 1,{world}" if c2 else
+                         ("C3 Maxwellian 3-D two-species plasma" if c3 else
+                          f"C5 warm 3-D two-species plasma around an immersed sphere (radius {S / 32:g} cells)"
+                          if c5 else "C4 warm 3-D two-species plasma")
+                         + f", {S}^3 grid, {args.ppc} ppc per species "
+                         f"({n_total} particles), 1D slab decomposition 1,1,{world}"),
+            "grid": [S] * nd,
             "ppc_per_species": args.ppc,
             "species": 2,
             "particles": n_total,
-            "decomposition": f"1,1,{world}",
-            "layout": args.layout + (f" (tile sort every {args.sort_interval} steps)" if args.layout == "tiled" else ""),
+            "decomposition": f"1,{world}" if c2 else f"1,1,{world}",
+            "layout": args.layout + ((f" (per-species tile sort once {args.sort_fraction:g} of the particles left "
+                                      f"their cell, at most {args.sort_max} steps apart)" if args.sort_fraction > 0 else
+                                      f" (tile sort every {args.sort_interval} steps)") if args.layout == "tiled" else ""),
             "poisson": ("spectral (sSolver, rocFFT r2c/c2r, global grid)" if c3 else
-                        f"multigrid mgVRecursive, {mg_levels} levels ({S}^3 down to {S >> (mg_levels - 1)}^3), "
+                        f"multigrid mgVRecursive, {mg_levels} levels ({S}^{nd} down to {S >> (mg_levels - 1)}^{nd}), "
                         "RB Gauss-Seidel 10/10/10, "
                         + ("native mode (correction scheme, coarse h^2 factor; the ini's 5 levels extended)"
                            if args.mg == "native" else "reference algorithm (parity mode)")),
@@ -373,7 +399,8 @@ def main() -> int:
     os.unlink(ini)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = _cpu_baseline(args.cpu_size, args.ppc, args.cpu_steps, args.mg == "native")
+        result["cpu_baseline"] = _cpu_baseline(S if c2 else args.cpu_size, args.ppc, args.cpu_steps,
+                                               args.mg == "native", args.workload if args.workload != "c5" else "c4")
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist is not None:

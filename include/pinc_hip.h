@@ -316,12 +316,14 @@ int pinc_hip_gs_sweep(const double *phiIn, double *phiOut, const double *rho, pi
 int pinc_hip_gs_sweep2x(const double *phiIn, double *phiOut, const double *rho, pinc_lvl_t L,
                         void *stream);
 /* Native mode: the whole V-cycle below (and including) a coarse level in one
- * 1024-thread workgroup, grids in LDS (at most 4800 points over all levels,
- * 3-D, each level half the previous).  levels[0] is the top coarse level:
- * its rho is read from `rho`, its correction starts at zero and is written
- * to `phi`; rho of the levels below is the restricted residual times 4. */
+ * 1024-thread workgroup, grids in LDS (at most 5500 points over all levels,
+ * 1-D to 3-D, each level half the previous in every dimension).  levels[0]
+ * is the top coarse level: its rho is read from `rho`, its correction starts
+ * at zero and is written to `phi`; rho of the levels below is the restricted
+ * residual times 4.  hw3d / gs3d select mgHalfRestrict3D / mgGS3D's forms
+ * (3-D only), else the ND forms. */
 int pinc_hip_mg_coarse(const double *rho, double *phi, int nLevels, const pinc_lvl_t *levels, int nPre,
-                       int nPost, int nCoarse, int hw3d, void *stream);
+                       int nPost, int nCoarse, int hw3d, int gs3d, void *stream);
 int pinc_hip_gs_materialize(double *phi, pinc_lvl_t L, int lastPass, const double *muA,
                             const double *muB, void *stream);
 /* phi -= *mu over all points */

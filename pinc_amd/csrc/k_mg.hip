@@ -689,18 +689,21 @@ __global__ __launch_bounds__(NT) void k_gs_sweep4(const double *__restrict__ phi
 
 // ------------------------------------------- coarse levels in one launch ---
 // Native mode: the V-cycle below level qc (every level with at most
-// kCoarseMax points, down to 2^3) runs inside one 1024-thread workgroup with
-// all its grids in LDS, replacing ~100 tiny launches per cycle.  Same
-// operators as the per-level kernels: GS (3-D form), residual, restrict,
-// prolong (prol_low), neutralisation after each smoothing and of rho.
+// kCoarseMax points, down to 2 per dimension) runs inside one 1024-thread
+// workgroup with all its grids in LDS, replacing ~100 tiny launches per
+// cycle.  Same operators and expression order as the per-level kernels:
+// GS (mgGS3D form when gs3d, else mgGSND), residual, restriction
+// (halfWeight / halfWeightND), prolongation (prol_low), neutralisation after
+// each smoothing and of rho.  1-D, 2-D and 3-D (ND).
 constexpr int kCoarseMax = 4096;          // points of the top coarse level
-constexpr int kCoarseLds = 4800 * 3;      // doubles: phi, rho, res of all levels
+constexpr int kCoarseLds = 5500 * 3;      // doubles: phi, rho, res of all levels (132 KB)
 
 struct CoarseArgs {
 	int nLevels;
-	int T[8][3];
+	int T[12][3];
 	int nPre, nPost, nCoarse;
 	int hw3d;
+	int gs3d;
 };
 
 __device__ double blk_sum(double v, double *wred) {
@@ -723,21 +726,36 @@ __device__ void blk_neutralize(double *a, long n, double *wred) {
 	__syncthreads();
 }
 
-__device__ void blk_smooth(double *phi, const double *rho, const Lv &L, int nIter) {
+__device__ __forceinline__ void blk_coords(const Lv &L, long g, int *c) {
+	c[0] = (int)(g % L.T[0]);
+	long r = g / L.T[0];
+	c[1] = (int)(r % L.T[1]);
+	c[2] = (int)(r / L.T[1]);
+}
+
+template <int ND>
+__device__ void blk_smooth(double *phi, const double *rho, const Lv &L, int nIter, bool gs3d) {
 	long n = (long)L.T[0] * L.T[1] * L.T[2];
 	for (int it = 0; it < nIter; it++) {
 		for (int pass = 0; pass < 2; pass++) {
 			for (long g = threadIdx.x; g < n; g += blockDim.x) {
 				int c[3];
-				c[0] = (int)(g % L.T[0]);
-				long r = g / L.T[0];
-				c[1] = (int)(r % L.T[1]);
-				c[2] = (int)(r / L.T[1]);
+				blk_coords(L, g, c);
 				if (((c[0] + c[1] + c[2]) & 1) != pass) continue;
-				double xp = phi[g + nb_up(L, c, 0)], xm = phi[g + nb_dn(L, c, 0)];
-				double yp = phi[g + nb_up(L, c, 1)], ym = phi[g + nb_dn(L, c, 1)];
-				double zp = phi[g + nb_up(L, c, 2)], zm = phi[g + nb_dn(L, c, 2)];
-				phi[g] = (1. / 6.) * (xp + xm + yp + ym + zp + zm + rho[g]);
+				double v;
+				if (ND == 3 && gs3d) {
+					double xp = phi[g + nb_up(L, c, 0)], xm = phi[g + nb_dn(L, c, 0)];
+					double yp = phi[g + nb_up(L, c, 1)], ym = phi[g + nb_dn(L, c, 1)];
+					double zp = phi[g + nb_up(L, c, 2)], zm = phi[g + nb_dn(L, c, 2)];
+					v = (1. / 6.) * (xp + xm + yp + ym + zp + zm + rho[g]);
+				} else {
+					v = 0;
+#pragma unroll
+					for (int d = 0; d < ND; d++) v += phi[g + nb_up(L, c, d)] + phi[g + nb_dn(L, c, d)];
+					v += rho[g];
+					v *= 1. / (2 * ND);
+				}
+				phi[g] = v;
 			}
 			__syncthreads();
 		}
@@ -752,12 +770,13 @@ struct CLevel {
 
 // level l's grids inside the LDS block (no dynamically indexed arrays:
 // everything is recomputed from the kernel arguments)
+template <int ND>
 __device__ __forceinline__ CLevel clevel(const CoarseArgs &a, double *lds, int l) {
 	CLevel c;
 	long off = 0;
 	for (int k = 0; k < l; k++) off += 3L * a.T[k][0] * a.T[k][1] * a.T[k][2];
 	pinc_lvl_t lp;
-	lp.nd = 3;
+	lp.nd = ND;
 	lp.T[0] = a.T[l][0];
 	lp.T[1] = a.T[l][1];
 	lp.T[2] = a.T[l][2];
@@ -769,12 +788,14 @@ __device__ __forceinline__ CLevel clevel(const CoarseArgs &a, double *lds, int l
 	return c;
 }
 
+template <int ND>
 __global__ __launch_bounds__(1024) void k_mg_coarse(const double *__restrict__ rhoIn,
                                                     double *__restrict__ phiOut, CoarseArgs a) {
 	__shared__ double lds[kCoarseLds];
 	__shared__ double wred[16];
+	const bool gs3d = a.gs3d;
 	{
-		CLevel t = clevel(a, lds, 0);
+		CLevel t = clevel<ND>(a, lds, 0);
 		for (long g = threadIdx.x; g < t.N; g += blockDim.x) {
 			t.rho[g] = rhoIn[g];
 			t.phi[g] = 0.0;
@@ -783,70 +804,61 @@ __global__ __launch_bounds__(1024) void k_mg_coarse(const double *__restrict__ r
 	__syncthreads();
 	const int B = a.nLevels - 1;
 	for (int l = 0; l < B; l++) {
-		CLevel f = clevel(a, lds, l), c = clevel(a, lds, l + 1);
+		CLevel f = clevel<ND>(a, lds, l), c = clevel<ND>(a, lds, l + 1);
 		blk_neutralize(f.rho, f.N, wred);
-		blk_smooth(f.phi, f.rho, f.L, a.nPre);
+		blk_smooth<ND>(f.phi, f.rho, f.L, a.nPre, gs3d);
 		for (long g = threadIdx.x; g < f.N; g += blockDim.x) {
 			int q[3];
-			q[0] = (int)(g % f.L.T[0]);
-			long r = g / f.L.T[0];
-			q[1] = (int)(r % f.L.T[1]);
-			q[2] = (int)(r / f.L.T[1]);
-			f.res[g] = residual_at<3>(f.phi, f.rho, f.L, q, g);
+			blk_coords(f.L, g, q);
+			f.res[g] = residual_at<ND>(f.phi, f.rho, f.L, q, g);
 		}
 		__syncthreads();
 		const Lv &F = f.L, &C = c.L;
 		for (long gc = threadIdx.x; gc < c.N; gc += blockDim.x) {
-			int cc[3], cf[3];
-			cc[0] = (int)(gc % C.T[0]);
-			long r = gc / C.T[0];
-			cc[1] = (int)(r % C.T[1]);
-			cc[2] = (int)(r / C.T[1]);
+			int cc[3], cf[3] = {0, 0, 0};
+			blk_coords(C, gc, cc);
 			long gf = 0;
 #pragma unroll
-			for (int d = 0; d < 3; d++) {
+			for (int d = 0; d < ND; d++) {
 				cf[d] = 2 * cc[d];
 				gf += (long)cf[d] * F.s[d];
 			}
 			const double *x = f.res;
 			double v;
-			if (a.hw3d) {
+			if (ND == 3 && a.hw3d) {
 				v = (1. / 12.) * (6 * x[gf] + x[gf + nb_up(F, cf, 0)] + x[gf + nb_dn(F, cf, 0)] +
 				                  x[gf + nb_up(F, cf, 1)] + x[gf + nb_dn(F, cf, 1)] +
 				                  x[gf + nb_up(F, cf, 2)] + x[gf + nb_dn(F, cf, 2)]);
 			} else {
-				v = 6. * x[gf];
+				v = (2. * ND) * x[gf];
 #pragma unroll
-				for (int d = 0; d < 3; d++) v += x[gf + nb_up(F, cf, d)] + x[gf + nb_dn(F, cf, d)];
-				v *= 1. / 12.;
+				for (int d = 0; d < ND; d++) v += x[gf + nb_up(F, cf, d)] + x[gf + nb_dn(F, cf, d)];
+				v *= 1. / (ND * 4);
 			}
-			c.rho[gc] = 4.0 * v;  // native: coarse h^2 factor
+			c.rho[gc] = v * 4.0;  // native: coarse h^2 factor (the host path's k_scale order)
 			c.phi[gc] = 0.0;      // correction scheme
 		}
 		__syncthreads();
 	}
 	{
-		CLevel b = clevel(a, lds, B);
+		CLevel b = clevel<ND>(a, lds, B);
 		blk_neutralize(b.rho, b.N, wred);
-		blk_smooth(b.phi, b.rho, b.L, a.nCoarse);
+		blk_smooth<ND>(b.phi, b.rho, b.L, a.nCoarse, gs3d);
 		blk_neutralize(b.phi, b.N, wred);
 	}
 	for (int l = B - 1; l >= 0; l--) {
-		CLevel f = clevel(a, lds, l), c = clevel(a, lds, l + 1);
+		CLevel f = clevel<ND>(a, lds, l), c = clevel<ND>(a, lds, l + 1);
 		for (long g = threadIdx.x; g < f.N; g += blockDim.x) {
 			int cf[3];
-			cf[0] = (int)(g % f.L.T[0]);
-			long r = g / f.L.T[0];
-			cf[1] = (int)(r % f.L.T[1]);
-			cf[2] = (int)(r / f.L.T[1]);
-			f.phi[g] += prol_low<3, 0>(c.phi, c.L, cf);
+			blk_coords(f.L, g, cf);
+			f.phi[g] += prol_low<ND, 0>(c.phi, c.L, cf);
 		}
 		__syncthreads();
 		blk_neutralize(f.phi, f.N, wred);
-		blk_smooth(f.phi, f.rho, f.L, a.nPost);
+		blk_smooth<ND>(f.phi, f.rho, f.L, a.nPost, gs3d);
 		blk_neutralize(f.phi, f.N, wred);
 	}
-	CLevel t = clevel(a, lds, 0);
+	CLevel t = clevel<ND>(a, lds, 0);
 	for (long g = threadIdx.x; g < t.N; g += blockDim.x) phiOut[g] = t.phi[g];
 }
 
@@ -960,18 +972,21 @@ extern "C" int pinc_hip_gs_sweep2x(const double *phiIn, double *phiOut, const do
 }
 
 extern "C" int pinc_hip_mg_coarse(const double *rho, double *phi, int nLevels, const pinc_lvl_t *levels, int nPre,
-                                  int nPost, int nCoarse, int hw3d, void *stream) {
+                                  int nPost, int nCoarse, int hw3d, int gs3d, void *stream) {
 	CoarseArgs a;
-	if (nLevels < 1 || nLevels > 8) return set_error(hipErrorInvalidValue, "mg_coarse: 1..8 levels");
+	if (nLevels < 1 || nLevels > 12) return set_error(hipErrorInvalidValue, "mg_coarse: 1..12 levels");
+	const int nd = levels[0].nd;
+	if (nd < 1 || nd > 3) return set_error(hipErrorInvalidValue, "mg_coarse: 1-3 dimensions");
+	if (nd != 3 && (hw3d || gs3d)) return set_error(hipErrorInvalidValue, "mg_coarse: 3-D operators on a non-3-D grid");
 	long tot = 0;
 	a.nLevels = nLevels;
 	for (int l = 0; l < nLevels; l++) {
-		if (levels[l].nd != 3) return set_error(hipErrorInvalidValue, "mg_coarse: 3-D levels only");
+		if (levels[l].nd != nd) return set_error(hipErrorInvalidValue, "mg_coarse: mixed dimensions");
 		long n = 1;
 		for (int d = 0; d < 3; d++) {
 			a.T[l][d] = levels[l].T[d];
 			n *= levels[l].T[d];
-			if (l > 0 && 2 * levels[l].T[d] != levels[l - 1].T[d])
+			if (l > 0 && d < nd && 2 * levels[l].T[d] != levels[l - 1].T[d])
 				return set_error(hipErrorInvalidValue, "mg_coarse: levels must halve");
 		}
 		tot += 3 * n;
@@ -981,6 +996,10 @@ extern "C" int pinc_hip_mg_coarse(const double *rho, double *phi, int nLevels, c
 	a.nPost = nPost;
 	a.nCoarse = nCoarse;
 	a.hw3d = hw3d;
-	hipLaunchKernelGGL(k_mg_coarse, dim3(1), dim3(1024), 0, (hipStream_t)stream, rho, phi, a);
+	a.gs3d = gs3d;
+	hipStream_t st = (hipStream_t)stream;
+	if (nd == 3) hipLaunchKernelGGL(k_mg_coarse<3>, dim3(1), dim3(1024), 0, st, rho, phi, a);
+	else if (nd == 2) hipLaunchKernelGGL(k_mg_coarse<2>, dim3(1), dim3(1024), 0, st, rho, phi, a);
+	else hipLaunchKernelGGL(k_mg_coarse<1>, dim3(1), dim3(1024), 0, st, rho, phi, a);
 	return check_launch("mg_coarse");
 }

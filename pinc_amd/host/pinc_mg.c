@@ -242,15 +242,20 @@ static void smooth(MultigridSolver *S, int q, int nIter, int nd3) {
 	           "gs materialize");
 }
 
-/* native mode, 3-D: first level from which the rest of the V-cycle fits the
- * single-workgroup LDS kernel (pinc_hip_mg_coarse), or -1 */
+/* native mode: first level from which the rest of the V-cycle fits the
+ * single-workgroup LDS kernel (pinc_hip_mg_coarse), or -1.  Its smoother is
+ * one form for every phase (all three 3-D, or all three N-D).  (A variant
+ * that also ran level 0 of small grids in that one workgroup, from L2, was
+ * slower at C2's 128^2: 3.7 ms per solve against 2.2 ms.) */
 static int coarse_start(const MultigridSolver *S) {
-	if (!S->native || S->L[0].nd != 3 || !S->pre3d || !S->post3d || !S->coarse3d) return -1;
+	if (!S->native) return -1;
+	int all3 = S->pre3d && S->post3d && S->coarse3d, none3 = !S->pre3d && !S->post3d && !S->coarse3d;
+	if (!all3 && !none3) return -1;
 	for (int q = 1; q < S->nLevels; q++) {
 		if (S->N[q] > 4096) continue;
 		long tot = 0;
 		for (int k = q; k < S->nLevels; k++) tot += 3 * S->N[k];
-		if (tot <= 14400 && S->nLevels - q <= 8) return q;
+		if (tot <= 5500 * 3 && S->nLevels - q <= 12) return q;
 	}
 	return -1;
 }
@@ -260,7 +265,7 @@ static void vrec(MultigridSolver *S, int q) {
 	int qc = coarse_start(S);
 	if (qc > 0 && q == qc) {
 		pinc_check(pinc_hip_mg_coarse(S->rho[q], S->phi[q], S->nLevels - q, &S->L[q], S->nPre, S->nPost, S->nCoarse,
-		                              S->restr3d, g_pinc.stream),
+		                              S->restr3d, S->pre3d, g_pinc.stream),
 		           "mg coarse");
 		pinc_check(pinc_hip_prolong_add(S->phi[q - 1], S->phi[q], S->L[q - 1], g_pinc.stream), "prolong");
 		return;

@@ -14,6 +14,7 @@ summation order of the neutralisation means and of the norm, so the
 histories agree to round-off until the residual itself approaches
 round-off.
 """
+import os
 import sys
 from pathlib import Path
 
@@ -85,3 +86,42 @@ def test_native_and_parity_modes_reach_the_same_potential():
     a = mg_history.run("gpu", 128, 5, 3000, 20261016, 1.0)
     b = mg_history.run("gpu", 128, 5, 200, 20261016, 1.0, native=True)
     assert np.max(np.abs(a["phi"] - b["phi"])) <= 1e-7 * np.max(np.abs(a["phi"]))
+
+
+@pytest.mark.parametrize("name,native", [("c2", True), ("c2", False), ("langmuir1d", True)])
+def test_nd_solve_matches_oracle(name, native):
+    """1-D and 2-D multigrid (mgGSND / halfWeightND / bilinearND; C2's
+    128^2 grid), native mode -- whose coarse levels run in the
+    single-workgroup kernel -- and parity mode, against the oracle on the
+    same rho: same cycle count (+-1), phi to 1e-9 of its maximum."""
+    import orc
+    from pinc_amd import Sim, configs
+    cfg = configs.config(name)
+    if native:
+        cfg["multigrid"]["native"] = "1"
+    ini = configs.write_ini(cfg)
+    try:
+        w = orc.World(ini)
+        shape = w.grid(0).shape
+        rho = np.zeros(shape)
+        inner = tuple(slice(1, -1) for _ in shape[:-1]) + (0,)
+        rho[inner] = np.random.default_rng(7).standard_normal(rho[inner].shape)
+        w.mg_limit(4000, 4000)
+        w.set_grid(0, rho)
+        w.op("solve")
+        ho = w.mg_history()
+        po = w.grid(1)[inner].copy()
+        w.close()
+        with Sim(ini, perturb=False) as s:
+            s.mg_limit(4000, 4000)
+            s.set_grid(0, rho)
+            s.op("solve")
+            hg = s.mg_history()
+            pg = s.grid(1)[inner].copy()
+    finally:
+        os.unlink(ini)
+    assert ho[-1] <= 1e-10 and hg[-1] <= 1e-10
+    assert abs(len(ho) - len(hg)) <= 1, (len(ho), len(hg))
+    if native:
+        assert len(hg) <= 12
+    assert np.max(np.abs(pg - po)) <= 1e-9 * np.max(np.abs(po))
