@@ -202,6 +202,8 @@ long mgCycleCount(const MultigridSolver *solver);
 void mgSetLimit(MultigridSolver *solver, long maxCycles, long histCap);
 long mgHistory(const MultigridSolver *solver, double *out, long cap);
 int mgLevels(const MultigridSolver *solver);
+/* halo planes of the sharded level 0 (multigrid:shard), 0 for a replicated solve */
+int mgShardHalo(const MultigridSolver *solver);
 
 /* ---------------------------------------------------------- spectral -- */
 /* spectral.c:14-115; N-D extension of the reference's 1-D solver on rocFFT */
@@ -281,6 +283,7 @@ long pinc_sim_cycles(const PincSim *sim);
  * Poisson solver is spectral) */
 int pinc_sim_mg_limit(PincSim *sim, long maxCycles, long histCap);
 int pinc_sim_mg_levels(PincSim *sim);  /* levels of the multigrid hierarchy in use */
+int pinc_sim_mg_shard(PincSim *sim);   /* mgShardHalo of the solver (0: replicated or spectral) */
 long pinc_sim_mg_history(PincSim *sim, double *out, long cap);
 int pinc_sim_nspecies(const PincSim *sim);
 int pinc_sim_ndims(const PincSim *sim);

@@ -324,6 +324,25 @@ int pinc_hip_gs_sweep2x(const double *phiIn, double *phiOut, const double *rho, 
  * (3-D only), else the ND forms. */
 int pinc_hip_mg_coarse(const double *rho, double *phi, int nLevels, const pinc_lvl_t *levels, int nPre,
                        int nPost, int nCoarse, int hw3d, int gs3d, void *stream);
+/* Sharded level 0 of the native multigrid (several ranks, 3-D): this rank's
+ * z-slab extended by halo planes, Lx = T0 x T1 x (nloc + 2 hz), x/y periodic,
+ * z neighbours read directly.
+ *   residual_slab        residual on planes [zlo, zhi) of the extended slab
+ *   residual_sumsq_slab  block partials of its square (RMS norm)
+ *   restrict_slab        this rank's level-1 planes (Lc: T0/2 x T1/2 x nloc/2)
+ *                        from the slab's residual starting at plane zf0,
+ *                        times 4 (coarse h^2 factor)
+ *   prolong_add_slab     every slab plane += the global level-1 correction
+ *                        (Lc global); slab plane zl is global plane z0 + zl
+ *                        (mod Tz) */
+int pinc_hip_residual_slab(double *res, const double *phi, const double *rho, pinc_lvl_t Lx, int zlo, int zhi,
+                           void *stream);
+int pinc_hip_residual_sumsq_slab(const double *phi, const double *rho, pinc_lvl_t Lx, int zlo, int zhi,
+                                 double *partial, int *nBlocks, void *stream);
+int pinc_hip_restrict_slab(const double *fineX, pinc_lvl_t Lx, int zf0, double *coarse, pinc_lvl_t Lc, int nd3,
+                           void *stream);
+int pinc_hip_prolong_add_slab(double *phiX, pinc_lvl_t Lx, int z0, int Tz, const double *phiC, pinc_lvl_t Lc,
+                              void *stream);
 int pinc_hip_gs_materialize(double *phi, pinc_lvl_t L, int lastPass, const double *muA,
                             const double *muB, void *stream);
 /* phi -= *mu over all points */

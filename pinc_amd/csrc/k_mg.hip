@@ -862,6 +862,95 @@ __global__ __launch_bounds__(1024) void k_mg_coarse(const double *__restrict__ r
 	for (long g = threadIdx.x; g < t.N; g += blockDim.x) phiOut[g] = t.phi[g];
 }
 
+// ----------------------------------------------- sharded level 0 (z-slabs) ---
+// Native mode with several ranks: level 0 lives as this
+// rank's z-slab extended by hz halo planes on each side, x/y periodic, the
+// slab dimension not (its halo planes are in memory).  Level 1 is global.
+// Restriction of the slab's residual into this rank's level-1 planes, and
+// bilinear prolongation of the global level-1 correction into every plane
+// of the extended slab, with the arithmetic of k_restrict / k_prolong_add.
+
+// residual on planes [zlo, zhi) of the extended slab (z neighbours direct);
+// SUMSQ: block partials of its square instead of storing it
+template <bool SUMSQ>
+__global__ __launch_bounds__(kThreads) void k_residual_slab(double *__restrict__ out, const double *__restrict__ phi,
+                                                            const double *__restrict__ rho, pinc_lvl_t Lp, int zlo,
+                                                            int zhi) {
+	__shared__ double red[kThreads / 64];
+	Lv L = make_lv(Lp);
+	const long ps = L.s[2];
+	const long n = ps * (zhi - zlo);
+	double acc = 0.;
+	for (long q = (long)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (long)gridDim.x * blockDim.x) {
+		const long g = (long)zlo * ps + q;
+		int c[3];
+		c[0] = (int)(g % L.T[0]);
+		long r = g / L.T[0];
+		c[1] = (int)(r % L.T[1]);
+		c[2] = (int)(r / L.T[1]);
+		double v = -6. * phi[g];
+		v += phi[g + nb_up(L, c, 0)] + phi[g + nb_dn(L, c, 0)] + phi[g + nb_up(L, c, 1)] + phi[g + nb_dn(L, c, 1)] +
+		     phi[g + ps] + phi[g - ps];
+		v = v + rho[g];
+		if (SUMSQ) acc += v * v;
+		else out[g] = v;
+	}
+	if (SUMSQ) {
+		double t = block_sum(acc, red);
+		if (threadIdx.x == 0) out[blockIdx.x] = t;
+	}
+}
+
+// coarse (x, y, z) of this rank's level-1 planes <- fine (2x, 2y, zf0 + 2z)
+// of the extended slab, halfWeight (HW3D) or halfWeightND, times 4 (native)
+template <bool HW3D>
+__global__ void k_restrict_slab(const double *__restrict__ fine, pinc_lvl_t Lfp, int zf0,
+                                double *__restrict__ coarse, pinc_lvl_t Lcp) {
+	Lv F = make_lv(Lfp), C = make_lv(Lcp);
+	const long ps = F.s[2];
+	const long n = (long)C.T[0] * C.T[1] * C.T[2];
+	for (long gc = (long)blockIdx.x * blockDim.x + threadIdx.x; gc < n; gc += (long)gridDim.x * blockDim.x) {
+		int cc[3];
+		cc[0] = (int)(gc % C.T[0]);
+		long r = gc / C.T[0];
+		cc[1] = (int)(r % C.T[1]);
+		cc[2] = (int)(r / C.T[1]);
+		int cf[3] = {2 * cc[0], 2 * cc[1], zf0 + 2 * cc[2]};
+		const long gf = (long)cf[0] + (long)cf[1] * F.s[1] + (long)cf[2] * ps;
+		double v;
+		if (HW3D) {
+			v = (1. / 12.) * (6 * fine[gf] + fine[gf + nb_up(F, cf, 0)] + fine[gf + nb_dn(F, cf, 0)] +
+			                  fine[gf + nb_up(F, cf, 1)] + fine[gf + nb_dn(F, cf, 1)] + fine[gf + ps] + fine[gf - ps]);
+		} else {
+			v = 6. * fine[gf];
+			v += fine[gf + nb_up(F, cf, 0)] + fine[gf + nb_dn(F, cf, 0)];
+			v += fine[gf + nb_up(F, cf, 1)] + fine[gf + nb_dn(F, cf, 1)];
+			v += fine[gf + ps] + fine[gf - ps];
+			v *= 1. / 12.;
+		}
+		coarse[gc] = v * 4.0;
+	}
+}
+
+// every plane of the extended slab += prolongated global level-1 correction;
+// plane zl of the slab is global plane (z0 + zl) mod Tz
+__global__ void k_prolong_add_slab(double *__restrict__ phiX, pinc_lvl_t Lxp, int z0, int Tz,
+                                   const double *__restrict__ phiC, pinc_lvl_t Lcp) {
+	Lv X = make_lv(Lxp), C = make_lv(Lcp);
+	const long n = (long)X.T[0] * X.T[1] * X.T[2];
+	for (long g = (long)blockIdx.x * blockDim.x + threadIdx.x; g < n; g += (long)gridDim.x * blockDim.x) {
+		int cf[3];
+		cf[0] = (int)(g % X.T[0]);
+		long r = g / X.T[0];
+		cf[1] = (int)(r % X.T[1]);
+		int z = z0 + (int)(r / X.T[1]);
+		z %= Tz;
+		if (z < 0) z += Tz;
+		cf[2] = z;
+		phiX[g] += prol_low<3, 0>(phiC, C, cf);
+	}
+}
+
 }  // namespace
 
 extern "C" int pinc_hip_gs_pass(double *phi, const double *rho, pinc_lvl_t L, int pass, int nd3,
@@ -1002,4 +1091,47 @@ extern "C" int pinc_hip_mg_coarse(const double *rho, double *phi, int nLevels, c
 	else if (nd == 2) hipLaunchKernelGGL(k_mg_coarse<2>, dim3(1), dim3(1024), 0, st, rho, phi, a);
 	else hipLaunchKernelGGL(k_mg_coarse<1>, dim3(1), dim3(1024), 0, st, rho, phi, a);
 	return check_launch("mg_coarse");
+}
+
+extern "C" int pinc_hip_residual_slab(double *res, const double *phi, const double *rho, pinc_lvl_t Lx, int zlo,
+                                      int zhi, void *stream) {
+	if (Lx.nd != 3 || zlo < 1 || zhi > Lx.T[2] - 1 || zhi <= zlo)
+		return set_error(hipErrorInvalidValue, "residual_slab: planes must have both z neighbours in the slab");
+	long n = (long)Lx.T[0] * Lx.T[1] * (zhi - zlo);
+	hipLaunchKernelGGL(k_residual_slab<false>, dim3(blocks_for(n)), dim3(kThreads), 0, (hipStream_t)stream, res, phi,
+	                   rho, Lx, zlo, zhi);
+	return check_launch("residual_slab");
+}
+
+extern "C" int pinc_hip_residual_sumsq_slab(const double *phi, const double *rho, pinc_lvl_t Lx, int zlo, int zhi,
+                                            double *partial, int *nBlocks, void *stream) {
+	if (Lx.nd != 3 || zlo < 1 || zhi > Lx.T[2] - 1 || zhi <= zlo)
+		return set_error(hipErrorInvalidValue, "residual_sumsq_slab: planes must have both z neighbours in the slab");
+	long n = (long)Lx.T[0] * Lx.T[1] * (zhi - zlo);
+	unsigned nb = blocks_for(n);
+	*nBlocks = (int)nb;
+	hipLaunchKernelGGL(k_residual_slab<true>, dim3(nb), dim3(kThreads), 0, (hipStream_t)stream, partial, phi, rho, Lx,
+	                   zlo, zhi);
+	return check_launch("residual_sumsq_slab");
+}
+
+extern "C" int pinc_hip_restrict_slab(const double *fineX, pinc_lvl_t Lx, int zf0, double *coarse, pinc_lvl_t Lc,
+                                      int nd3, void *stream) {
+	if (Lx.nd != 3 || Lc.nd != 3 || 2 * Lc.T[0] != Lx.T[0] || 2 * Lc.T[1] != Lx.T[1] || zf0 < 1 ||
+	    zf0 + 2 * Lc.T[2] > Lx.T[2])
+		return set_error(hipErrorInvalidValue, "restrict_slab: geometry");
+	unsigned nb = blocks_for(npts(Lc));
+	hipStream_t st = (hipStream_t)stream;
+	if (nd3) hipLaunchKernelGGL(k_restrict_slab<true>, dim3(nb), dim3(kThreads), 0, st, fineX, Lx, zf0, coarse, Lc);
+	else hipLaunchKernelGGL(k_restrict_slab<false>, dim3(nb), dim3(kThreads), 0, st, fineX, Lx, zf0, coarse, Lc);
+	return check_launch("restrict_slab");
+}
+
+extern "C" int pinc_hip_prolong_add_slab(double *phiX, pinc_lvl_t Lx, int z0, int Tz, const double *phiC,
+                                         pinc_lvl_t Lc, void *stream) {
+	if (Lx.nd != 3 || Lc.nd != 3 || 2 * Lc.T[0] != Lx.T[0] || 2 * Lc.T[1] != Lx.T[1] || 2 * Lc.T[2] != Tz)
+		return set_error(hipErrorInvalidValue, "prolong_add_slab: geometry");
+	hipLaunchKernelGGL(k_prolong_add_slab, dim3(blocks_for(npts(Lx))), dim3(kThreads), 0, (hipStream_t)stream, phiX,
+	                   Lx, z0, Tz, phiC, Lc);
+	return check_launch("prolong_add_slab");
 }

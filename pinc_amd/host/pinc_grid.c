@@ -244,6 +244,28 @@ static void exchange_planes(Grid *g, int upPlane, int downPlane) {
 	pinc_comm_exchange(2, sp, sb, nb, rp, rb, nb, "halo exchange");
 }
 
+/* Refresh the h halo planes on each side of an extended slab (nloc owned
+ * planes at [h, h+nloc), planes of ps nodes) from the neighbouring slabs,
+ * z-1 below and z+1 above, periodic; on one rank the halo is the slab's own
+ * periodic image.  Collective over the ranks. */
+void pinc_ext_halo(double *a, long ps, int nloc, int h) {
+	long bytes = (long)h * ps * sizeof(double);
+	if (g_pinc.nranks == 1) {
+		pinc_check(pinc_hip_d2d(a, a + (long)nloc * ps, bytes, g_pinc.stream), "ext halo");
+		pinc_check(pinc_hip_d2d(a + (long)(h + nloc) * ps, a + (long)h * ps, bytes, g_pinc.stream), "ext halo");
+		return;
+	}
+	int P = g_pinc.nranks, r = g_pinc.rank;
+	int up = (r + 1) % P, dn = (r - 1 + P) % P;
+	/* top owned planes [nloc, nloc+h) go up into the upper slab's lower halo,
+	 * bottom owned planes [h, 2h) go down into the lower slab's upper halo */
+	int sp[2] = {up, dn}, rp[2] = {dn, up};
+	void *sb[2] = {a + (long)nloc * ps, a + (long)h * ps};
+	void *rb[2] = {a, a + (long)(h + nloc) * ps};
+	long nb[2] = {bytes, bytes};
+	pinc_comm_exchange(2, sp, sb, nb, rp, rb, nb, "ext halo");
+}
+
 void gHaloOp(funPtr sliceOp, Grid *grid, const MpiInfo *mpiInfo, opDirection dir) {
 	(void)mpiInfo;
 	PincDevGrid *dv = grid->dev;
@@ -287,6 +309,21 @@ void gHaloOp(funPtr sliceOp, Grid *grid, const MpiInfo *mpiInfo, opDirection dir
 }
 
 void gFinDiff1st(const Grid *scalar, Grid *field) {
+	if (scalar->dev->ext) {
+		/* sharded multigrid: the extended slab holds planes off-hz .. of the
+		 * potential, every plane E reads exact (pinc_mg.c) */
+		PincDevGrid *sv = scalar->dev;
+		if (sv->extStale) {
+			pinc_ext_halo(sv->ext, sv->planeSize, sv->geom.nloc, sv->extOff);
+			sv->extStale = 0;
+		}
+		pinc_geom_t g = field->dev->geom;
+		g.T[g.nd - 1] = scalar->dev->extPlanes;
+		g.off = scalar->dev->extOff;
+		pinc_check(pinc_hip_efield(scalar->dev->ext, g, field->dev->d, g_pinc.stream), "efield");
+		field->dev->ghostsValid = 1;
+		return;
+	}
 	const double *phi = scalar->dev->global ? scalar->dev->global : scalar->dev->d + scalar->dev->planeSize;
 	if (!scalar->dev->global && g_pinc.nranks > 1)
 		msg(ERROR, "gFinDiff1st needs the global potential (run the solver first)");
@@ -406,6 +443,16 @@ void gSyncToDevice(Grid *grid) {
 	}
 	pinc_check(pinc_hip_h2d(dv->d, tmp, dv->n * sizeof(double), g_pinc.stream), "gSyncToDevice");
 	free(tmp);
+	if (dv->ext) {
+		/* sharded multigrid: the owned planes of the extended slab (its halo
+		 * is refreshed before every smoothing chunk) */
+		long ps = dv->planeSize;
+		pinc_check(pinc_hip_d2d(dv->ext + (long)dv->extOff * ps, dv->d + ps, ps * dv->geom.nloc * sizeof(double),
+		                        g_pinc.stream), "gSyncToDevice ext");
+		dv->ghostsValid = 0;
+		dv->extStale = 1;
+		return;
+	}
 	if (dv->global && dv->ownsGlobal) {
 		long ps = dv->planeSize * nv;
 		pinc_check(pinc_hip_d2d(dv->global + (long)dv->geom.off * ps, dv->d + ps,

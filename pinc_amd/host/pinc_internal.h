@@ -122,6 +122,11 @@ struct PincDevGrid {
 	int ghostsValid;    /* slab ghost planes already hold periodic images */
 	double *recv[2];    /* halo receive planes (multi-rank) */
 	double *scaled;     /* E as rescaled for the species being pushed (lazy) */
+	/* sharded multigrid (phi only): this rank's slab with extOff halo planes
+	 * on each side, extPlanes planes in all, owned by the solver */
+	double *ext;
+	int extOff, extPlanes;
+	int extStale;       /* owned planes written (gSyncToDevice), halo not yet refreshed */
 };
 
 /* immersed objects (pinc_obj.c; object.c, config C5) */
@@ -155,6 +160,14 @@ struct MultigridSolver {
 	double *hist;
 	long histCap, histN, maxCycles;
 	long fusedMin;     /* smallest level (points) smoothed by the fused sweeps */
+	/* sharded level 0 (native mode, multigrid:shard):
+	 * rho[0]/phi[0]/res[0] are this rank's z-slab with hz halo planes on
+	 * each side (L[0], N[0] = that extended slab), levels >= 1 global */
+	int shard, hz, chunk, nloc0;
+	long ps0, Ng0;                 /* plane size, global level-0 points */
+	int z0;                        /* global plane of extended plane 0 */
+	double *rho1Slab;              /* this rank's level-1 planes before the all-gather */
+	pinc_lvl_t L1s;
 };
 
 /* collectives over RCCL or the host transport (pinc_comm.c) */
@@ -163,6 +176,7 @@ void pinc_comm_exchange(int nOps, const int *sendPeer, void *const *sendbuf, con
 void pinc_comm_allgather(const double *send, double *recv, long count, const char *what);
 void pinc_comm_allreduce_sum(double *buf, long count, const char *what);
 int pinc_comm_host_transport(void);
+void pinc_ext_halo(double *a, long ps, int nloc, int h);
 
 /* helpers shared by the host translation units */
 void pinc_ctx_require(void);

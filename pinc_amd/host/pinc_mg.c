@@ -46,6 +46,64 @@ static int smootherIs3D(const dictionary *ini, const char *key, int nd) {
 	return r;
 }
 
+/* Sharded level 0 (native mode).  multigrid:shard = 0
+ * (replicated solve), 1 (shard whenever the geometry allows it, also on one
+ * rank, whose halo is then its own periodic image) or auto (default: shard
+ * with several ranks once the extended slab is at most half the global
+ * grid, i.e. from 4 ranks at 256^3).  Each rank smooths its z-slab extended
+ * by hz planes on each side; after `chunk` red-black iterations the planes
+ * within 2 chunk + 2 of the slab ends are stale, so the halo is refreshed
+ * (hz planes each way) before every chunk, and hz >= 2 chunk + 2 keeps the
+ * planes that the residual, the restriction and E read exact. */
+static void shard_setup(MultigridSolver *S, const dictionary *ini, const Grid *rho, Grid *phi) {
+	pinc_geom_t g = rho->dev->geom;
+	int mode = -1; /* auto */
+	if (iniHas(ini, "multigrid:shard")) {
+		char *v = iniGetStr(ini, "multigrid:shard");
+		if (!strcmp(v, "auto")) mode = -1;
+		else mode = atoi(v) ? 1 : 0;
+		free(v);
+	}
+	S->shard = 0;
+	int objects = iniHas(ini, "objects:sphere") || iniHas(ini, "objects:file");
+	int nl = g.nloc;
+	int m = S->nPre > S->nPost ? S->nPre : S->nPost;
+	if (m > (nl - 2) / 2) m = (nl - 2) / 2;
+	int ok = S->native && g.nd == 3 && !objects && S->nLevels >= 2 && nl % 2 == 0 && m >= 1;
+	if (!mode || !ok) {
+		if (mode == 1 && !ok)
+			msg(WARNING, "multigrid:shard=1 needs native mode, 3-D, no objects and slabs of >= 4 planes: "
+			             "replicated solve");
+		return;
+	}
+	int h = 2 * m + 2;
+	/* extended slab a multiple of 16 planes (the fused sweeps), if the slab
+	 * is deep enough to supply the extra halo */
+	for (int h2 = h; h2 <= nl; h2 += 2)
+		if ((nl + 2 * h2) % 16 == 0) {
+			h = h2;
+			break;
+		}
+	int E = nl + 2 * h;
+	if (mode < 0 && !(g_pinc.nranks > 1 && 2 * E <= g.T[2])) return;
+	S->shard = 1;
+	S->hz = h;
+	S->chunk = m;
+	S->nloc0 = nl;
+	S->ps0 = (long)g.T[0] * g.T[1];
+	S->z0 = g.off - h;
+	S->L[0].T[2] = E;
+	S->N[0] = S->ps0 * E;
+	S->L1s = S->L[1];
+	S->L1s.T[2] = nl / 2;
+	long n1 = (long)S->L1s.T[0] * S->L1s.T[1] * S->L1s.T[2];
+	pinc_check(pinc_hip_malloc((void **)&S->rho1Slab, n1 * sizeof(double)), "mg shard");
+	/* rho[0], phi[0], res[0] are allocated with the other levels (size N[0]) */
+	phi->dev->extOff = h;
+	phi->dev->extPlanes = E;
+	S->useGraph = 0; /* the halo exchanges are host-driven */
+}
+
 MultigridSolver *mgAllocSolver(const dictionary *ini, Grid *rho, Grid *phi) {
 	MultigridSolver *S = calloc(1, sizeof(*S));
 	int nd = rho->rank - 1;
@@ -109,7 +167,11 @@ MultigridSolver *mgAllocSolver(const dictionary *ini, Grid *rho, Grid *phi) {
 		}
 	}
 	long ps = rho->dev->planeSize;
-	if (g_pinc.nranks == 1) {
+	S->Ng0 = S->N[0];
+	shard_setup(S, ini, rho, phi);
+	if (S->shard) {
+		/* level 0 is this rank's extended slab; no global level-0 arrays */
+	} else if (g_pinc.nranks == 1) {
 		rho->dev->global = rho->dev->d + ps;
 		phi->dev->global = phi->dev->d + ps;
 	} else {
@@ -118,10 +180,12 @@ MultigridSolver *mgAllocSolver(const dictionary *ini, Grid *rho, Grid *phi) {
 		pinc_check(pinc_hip_memset(phi->dev->global, 0, S->N[0] * sizeof(double), g_pinc.stream), "global phi");
 		rho->dev->ownsGlobal = phi->dev->ownsGlobal = 1;
 	}
-	S->rho[0] = rho->dev->global;
-	S->phi[0] = phi->dev->global;
+	if (!S->shard) {
+		S->rho[0] = rho->dev->global;
+		S->phi[0] = phi->dev->global;
+	}
 	for (int q = 0; q < S->nLevels; q++) {
-		if (q > 0) {
+		if (q > 0 || S->shard) {
 			pinc_check(pinc_hip_malloc((void **)&S->rho[q], S->N[q] * sizeof(double)), "mg level");
 			pinc_check(pinc_hip_malloc((void **)&S->phi[q], S->N[q] * sizeof(double)), "mg level");
 			pinc_check(pinc_hip_memset(S->rho[q], 0, S->N[q] * sizeof(double), g_pinc.stream), "mg level");
@@ -129,6 +193,7 @@ MultigridSolver *mgAllocSolver(const dictionary *ini, Grid *rho, Grid *phi) {
 		}
 		pinc_check(pinc_hip_malloc((void **)&S->res[q], S->N[q] * sizeof(double)), "mg level");
 	}
+	if (S->shard) phi->dev->ext = S->phi[0];
 	S->rhoGrid = rho;
 	S->phiGrid = phi;
 	return S;
@@ -139,11 +204,15 @@ void mgFreeSolver(MultigridSolver *S) {
 	pinc_hip_graph_destroy(S->cycleGraph);
 	free(S->hist);
 	for (int q = 0; q < S->nLevels; q++) {
-		if (q > 0) {
+		if (q > 0 || S->shard) {
 			pinc_hip_free(S->rho[q]);
 			pinc_hip_free(S->phi[q]);
 		}
 		pinc_hip_free(S->res[q]);
+	}
+	if (S->shard) {
+		pinc_hip_free(S->rho1Slab);
+		S->phiGrid->dev->ext = NULL; /* the grids outlive the solver (main.c:283-290) */
 	}
 	free(S);
 }
@@ -160,6 +229,8 @@ void mgSetLimit(MultigridSolver *S, long maxCycles, long histCap) {
 
 int mgLevels(const MultigridSolver *S) { return S->nLevels; }
 
+int mgShardHalo(const MultigridSolver *S) { return S->shard ? S->hz : 0; }
+
 long mgHistory(const MultigridSolver *S, double *out, long cap) {
 	long n = S->histN < S->histCap ? S->histN : S->histCap;
 	if (out)
@@ -171,6 +242,54 @@ long mgHistory(const MultigridSolver *S, double *out, long cap) {
 static void neutralize(double *a, long N) {
 	pinc_check(pinc_hip_sum_div(a, N, (double)N, g_pinc.dScratch, PINC_SLOT(TMP_SLOT), g_pinc.stream), "mean");
 	pinc_check(pinc_hip_sub_dev(a, N, PINC_SLOT(TMP_SLOT), g_pinc.stream), "neutralize");
+}
+
+/* sharded level 0: refresh the hz halo planes of an extended slab */
+static void shard_halo(MultigridSolver *S, double *a) { pinc_ext_halo(a, S->ps0, S->nloc0, S->hz); }
+
+/* gNeutralizeGrid of the sharded level 0: mean over the owned planes of
+ * all ranks, subtracted from the whole extended slab */
+static void neutralize_shard(MultigridSolver *S, double *a) {
+	long ps = S->ps0;
+	pinc_check(pinc_hip_sum(a + (long)S->hz * ps, ps * S->nloc0, g_pinc.dScratch, PINC_SLOT(TMP_SLOT), g_pinc.stream),
+	           "mean");
+	if (g_pinc.nranks > 1) pinc_comm_allreduce_sum(PINC_SLOT(TMP_SLOT), 1, "mg mean");
+	pinc_check(pinc_hip_reduce(PINC_SLOT(TMP_SLOT), 1, (double)S->Ng0, PINC_SLOT(TMP_SLOT + 2), g_pinc.stream), "mean");
+	pinc_check(pinc_hip_sub_dev(a, S->N[0], PINC_SLOT(TMP_SLOT + 2), g_pinc.stream), "neutralize");
+}
+
+static void neutralize_level(MultigridSolver *S, int q, double *a) {
+	if (q == 0 && S->shard) neutralize_shard(S, a);
+	else neutralize(a, S->N[q]);
+}
+
+/* phi[qf] += prolongated phi[qf + 1] */
+static void prolong_into(MultigridSolver *S, int qf) {
+	if (qf == 0 && S->shard)
+		pinc_check(pinc_hip_prolong_add_slab(S->phi[0], S->L[0], S->z0, S->L[1].T[2] * 2, S->phi[1], S->L[1],
+		                                     g_pinc.stream),
+		           "prolong slab");
+	else pinc_check(pinc_hip_prolong_add(S->phi[qf], S->phi[qf + 1], S->L[qf], g_pinc.stream), "prolong");
+}
+
+/* residual of level q restricted into rho[q + 1] (times 4 in native mode) */
+static void restrict_residual(MultigridSolver *S, int q) {
+	if (q == 0 && S->shard) {
+		/* the restriction reads fine planes h-1 .. h+nloc-1 */
+		int h = S->hz;
+		pinc_check(pinc_hip_residual_slab(S->res[0], S->phi[0], S->rho[0], S->L[0], h - 1, h + S->nloc0,
+		                                  g_pinc.stream),
+		           "residual slab");
+		pinc_check(pinc_hip_restrict_slab(S->res[0], S->L[0], h, S->rho1Slab, S->L1s, S->restr3d, g_pinc.stream),
+		           "restrict slab");
+		long n1 = (long)S->L1s.T[0] * S->L1s.T[1] * S->L1s.T[2];
+		if (g_pinc.nranks > 1) pinc_comm_allgather(S->rho1Slab, S->rho[1], n1, "gather level 1");
+		else pinc_check(pinc_hip_d2d(S->rho[1], S->rho1Slab, n1 * sizeof(double), g_pinc.stream), "level 1");
+		return;
+	}
+	pinc_check(pinc_hip_residual(S->res[q], S->phi[q], S->rho[q], S->L[q], g_pinc.stream), "residual");
+	pinc_check(pinc_hip_restrict(S->res[q], S->rho[q + 1], S->L[q + 1], S->restr3d, g_pinc.stream), "restrict");
+	if (S->native) pinc_check(pinc_hip_scale(S->rho[q + 1], S->N[q + 1], 4.0, g_pinc.stream), "native scale");
 }
 
 /* nIter red-black iterations, each colour followed by a neutralisation:
@@ -185,7 +304,7 @@ static void smooth_native(MultigridSolver *S, int q, int nIter, int nd3) {
 	 * 256^3: 128^3 and below are as fast, launch-latency bound, as two
 	 * passes; rechecked with the 32x8 two-ahead sweep) */
 	int fused = nd3 && L.nd == 3 && L.T[0] % 16 == 0 && L.T[1] % 16 == 0 && L.T[2] % 16 == 0 &&
-	            S->N[q] >= S->fusedMin;
+	            (S->N[q] >= S->fusedMin || (q == 0 && S->shard && S->N[q] >= S->fusedMin / 4));
 	int k = 0;
 	/* two iterations per launch (pinc_hip_gs_sweep2x) in pairs, so that the
 	 * ping-pong ends in phi */
@@ -219,6 +338,13 @@ static void smooth_native(MultigridSolver *S, int q, int nIter, int nd3) {
 
 static void smooth(MultigridSolver *S, int q, int nIter, int nd3) {
 	if (nIter <= 0) return;
+	if (q == 0 && S->shard) {
+		for (int k = 0; k < nIter; k += S->chunk) {
+			shard_halo(S, S->phi[0]);
+			smooth_native(S, 0, nIter - k < S->chunk ? nIter - k : S->chunk, nd3);
+		}
+		return;
+	}
 	if (S->native) {
 		smooth_native(S, q, nIter, nd3);
 		return;
@@ -267,7 +393,7 @@ static void vrec(MultigridSolver *S, int q) {
 		pinc_check(pinc_hip_mg_coarse(S->rho[q], S->phi[q], S->nLevels - q, &S->L[q], S->nPre, S->nPost, S->nCoarse,
 		                              S->restr3d, S->pre3d, g_pinc.stream),
 		           "mg coarse");
-		pinc_check(pinc_hip_prolong_add(S->phi[q - 1], S->phi[q], S->L[q - 1], g_pinc.stream), "prolong");
+		prolong_into(S, q - 1);
 		return;
 	}
 	/* native mode: correction scheme, each coarse visit solves for the
@@ -277,26 +403,31 @@ static void vrec(MultigridSolver *S, int q) {
 		neutralize(S->rho[q], S->N[q]);
 		smooth(S, q, S->nCoarse, S->coarse3d);
 		neutralize(S->phi[q], S->N[q]);
-		pinc_check(pinc_hip_prolong_add(S->phi[q - 1], S->phi[q], S->L[q - 1], g_pinc.stream), "prolong");
+		prolong_into(S, q - 1);
 		return;
 	}
-	neutralize(S->rho[q], S->N[q]);
+	neutralize_level(S, q, S->rho[q]);
 	smooth(S, q, S->nPre, S->pre3d);
-	pinc_check(pinc_hip_residual(S->res[q], S->phi[q], S->rho[q], S->L[q], g_pinc.stream), "residual");
-	pinc_check(pinc_hip_restrict(S->res[q], S->rho[q + 1], S->L[q + 1], S->restr3d, g_pinc.stream), "restrict");
-	if (S->native) pinc_check(pinc_hip_scale(S->rho[q + 1], S->N[q + 1], 4.0, g_pinc.stream), "native scale");
+	restrict_residual(S, q);
 	vrec(S, q + 1);
-	neutralize(S->phi[q], S->N[q]);
+	neutralize_level(S, q, S->phi[q]);
 	smooth(S, q, S->nPost, S->post3d);
-	neutralize(S->phi[q], S->N[q]);
-	if (q > 0) pinc_check(pinc_hip_prolong_add(S->phi[q - 1], S->phi[q], S->L[q - 1], g_pinc.stream), "prolong");
+	neutralize_level(S, q, S->phi[q]);
+	if (q > 0) prolong_into(S, q - 1);
 }
 
 void mgSolve(MultigridSolver *S, Grid *rho, Grid *phi, const MpiInfo *mpiInfo) {
 	(void)mpiInfo;
 	(void)phi;
 	pinc_phase_begin(4);
-	if (g_pinc.nranks > 1) {
+	if (S->shard) {
+		/* this rank's rho into the extended slab, halo from the neighbours */
+		long ps = S->ps0;
+		pinc_check(pinc_hip_d2d(S->rho[0] + (long)S->hz * ps, rho->dev->d + ps, ps * S->nloc0 * sizeof(double),
+		                        g_pinc.stream),
+		           "shard rho");
+		shard_halo(S, S->rho[0]);
+	} else if (g_pinc.nranks > 1) {
 		long ps = rho->dev->planeSize;
 		pinc_comm_allgather(rho->dev->d + ps, rho->dev->global, ps * rho->dev->geom.nloc, "gather rho");
 	}
@@ -329,13 +460,23 @@ void mgSolve(MultigridSolver *S, Grid *rho, Grid *phi, const MpiInfo *mpiInfo) {
 			S->cycles++;
 			int nb = 0;
 			int slot = pinc_probe_begin(PINC_PROBE_RESIDUAL);
-			pinc_check(pinc_hip_residual_sumsq(S->phi[0], S->rho[0], S->L[0], g_pinc.dScratch, &nb, g_pinc.stream),
-			           "residual norm");
-			pinc_probe_end(PINC_PROBE_RESIDUAL, slot, 16.0 * S->N[0]);
-			pinc_check(pinc_hip_reduce(g_pinc.dScratch, nb, 1.0, PINC_SLOT(TMP_SLOT + 1), g_pinc.stream), "norm");
+			if (S->shard) {
+				/* owned planes, summed over the ranks */
+				pinc_check(pinc_hip_residual_sumsq_slab(S->phi[0], S->rho[0], S->L[0], S->hz, S->hz + S->nloc0,
+				                                        g_pinc.dScratch, &nb, g_pinc.stream),
+				           "residual norm");
+				pinc_probe_end(PINC_PROBE_RESIDUAL, slot, 16.0 * S->ps0 * S->nloc0);
+				pinc_check(pinc_hip_reduce(g_pinc.dScratch, nb, 1.0, PINC_SLOT(TMP_SLOT + 1), g_pinc.stream), "norm");
+				if (g_pinc.nranks > 1) pinc_comm_allreduce_sum(PINC_SLOT(TMP_SLOT + 1), 1, "norm");
+			} else {
+				pinc_check(pinc_hip_residual_sumsq(S->phi[0], S->rho[0], S->L[0], g_pinc.dScratch, &nb, g_pinc.stream),
+				           "residual norm");
+				pinc_probe_end(PINC_PROBE_RESIDUAL, slot, 16.0 * S->N[0]);
+				pinc_check(pinc_hip_reduce(g_pinc.dScratch, nb, 1.0, PINC_SLOT(TMP_SLOT + 1), g_pinc.stream), "norm");
+			}
 			double sum = 0;
 			pinc_check(pinc_hip_d2h(&sum, PINC_SLOT(TMP_SLOT + 1), sizeof(double), g_pinc.stream), "norm");
-			barRes = sqrt(sum / S->N[0]);
+			barRes = sqrt(sum / S->Ng0);
 			if (S->histN < S->histCap) S->hist[S->histN] = barRes;
 			S->histN++;
 			if (S->maxCycles && !isfinite(barRes)) {
@@ -361,5 +502,15 @@ void mgSolve(MultigridSolver *S, Grid *rho, Grid *phi, const MpiInfo *mpiInfo) {
 		}
 	}
 	phi->dev->ghostsValid = 0;
+	if (S->shard) {
+		/* the slab with its ghost planes (exact: within hz - 2 chunk of the
+		 * owned planes); E reads the extended slab directly (gFinDiff1st) */
+		long ps = S->ps0;
+		pinc_check(pinc_hip_d2d(phi->dev->d, S->phi[0] + (long)(S->hz - 1) * ps, ps * (S->nloc0 + 2) * sizeof(double),
+		                        g_pinc.stream),
+		           "shard phi");
+		phi->dev->ghostsValid = 1;
+		phi->dev->extStale = 0;
+	}
 	pinc_phase_end(4);
 }

@@ -23,7 +23,7 @@
  *   pinc_obj_add_rho      gAddTo(rho, rhoObj) (main.c:230)
  *   pinc_obj_apply        oApplyCapacitanceMatrix (object.c:301-366)
  *
- * The checker is the object restatement under oracle/ (oracle/orc_obj.c),
+ * The checker is the object restatement under oracle/,
  * with the same five corrections of reference defects, named in its header:
  *   1. pCut gets the particle, not the node index (object.c:499);
  *   2. the particle swapped into a removed one's slot is re-tested;

@@ -348,6 +348,7 @@ int pinc_sim_mg_limit(PincSim *S, long maxCycles, long histCap) {
 }
 
 int pinc_sim_mg_levels(PincSim *S) { return S->spectral ? 0 : mgLevels(S->solver); }
+int pinc_sim_mg_shard(PincSim *S) { return S->spectral ? 0 : mgShardHalo(S->solver); }
 
 long pinc_sim_mg_history(PincSim *S, double *out, long cap) {
 	if (S->spectral) return -1;

@@ -107,6 +107,11 @@ class Sim:
         """Levels of the multigrid hierarchy in use (0 for the spectral solver)."""
         return HOST.pinc_sim_mg_levels(self._h)
 
+    @property
+    def mg_shard(self) -> int:
+        """Halo planes of the sharded multigrid level 0 (0: replicated solve)."""
+        return HOST.pinc_sim_mg_shard(self._h)
+
     def mg_history(self) -> np.ndarray:
         """RMS residual after each V-cycle of the last solve (mgHistory)."""
         n = HOST.pinc_sim_mg_history(self._h, None, 0)

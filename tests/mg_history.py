@@ -41,19 +41,30 @@ def make_rho(size: int, seed: int, amp: float) -> np.ndarray:
     return out
 
 
-def ini_for(size: int, levels: int, native: bool) -> str:
+def ini_for(size: int, levels: int, native: bool, nranks: int = 1, shard: str | None = None) -> str:
     from pinc_amd import configs
-    cfg = configs.config("warm", true_size=(size, size, size), nsub=(1, 1, 1), ppc=1, nalloc_pc=2, levels=levels)
+    cfg = configs.config("warm", true_size=(size, size, size // nranks), nsub=(1, 1, nranks), ppc=1, nalloc_pc=2,
+                         levels=levels)
     if native:
         cfg["multigrid"]["native"] = "1"
+    if shard is not None:
+        cfg["multigrid"]["shard"] = shard
     return configs.write_ini(cfg)
 
 
+def rank_slab(rho: np.ndarray, rank: int, nranks: int) -> np.ndarray:
+    """This rank's planes of a reference-layout global grid (ghost planes are
+    the neighbours' planes; the solvers read true nodes only)."""
+    nloc = (rho.shape[0] - 2) // nranks
+    return np.ascontiguousarray(rho[rank * nloc: rank * nloc + nloc + 2])
+
+
 def run(side: str, size: int, levels: int, cycles: int, seed: int, amp: float, native: bool = False,
-        solves: int = 1) -> dict:
+        solves: int = 1, shard: str | None = None) -> dict:
     rho = make_rho(size, seed, amp)
     digest = hashlib.sha256(rho.tobytes()).hexdigest()
-    ini = ini_for(size, levels, native)
+    ini = ini_for(size, levels, native, shard=shard)
+    halo = 0
     t0 = time.perf_counter()
     hists = []
     try:
@@ -77,11 +88,12 @@ def run(side: str, size: int, levels: int, cycles: int, seed: int, amp: float, n
                 s.op("solve")
                 hists.append(s.mg_history().tolist())
             phi = s.grid(1)[1:-1, 1:-1, 1:-1].copy()
+            halo = s.mg_shard
             s.close()
     finally:
         os.unlink(ini)
     return {"side": side, "size": size, "levels": levels, "native": native, "cycle_cap": cycles, "seed": seed,
-            "amp": amp, "rho_sha256": digest, "seconds": time.perf_counter() - t0, "residual": hists,
+            "amp": amp, "shard_halo": halo, "rho_sha256": digest, "seconds": time.perf_counter() - t0, "residual": hists,
             "phi_rms": float(np.sqrt(np.mean(phi ** 2))), "phi_sample": phi[::max(1, size // 8), 3, 5].tolist(),
             "phi": phi}
 

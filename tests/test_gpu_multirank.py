@@ -34,10 +34,17 @@ def _sorted_rows(a):
 
 
 @pytest.mark.parametrize("layout,poisson", [("reference", "mgSolver"), ("tiled", "mgSolver"),
-                                            ("reference", "sSolver")])
+                                            ("reference", "sSolver"), ("reference", "mgShard")])
 def test_two_ranks_one_gpu(built, tmp_path, layout, poisson):
+    """mgShard: native multigrid with level 0 sharded over the two slabs
+    (8 halo planes, smoothing in chunks of 3 iterations) against the
+    oracle's native solve."""
     cfg = configs.config("cold3d", true_size=(16, 16, 8), nsub=(1, 1, 2))
     cfg["multigrid"]["mgLevels"] = "3"
+    if poisson == "mgShard":
+        cfg["multigrid"]["native"] = "1"
+        cfg["multigrid"]["shard"] = "1"
+        poisson = "mgSolver"
     cfg["methods"]["poisson"] = poisson
     ini_ref = configs.write_ini(cfg)
     if layout == "tiled":
