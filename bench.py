@@ -29,6 +29,8 @@ import sys
 import time
 from pathlib import Path
 
+import numpy as np
+
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
@@ -151,6 +153,10 @@ def main() -> int:
                     help="native: correction-scheme V-cycle with the coarse h^2 factor (default; the reference "
                          "algorithm does not converge at 256^3 with 5 levels, DESIGN.md section 6); reference: "
                          "the reference's mgVRecursive exactly")
+    ap.add_argument("--mg-shard", default="auto", choices=["auto", "0", "1"],
+                    help="native multigrid level 0 sharded over the z-slabs with a deep halo (DESIGN.md section 7): "
+                         "auto (default: from the rank count at which the extended slab is at most half the grid, "
+                         "4 at 256^3), 1 (whenever possible, also on one rank), 0 (replicated solve)")
     ap.add_argument("--layout", default="tiled", choices=["tiled", "reference"],
                     help="tiled: particles re-sorted by 4^3-cell tile every --sort-interval moves (default); "
                          "reference: the reference's particle order (bit-exact indices)")
@@ -231,6 +237,7 @@ def main() -> int:
                              nalloc_pc=args.ppc + 8)
     if args.mg == "native":
         cfg["multigrid"]["native"] = "1"
+        cfg["multigrid"]["shard"] = args.mg_shard
     if c5:
         # a generated sphere (the reference's bepiColombo object file is not
         # available): centre of the grid, radius S/32
@@ -288,6 +295,13 @@ def main() -> int:
     n_local = sim.total_particles()
     ke, pe, _ = sim.energy()
     mg_levels = sim.mg_levels
+    mg_halo = sim.mg_shard
+    # particles that left through the slab faces in the last step (this
+    # rank's; at one rank, those that would cross a slab boundary): the
+    # migration exchange, one record of 2 nd + 1 doubles each
+    em = sim.emigrants()   # [3^nd neighbours, species]
+    slab_axis = (np.arange(3 ** nd) // 3 ** (nd - 1)) != 1
+    z_emig = int(em[slab_axis].sum())
 
     dt_max = dt
     n_total = n_local
@@ -359,7 +373,9 @@ def main() -> int:
                         f"multigrid mgVRecursive, {mg_levels} levels ({S}^{nd} down to {S >> (mg_levels - 1)}^{nd}), "
                         "RB Gauss-Seidel 10/10/10, "
                         + ("native mode (correction scheme, coarse h^2 factor; the ini's 5 levels extended)"
-                           if args.mg == "native" else "reference algorithm (parity mode)")),
+                           if args.mg == "native" else "reference algorithm (parity mode)")
+                        + (f", level 0 sharded over the slabs ({mg_halo} halo planes per side), levels >= 1 "
+                           "all-gathered" if mg_halo else (", replicated on every rank" if world > 1 else ""))),
         },
         "poisson_ms_per_step": solve_ms,
         "push_deposit_ms_per_step": push_ms,
@@ -368,6 +384,8 @@ def main() -> int:
         "phase_ms_per_step": {k: v / K for k, v in phases.items()},
         "init_s": t_init,
         "init_cycles": cycles_init,
+        "migration": {"slab_face_emigrants_last_step": z_emig, "record_bytes": 8 * (2 * nd + 1),
+                      "bytes_last_step": z_emig * 8 * (2 * nd + 1)},
         "energy": {"KE": ke, "PE": pe},
         "roofline": {
             "bound": "hbm",

@@ -5,6 +5,7 @@ directory, for the kernels with a grid of at least 2^20 work-items.
     python tools/pmc_kernels.py <pmc_dir> [out.json]
 """
 import json
+import os
 import sqlite3
 import sys
 from collections import defaultdict
@@ -22,7 +23,7 @@ def main() -> int:
         c = sqlite3.connect(db)
         q = "select kernel_name, grid_size, counter_name, value from counters_collection"
         for k, g, n, v in c.execute(q):
-            if int(g) >= 1 << 20:
+            if int(g) >= int(os.environ.get("PMC_MIN_GRID", 1 << 20)):
                 per[(short(k), int(g))][n].append(float(v))
     out = {f"{k[0]} grid={k[1]}": {n: {"mean": sum(v) / len(v), "n": len(v)} for n, v in cs.items()}
            for k, cs in per.items()}
