@@ -275,6 +275,9 @@ constexpr int kSwZ = 16;       // planes per workgroup
 // interiors in the same L2.  A bijection for any grid, placement only.
 // Measured neutral at C4 (k_gs_sweep4 0.192 ms either way: the march is
 // latency-bound, not L2-miss bound), so off by default.
+#ifndef PINC_MG_SWEEP4C
+#define PINC_MG_SWEEP4C 1
+#endif
 #ifndef PINC_MG_XCD
 #define PINC_MG_XCD 0
 #endif
@@ -687,6 +690,184 @@ __global__ __launch_bounds__(NT) void k_gs_sweep4(const double *__restrict__ phi
 	}
 }
 
+// k_gs_sweep4 restructured for instruction count (same stages, ring and
+// arithmetic, bit-identical results).  The profile of k_gs_sweep4 at 256^3
+// (profiles/r02s_mg_pmc*.json) is issue-bound, not HBM-bound: per wave 8.7 k
+// VALU and 17 k SALU instructions for 72 plane steps, and LDS bank
+// conflicts on the checkerboard (lanes two doubles apart).  Here
+//   * the LDS ring stores each row split by x parity ([y][x & 1][x >> 1]),
+//     so a stage's nodes -- one colour, hence one x parity per row -- and
+//     their y and z neighbours are consecutive doubles across lanes, and
+//     the two x neighbours are a consecutive pair (one ds_read2);
+//   * every per-node LDS index and global rho offset is computed once per
+//     thread and plane parity, before the march;
+//   * the march is unrolled over the 8 ring planes, so plane slots, plane
+//     parities and the phi double buffer are compile-time, and LDS
+//     addresses are a per-thread base plus an immediate offset;
+//   * global loads are a per-plane scalar base plus a 32-bit byte offset.
+template <int SX, int SY, int NT>
+struct Sweep4c {
+	static constexpr int H = 4;
+	static constexpr int HX = SX + 2 * H, HY = SY + 2 * H, HW = HX / 2;
+	static constexpr int PL = HX * HY;  // doubles per ring plane
+	static constexpr int PhiSlots = (PL + NT - 1) / NT;
+	static constexpr int nodes(int h) { return (SX + 2 * h) / 2 * (SY + 2 * h); }
+	static_assert(nodes(3) <= 2 * NT && nodes(2) <= NT && nodes(1) <= NT, "stage slots");
+	static_assert(SX * SY == NT, "one output node per thread and plane");
+	static_assert(PhiSlots == 3, "phi fetch slots");
+};
+
+struct S4Node {
+	unsigned li, lxm;  // LDS indices of the node and of its x-1 neighbour (x+1 follows)
+	unsigned roff;     // byte offset of the node in a plane of the level
+};
+
+template <int SX, int SY, int NT>
+__global__ __launch_bounds__(NT) void k_gs_sweep4c(const double *__restrict__ phiIn, double *__restrict__ phiOut,
+                                                   const double *__restrict__ rho, pinc_lvl_t Lp, int zPlanes) {
+	using S = Sweep4c<SX, SY, NT>;
+	constexpr int H = S::H, HX = S::HX, HW = S::HW, PL = S::PL;
+	__shared__ double L[8 * PL];
+	const int TX = Lp.T[0], TY = Lp.T[1], TZ = Lp.T[2];
+	const long sz = (long)TX * TY;
+	const int ntx = TX / SX, nty = TY / SY;
+	const unsigned tb = xcd_tile(blockIdx.x, gridDim.x);
+	const int bx = tb % ntx, by = (tb / ntx) % nty, bz = tb / (ntx * nty);
+	const int x0 = bx * SX, y0 = by * SY, z0 = bz * zPlanes;
+	const int tid = threadIdx.x;
+	auto wrapi = [](int i, int T) { return i < 0 ? i + T : (i >= T ? i - T : i); };
+	auto lidx = [](int lx, int ly) { return (unsigned)(ly * HX + (lx & 1) * HW + (lx >> 1)); };
+	auto poff = [&](int gx, int gy) { return (unsigned)(wrapi(gx, TX) + wrapi(gy, TY) * TX) * 8u; };
+	// node j of colour c on a plane of parity P, tile grown by h (the
+	// k_gs_sweep4 enumeration)
+	auto mknode = [&](int j, int c, int h, int P) {
+		const int hw = (SX + 2 * h) / 2;
+		if (j >= S::nodes(h)) j = 0;  // idle lane: any valid node
+		const int ty = j / hw - h;
+		const int tx = -h + 2 * (j % hw) + ((c - (x0 - h + y0 + ty + P)) & 1);
+		S4Node n;
+		n.li = lidx(tx + H, ty + H);
+		n.lxm = lidx(tx + H - 1, ty + H);
+		n.roff = poff(x0 + tx, y0 + ty);
+		return n;
+	};
+	// stage nodes per plane parity: red 1st (h = 3, two slots), black 1st
+	// (h = 2), red 2nd (h = 1)
+	S4Node r1n[2][2], b1n[2], r2n[2];
+#pragma unroll
+	for (int P = 0; P < 2; P++) {
+		r1n[P][0] = mknode(tid, 0, 3, P);
+		r1n[P][1] = mknode(tid + NT, 0, 3, P);
+		b1n[P] = mknode(tid, 1, 2, P);
+		r2n[P] = mknode(tid, 0, 1, P);
+	}
+	const bool r1second = tid + NT < S::nodes(3), b1ok = tid < S::nodes(2), r2ok = tid < S::nodes(1);
+	// the output node (black, 2nd iteration): this thread's tile node
+	const int otx = tid % SX, oty = tid / SX;
+	const unsigned oli = lidx(otx + H, oty + H), olxm = lidx(otx + H - 1, oty + H);
+	const unsigned ooff = (unsigned)((x0 + otx) + (y0 + oty) * TX) * 8u;
+	const int oblack0 = (x0 + otx + y0 + oty) & 1;  // black on even planes
+	// phi halo fetch: region element i = tid + NT k (row-major, HX wide)
+	unsigned foff[3], fli[3];
+#pragma unroll
+	for (int k = 0; k < 3; k++) {
+		int i = tid + NT * k;
+		if (i >= PL) i = 0;
+		foff[k] = poff(x0 + i % HX - H, y0 + i / HX - H);
+		fli[k] = lidx(i % HX, i / HX);
+	}
+	const bool f2ok = tid + 2 * NT < PL;
+	auto at = [](const double *base, unsigned byteOff) {
+		return *(const double *)((const char *)base + byteOff);
+	};
+	auto plane = [&](const double *a, int q) { return a + (long)wrapi(q, TZ) * sz; };
+	auto fetch = [&](int q, double *f) {
+		const double *b = plane(phiIn, q);
+		f[0] = at(b, foff[0]);
+		f[1] = at(b, foff[1]);
+		if (f2ok) f[2] = at(b, foff[2]);
+	};
+	auto putPhi = [&](int slot, const double *f) {
+		L[slot * PL + fli[0]] = f[0];
+		L[slot * PL + fli[1]] = f[1];
+		if (f2ok) L[slot * PL + fli[2]] = f[2];
+	};
+	struct Rho {
+		double r1[2], b1, r2, b2;
+	};
+	// rho of the four stages of step t (t of parity PT)
+	auto fetchRho = [&](int t, int PT, Rho &R) {
+		const double *b3 = plane(rho, t + 3), *b2p = plane(rho, t + 2), *b0 = plane(rho, t), *bm = plane(rho, t - 2);
+		R.r1[0] = at(b3, r1n[PT ^ 1][0].roff);
+		if (r1second) R.r1[1] = at(b3, r1n[PT ^ 1][1].roff);
+		R.b1 = at(b2p, b1n[PT].roff);
+		R.r2 = at(b0, r2n[PT].roff);
+		R.b2 = at(bm, ooff);
+	};
+	// GS update of node n on ring slot SL (neighbours on slots SM, SP)
+	auto upd = [&](int SL, int SM, int SP, unsigned li, unsigned lxm, double r) {
+		const double xm = L[SL * PL + lxm], xp = L[SL * PL + lxm + 1];
+		const double ym = L[SL * PL + li - HX], yp = L[SL * PL + li + HX];
+		const double zm = L[SM * PL + li], zp = L[SP * PL + li];
+		return (1. / 6.) * (xp + xm + yp + ym + zp + zm + r);
+	};
+
+	// prologue: phi z0-4 .. z0-2 into LDS, z0-1 into F[1]; rho of the first
+	// two steps (z0 is a multiple of 8: plane q sits in slot q & 7)
+	double F[2][3];
+	for (int q = z0 - 4; q <= z0 - 2; q++) {
+		fetch(q, F[0]);
+		putPhi(q & 7, F[0]);
+	}
+	fetch(z0 - 1, F[1]);
+	Rho RA, RB, RC;
+	fetchRho(z0 - 6, 0, RA);
+	fetchRho(z0 - 5, 1, RB);
+	__syncthreads();
+	const int zEnd = z0 + zPlanes;  // outputs z0 .. zEnd-1
+	// steps s = z0-6 .. zEnd+1: zPlanes + 8 of them, in blocks of 8 starting
+	// at s = 2 (mod 8), so plane s+d sits in slot (2 + k + d) & 7
+	for (int s0 = z0 - 6; s0 <= zEnd + 1; s0 += 8) {
+#pragma unroll
+		for (int k = 0; k < 8; k++) {
+			const int s = s0 + k;
+			const int P = k & 1;  // parity of s (s0 even)
+			auto sl = [&](int d) { return (2 + k + d) & 7; };
+			if (s <= zEnd) {  // two steps ahead of their use
+				fetch(s + 6, F[P]);
+				fetchRho(s + 2, P, RC);
+			}
+			if (s + 3 <= zEnd + 2) {  // red, 1st iteration, plane s+3 (parity P^1)
+				const S4Node &a = r1n[P ^ 1][0], &b = r1n[P ^ 1][1];
+				const double va = upd(sl(3), sl(2), sl(4), a.li, a.lxm, RA.r1[0]);
+				double vb = 0;
+				if (r1second) vb = upd(sl(3), sl(2), sl(4), b.li, b.lxm, RA.r1[1]);
+				L[sl(3) * PL + a.li] = va;
+				if (r1second) L[sl(3) * PL + b.li] = vb;
+			}
+			if (s >= z0 - 1 && s <= zEnd && r2ok) {  // red, 2nd, plane s
+				const S4Node &a = r2n[P];
+				L[sl(0) * PL + a.li] = upd(sl(0), sl(-1), sl(1), a.li, a.lxm, RA.r2);
+			}
+			if (s - 2 >= z0 && s - 2 < zEnd) {  // black, 2nd, plane s-2: out
+				double v = L[sl(-2) * PL + oli];
+				if (oblack0 ^ P) v = upd(sl(-2), sl(-3), sl(-1), oli, olxm, RA.b2);
+				*(double *)((char *)plane(phiOut, s - 2) + ooff) = v;
+			}
+			__syncthreads();
+			if (s + 2 >= z0 - 2 && s + 2 <= zEnd + 1 && b1ok) {  // black, 1st, plane s+2
+				const S4Node &a = b1n[P];
+				L[sl(2) * PL + a.li] = upd(sl(2), sl(1), sl(3), a.li, a.lxm, RA.b1);
+			}
+			// phi s+5 into the slot of s-3 (last read by the black output above)
+			putPhi(sl(5), F[P ^ 1]);
+			__syncthreads();
+			RA = RB;
+			RB = RC;
+		}
+	}
+}
+
 // ------------------------------------------- coarse levels in one launch ---
 // Native mode: the V-cycle below level qc (every level with at most
 // kCoarseMax points, down to 2 per dimension) runs inside one 1024-thread
@@ -1055,8 +1236,13 @@ extern "C" int pinc_hip_gs_sweep2x(const double *phiIn, double *phiOut, const do
 			break;
 		}
 	unsigned nb = (unsigned)(cols * (L.T[2] / zp));
+#if PINC_MG_SWEEP4C
+	hipLaunchKernelGGL((k_gs_sweep4c<32, 8, 256>), dim3(nb), dim3(256), 0, (hipStream_t)stream, phiIn, phiOut, rho, L,
+	                   zp);
+#else
 	hipLaunchKernelGGL((k_gs_sweep4<32, 8, 256>), dim3(nb), dim3(256), 0, (hipStream_t)stream, phiIn, phiOut, rho, L,
 	                   zp);
+#endif
 	return check_launch("gs_sweep2x");
 }
 

@@ -5,6 +5,12 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp PINC_QUIET=1 PMC_MIN_GRID=65536
 O=gpurun_out/${1:-mgpmc}
 mkdir -p $O
+timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $O/kt -o run -- python3 tools/mg_shard_probe.py --cases rep256 --out $O/kt.json > $O/kt.log 2>&1 &&
+python3 -c "
+import sqlite3,glob
+db=sqlite3.connect(glob.glob(\"$O/kt/**/*.db\",recursive=True)[0])
+for r in db.execute(\"select * from top_kernels limit 12\"): print(r)
+" > $O/kt_top.txt && rm -rf $O/kt &&
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_WAVE_CYCLES \
 	-d $O/pmcA -o run -- python3 tools/mg_shard_probe.py --cases rep256 --out $O/a.json > $O/pmcA.log 2>&1 &&
 python3 tools/pmc_kernels.py $O/pmcA $O/pmcA_summary.json > /dev/null &&
