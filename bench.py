@@ -144,8 +144,8 @@ def main() -> int:
     ap.add_argument("--workload", default="c4", choices=["c4", "c3", "c5", "c2"],
                     help="c4: warm 3-D plasma, 256^3, 64 ppc, multigrid (BASELINE.json metric, default); "
                          "c3: Maxwellian 128^3, 32 ppc, spectral (rocFFT) Poisson solve; "
-                         "c5: c4 plus an immersed sphere (object.c: charge collection, capacitance "
-                         "correction, second solve), unfused operators; "
+                         "c5: c4 plus an immersed sphere (object.c: charge collection in the fused push, "
+                         "capacitance correction, second solve); "
                          "c2: input/langmuir2D.ini at 128^2, 32 ppc (Langmuir perturbation, cold), multigrid")
     ap.add_argument("--size", type=int, default=None, help="global cells per dimension (c4: 256, c3: 128)")
     ap.add_argument("--ppc", type=int, default=None, help="particles per cell per species (c4: 64, c3: 32)")
@@ -163,6 +163,8 @@ def main() -> int:
     ap.add_argument("--obj-capacitance", default="solve", choices=["solve", "green"],
                     help="c5: capacitance matrix by one solve per surface node (the reference's, default) or "
                          "by translating one periodic response (objects:capacitance = green)")
+    ap.add_argument("--c5-fused", type=int, default=1, choices=[0, 1],
+                    help="c5: 1 = collection in the fused push (default), 0 = the unfused operators")
     ap.add_argument("--sort-interval", type=int, default=8)
     ap.add_argument("--sort-fraction", type=float, default=0.8,
                     help="> 0: sort each species once this fraction of its particles left their cell since its "
@@ -242,7 +244,7 @@ def main() -> int:
         # a generated sphere (the reference's bepiColombo object file is not
         # available): centre of the grid, radius S/32
         cfg["objects"] = {"sphere": f"{S / 2},{S / 2},{S / 2},{S / 32}", "capacitance": args.obj_capacitance}
-        cfg["population"]["fused"] = "0"
+        cfg["population"]["fused"] = str(args.c5_fused)
     if args.layout == "tiled":
         cfg["population"]["layout"] = "tiled"
         cfg["population"]["sortInterval"] = str(args.sort_interval)

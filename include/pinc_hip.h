@@ -131,6 +131,17 @@ typedef struct {
 	int *perm;
 	unsigned long long *moved; /* if set: += particles that stay and changed cell */
 	unsigned long long *tstamp; /* if set: 8 phase timestamps per block (diagnostics) */
+	/* immersed objects (fused collection, oCollectObjectCharge's test at
+	 * object.c:489-494 on the moved position): if objInside is set, a
+	 * particle that stays and whose cell's lower node has an object id > 0
+	 * in objInside (padded local nodes, strides 1, objSy, objSz; objNodes
+	 * nodes) is flagged PINC_NE_SINK instead of deposited, and counted in
+	 * objCount[id - 1] */
+	const unsigned char *objInside;
+	long objSy, objSz, objNodes;
+	int *objCount;
+	int objLo[3], objHi[3];   /* bounding box (padded node coordinates, inclusive)
+	                             of the nodes with an id: only cells there are looked up */
 } pinc_push_t;
 int pinc_hip_push(pinc_pop_t pop, int s, pinc_geom_t g, const pinc_push_t *args, int *nBlocks, void *stream);
 /* number of sort keys (cells incl. the wrap layer) of the tiled layout */
@@ -179,7 +190,8 @@ int pinc_hip_deposit_cells(pinc_pop_t pop, int s, pinc_geom_t g, int tileWidth, 
  * direction.  Work arrays: see DESIGN.md "Migration".  Outputs:
  *   buf   (6 doubles per emigrant, SoA blocks of cap entries: x,y,z,vx,vy,vz)
  *   bufNe direction of each buffered emigrant
- *   neCount[27] emigrants per direction (species s)
+ *   neCount[PINC_NE_CODES] emigrants per direction (species s), then the
+ *         particles a fused push collected into objects (PINC_NE_SINK)
  * Returns the number of emigrants in *nEmig.  Compacts species s in place
  * (iStop[s] decreases by *nEmig on the host side). */
 typedef struct {
@@ -188,13 +200,18 @@ typedef struct {
 	int *tail;          /* >= nEmig+1 */
 	int *holes;         /* >= nEmig+1 */
 	int *order;         /* >= nEmig   */
-	int *blockHist;     /* >= 27*ceil(nEmig/1024)+27 */
+	int *blockHist;     /* >= 28*ceil(nEmig/1024)+28 */
 	int *scratch;       /* >= 64 ints */
 	double *buf;        /* 6*cap doubles */
 	unsigned char *bufNe;
 	long cap;
 } pinc_extract_ws_t;
 #define PINC_ERR_CAPACITY 77  /* *nEmig emigrants exceed ws.cap: grow and retry */
+/* flag of a particle collected by an object in the fused push: extracted
+ * like an emigrant, after every direction (neCount[PINC_NE_SINK]); neCount
+ * has PINC_NE_CODES entries */
+#define PINC_NE_SINK 27
+#define PINC_NE_CODES 28
 int pinc_hip_extract(pinc_pop_t pop, int s, const unsigned char *flags, int *chunkCount,
                      int center, int nNeighbors, pinc_extract_ws_t ws, long *nEmig,
                      long *neCount, void *stream);

@@ -135,6 +135,9 @@ __global__ __launch_bounds__(kThreads) void k_extract_a(
 	long m = n - E;
 	long base = (long)blockIdx.x * PINC_CHUNK;
 	int running = chunkOffset[blockIdx.x];
+	// a chunk with no emigrants wholly before m has no holes and no tail
+	// survivors: nothing to record (most chunks when few particles leave)
+	if (chunkOffset[blockIdx.x + 1] == running && base + PINC_CHUNK <= m) return;
 	int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 	for (int k = 0; k < kItems; k++) {
 		long i = base + k * kThreads + threadIdx.x;
@@ -183,7 +186,7 @@ __global__ void k_extract_b(const unsigned char *__restrict__ flags, long n, lon
 // per-block direction histogram over the extraction order
 constexpr int kRankItems = 4;
 constexpr int kRankChunk = kThreads * kRankItems;
-constexpr int kMaxNe = 27;
+constexpr int kMaxNe = PINC_NE_CODES;  // 27 directions + the object sink
 
 __global__ __launch_bounds__(kThreads) void k_rank_hist(const unsigned char *__restrict__ flags,
                                                         const int *__restrict__ order, long E,
@@ -203,7 +206,7 @@ __global__ __launch_bounds__(kThreads) void k_rank_hist(const unsigned char *__r
 // exclusive scan per direction over blocks; bases per direction; counts
 __global__ __launch_bounds__(kMaxNe * 32) void k_hist_scan(int *__restrict__ blockHist, int nb,
                                                            int *__restrict__ scratch) {
-	// scratch[32..32+27): base of each direction, scratch[64..64+27): count
+	// scratch[32..32+kMaxNe): base of each direction, scratch[64..64+kMaxNe): count
 	__shared__ int tot[kMaxNe];
 	int ne = threadIdx.x >> 5, l = threadIdx.x & 31;
 	if (ne < kMaxNe && l == 0) {
@@ -1223,6 +1226,10 @@ struct PushArgs {
 	int *perm;           // perm[i] = destination of particle i
 	unsigned long long *moved;  // += particles that stay but changed cell (nullable)
 	unsigned long long *tstamp;  // 8 phase timestamps per block (diagnostics, nullable)
+	const unsigned char *objIn;  // object ids of the padded nodes (nullable: no objects)
+	long objSy, objSz, objN;
+	int *objCount;
+	int objLo[3], objExt[3];     // bounding box of the object nodes: lower corner, extent - 1
 };
 // phase timestamp of the block (thread 0, s_memrealtime at 100 MHz)
 #define PUSH_TS(slot) \
@@ -1498,7 +1505,9 @@ __device__ __forceinline__ int tile_key_cells(const TileGeo &tg, const int *cin)
 
 typedef double dvec2 __attribute__((ext_vector_type(2)));
 
-template <int ND, bool V3D, bool KICK, bool SORT>
+// OBJ: the object test of the fused collection (separate instances, so the
+// plain push carries none of its code)
+template <int ND, bool V3D, bool KICK, bool SORT, bool OBJ = false>
 __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PINC_PUSH_WPE))) void k_push(PushArgs a) {
 	constexpr int NC = 1 << ND;
 	constexpr int NW = kPushThreads / 64;
@@ -1845,6 +1854,22 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 		// emigrant path so that nothing indexes the grid with it
 		bad |= (int)outside << 1;
 		if (outside) ne = 0;
+		if (OBJ && ne == a.center) {
+			// oCollectObjectCharge (object.c:489-494): the cell's lower node,
+			// looked up only inside the objects' bounding box (which lies in
+			// the node table: 32-bit index)
+			bool inBB = true;
+#pragma unroll
+			for (int d = 0; d < ND; d++) inBB &= (unsigned)((int)p[k][d] - a.objLo[d]) <= (unsigned)a.objExt[d];
+			unsigned node = (unsigned)(int)p[k][0];
+			if (ND > 1) node += (unsigned)(int)p[k][1] * (unsigned)a.objSy;
+			if (ND > 2) node += (unsigned)(int)p[k][2] * (unsigned)a.objSz;
+			const int id = inBB ? a.objIn[node] : 0;
+			if (id) {
+				ne = PINC_NE_SINK;
+				atomicAdd(&a.objCount[id - 1], 1);  // rare: particles entering an object
+			}
+		}
 		if (SORT) {
 			// flag staged by block slot (outside the box: by item position)
 			const int r = rlL[k * kPushThreads + threadIdx.x];
@@ -2545,6 +2570,21 @@ extern "C" int pinc_hip_push(pinc_pop_t pop, int s, pinc_geom_t g, const pinc_pu
 	a.perm = args->perm;
 	a.moved = args->moved;
 	a.tstamp = args->tstamp;
+	a.objIn = args->objInside;
+	a.objSy = args->objSy;
+	a.objSz = args->objSz;
+	a.objN = args->objNodes;
+	a.objCount = args->objCount;
+	for (int d = 0; d < 3; d++) {
+		a.objLo[d] = args->objLo[d];
+		a.objExt[d] = args->objHi[d] - args->objLo[d];
+	}
+	if (a.objIn && !a.objCount) return set_error(hipErrorInvalidValue, "push: objInside without objCount");
+	if (a.objIn && (nd != 3 || a.objN > 2147483647L)) return set_error(hipErrorInvalidValue, "push: objects are 3-D");
+	for (int d = 0; a.objIn && d < 3; d++)
+		if (a.objExt[d] >= 0 && (a.objLo[d] < 0 || (long)a.objLo[d] + a.objExt[d] >= (d == 0 ? a.objSy : d == 1 ? a.objSz / a.objSy
+		                                                                                             : a.objN / a.objSz)))
+			return set_error(hipErrorInvalidValue, "push: object box outside the node table");
 	unsigned nb = (unsigned)ceil_div(n, kPushChunk);
 	*nBlocks = (int)nb;
 	hipStream_t st = (hipStream_t)stream;
@@ -2556,7 +2596,12 @@ extern "C" int pinc_hip_push(pinc_pop_t pop, int s, pinc_geom_t g, const pinc_pu
 		else if (sort) hipLaunchKernelGGL((k_push<ND, V3D, false, true>), dim3(nb), dim3(kPushThreads), 0, st, a);     \
 		else hipLaunchKernelGGL((k_push<ND, V3D, false, false>), dim3(nb), dim3(kPushThreads), 0, st, a);              \
 	} while (0)
-	if (nd == 3) LAUNCH_PUSH(3, true);
+	if (nd == 3 && a.objIn) {
+		if (kick && sort) hipLaunchKernelGGL((k_push<3, true, true, true, true>), dim3(nb), dim3(kPushThreads), 0, st, a);
+		else if (kick) hipLaunchKernelGGL((k_push<3, true, true, false, true>), dim3(nb), dim3(kPushThreads), 0, st, a);
+		else if (sort) hipLaunchKernelGGL((k_push<3, true, false, true, true>), dim3(nb), dim3(kPushThreads), 0, st, a);
+		else hipLaunchKernelGGL((k_push<3, true, false, false, true>), dim3(nb), dim3(kPushThreads), 0, st, a);
+	} else if (nd == 3) LAUNCH_PUSH(3, true);
 	else if (nd == 2) LAUNCH_PUSH(2, false);
 	else LAUNCH_PUSH(1, false);
 #undef LAUNCH_PUSH

@@ -60,7 +60,7 @@ struct PincDevPop {
 	int flagsValid;
 	pinc_extract_ws_t ws[PINC_MAX_SPECIES];
 	long nEmig[PINC_MAX_SPECIES];
-	long neCount[PINC_MAX_SPECIES][PINC_NNE];
+	long neCount[PINC_MAX_SPECIES][PINC_NE_CODES]; /* directions + the object sink */
 	double *qm, *mq;              /* device q/m and m/q per species */
 	double *kePartial;
 	pinc_geom_t geom;
@@ -106,6 +106,14 @@ struct PincDevPop {
 	unsigned long long *movedCnt;       /* device, per species, this push */
 	double movedFrac[PINC_MAX_SPECIES], lastRate[PINC_MAX_SPECIES];
 	int sinceSort[PINC_MAX_SPECIES], sortNext[PINC_MAX_SPECIES];
+	/* fused object collection (pinc_obj_attach): the push flags a particle
+	 * that enters an object PINC_NE_SINK (removed by the next extract, not
+	 * deposited) and counts it in objCount[s * objK + id - 1] */
+	const unsigned char *objInside;
+	long objSy, objSz, objNodes;
+	int *objCount;
+	int objK;
+	int objLo[3], objHi[3];
 	/* multi-rank migration buffers (AoS records: nd pos, nd vel, ne) */
 	double *sendBuf[2], *recvBuf[2];
 	long sendCap, recvCap;
@@ -137,6 +145,7 @@ void pinc_obj_capacitance(PincObj *o, Grid *rho, Grid *phi, void *solver,
                           void (*solve)(void *, Grid *, Grid *, const MpiInfo *), const MpiInfo *mpi);
 void pinc_obj_collect(PincObj *o, Population *pop, int discard);
 void pinc_obj_add_rho(PincObj *o, Grid *rho);
+void pinc_obj_attach(PincObj *o, Population *pop);
 double pinc_obj_apply(PincObj *o, Grid *rho, const Grid *phi);
 long pinc_obj_nsurface(const PincObj *o);
 double pinc_obj_collected(const PincObj *o);

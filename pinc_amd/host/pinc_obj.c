@@ -1,10 +1,10 @@
 /*
  * pinc_obj.c -- immersed objects (object.c, config C5) on the device path,
  * any number of z-slabs (the solve is replicated, so phi is read from its
- * global view and the charge corrections go to the owning slab), unfused
- * operators (either particle layout: with
- * the tiled one the back-filled slots are deposited individually until the
- * next sort, as after a migration).
+ * global view and the charge corrections go to the owning slab), fused or
+ * unfused operators, either particle layout (with the tiled one the
+ * back-filled slots are deposited individually until the next sort, as
+ * after a migration).
  *
  *   pinc_obj_create       oFillLookupTables (object.c:111-160) and
  *                         oFindObjectSurfaceNodes (object.c:368-458) on the
@@ -15,11 +15,17 @@
  *   pinc_obj_capacitance  oComputeCapacitanceMatrix (object.c:163-298): one
  *                         device solve per surface node with a unit charge
  *                         there; the inverse (host Gauss-Jordan, GSL's LU in
- *                         the reference) goes to the device
+ *                         the reference) goes to the device.  It uses the
+ *                         run's Poisson solver: multigrid as the reference
+ *                         (which builds one for it, object.c:176-178) or,
+ *                         an extension with parity unpinned, the spectral
+ *                         one (exact discrete response)
  *   pinc_obj_collect      oCollectObjectCharge (object.c:460-515): flag kernel
  *                         + the emigrant back-fill (pinc_hip_extract) removes
  *                         the particles; their charge is spread over the
- *                         surface nodes of rhoObj
+ *                         surface nodes of rhoObj.  With the fused push the
+ *                         test rides in k_push (pinc_obj_attach) and the flag
+ *                         kernel only sees the immigrants
  *   pinc_obj_add_rho      gAddTo(rho, rhoObj) (main.c:230)
  *   pinc_obj_apply        oApplyCapacitanceMatrix (object.c:301-366)
  *
@@ -65,6 +71,9 @@ struct PincObj {
 	double *collected;   /* per object */
 	int haveCap;
 	int green;           /* objects:capacitance = green: columns by translation */
+	int *dPushCount;     /* device: per species and object, particles the fused push collected */
+	int bbLo[3], bbHi[3]; /* bounding box of this rank's interior nodes (padded coordinates) */
+	PincDevPop *pop;     /* population attached for the fused collection */
 	int T[3];
 };
 
@@ -162,6 +171,23 @@ static PincObj *obj_create(const dictionary *ini, const pinc_geom_t *g) {
 		int id = ID(c[0] - 1, c[1] - 1, g->off + c[2] - 1);
 		inside[node] = (unsigned char)(id > 0 ? id : 0);
 	}
+	for (int d = 0; d < 3; d++) {
+		o->bbLo[d] = 1 << 30;
+		o->bbHi[d] = -1;
+	}
+	for (long node = 0; node < o->nNodes; node++) {
+		if (!inside[node]) continue;
+		int c[3] = {(int)(node % S[0]), (int)((node / o->sy) % S[1]), (int)(node / o->sz)};
+		for (int d = 0; d < 3; d++) {
+			if (c[d] < o->bbLo[d]) o->bbLo[d] = c[d];
+			if (c[d] > o->bbHi[d]) o->bbHi[d] = c[d];
+		}
+	}
+	if (o->bbHi[0] < 0)
+		for (int d = 0; d < 3; d++) { /* no object node in this slab: empty box (hi < lo) */
+			o->bbLo[d] = 0;
+			o->bbHi[d] = -1;
+		}
 	/* surface (object.c:368-458): global true nodes with 1..7 of the 8
 	 * nodes at offsets {0,-1}^3 in the object, in global z,y,x order (for
 	 * z-slabs the reference's rank-then-local order) */
@@ -228,6 +254,12 @@ PincObj *pinc_obj_create(const dictionary *ini, const Grid *rho) {
 
 void pinc_obj_free(PincObj *o) {
 	if (!o) return;
+	if (o->pop) {
+		/* the population outlives the objects (main.c:283-290) */
+		o->pop->objInside = NULL;
+		o->pop->objCount = NULL;
+	}
+	pinc_hip_free(o->dPushCount);
 	pinc_hip_free(o->dInside);
 	pinc_hip_free(o->dSurf);
 	pinc_hip_free(o->dSurfG);
@@ -349,26 +381,66 @@ void pinc_obj_capacitance(PincObj *o, Grid *rho, Grid *phi, void *solver,
 	o->haveCap = 1;
 }
 
+/* Fused push (population:fused = 1): the push tests every particle that
+ * stays against the object table (the test of object.c:489-494 on its new
+ * position), flags the ones inside PINC_NE_SINK instead of depositing them
+ * and counts them per species and object; the next extract removes them
+ * with the emigrants' back-fill (k_push, pinc_pusher.c extract). */
+void pinc_obj_attach(PincObj *o, Population *pop) {
+	PincDevPop *dv = pop->dev;
+	if (!o || !dv->fused) return;
+	long n = (long)PINC_MAX_SPECIES * o->nObj;
+	pinc_check(pinc_hip_malloc((void **)&o->dPushCount, n * sizeof(int)), "object push counts");
+	pinc_check(pinc_hip_memset(o->dPushCount, 0, n * sizeof(int), g_pinc.stream), "object push counts");
+	dv->objInside = o->dInside;
+	dv->objSy = o->sy;
+	dv->objSz = o->sz;
+	dv->objNodes = o->nNodes;
+	dv->objK = o->nObj;
+	dv->objCount = o->dPushCount;
+	for (int d = 0; d < 3; d++) {
+		dv->objLo[d] = o->bbLo[d];
+		dv->objHi[d] = o->bbHi[d];
+	}
+	o->pop = dv;
+}
+
 /* object.c:460-515 (corrected): remove the particles whose cell's lower
  * node is interior, with the emigrant back-fill order; their charge goes
- * to rhoObj's surface nodes.  discard: main.c:163-166 (charge dropped). */
+ * to rhoObj's surface nodes.  discard: main.c:163-166 (charge dropped).
+ * With the fused push (pinc_obj_attach) the particles that stayed were
+ * tested by the push and are gone already (their counts are read here);
+ * only the particles imported since -- [depEnd, iStop) of each species --
+ * go through the flag pass. */
 void pinc_obj_collect(PincObj *o, Population *pop, int discard) {
 	PincDevPop *dv = pop->dev;
-	if (dv->fused) msg(ERROR, "objects need population:fused=0 (collection runs between migrate and deposit)");
 	int K = o->nObj;
 	double *cnt = calloc(K + 1, sizeof(double));
 	int *hc = calloc(K + 1, sizeof(int));
+	const int fusedPath = dv->objInside && !discard;
+	if (fusedPath) {
+		int ns = pop->nSpecies;
+		int *pc = malloc((size_t)ns * K * sizeof(int));
+		pinc_check(pinc_hip_d2h(pc, dv->objCount, (size_t)ns * K * sizeof(int), g_pinc.stream), "object push counts");
+		pinc_check(pinc_hip_memset(dv->objCount, 0, (size_t)ns * K * sizeof(int), g_pinc.stream), "object push counts");
+		for (int s = 0; s < ns; s++)
+			for (int a = 0; a < K; a++) cnt[a] += pop->charge[s] * (double)pc[s * K + a];
+		free(pc);
+	}
 	for (int s = 0; s < pop->nSpecies; s++) {
-		long n = pop->iStop[s] - pop->iStart[s];
+		long first = pop->iStart[s];
+		if (fusedPath && dv->depValid && dv->depExtracted) first = dv->depEnd[s];
+		long n = pop->iStop[s] - first;
 		if (n <= 0) continue;
 		for (int attempt = 0;; attempt++) {
 			pinc_pop_t p = pinc_devpop(pop);
+			p.iStart[s] = first;
 			pinc_check(pinc_hip_memset(o->dCount, 0, (K + 1) * sizeof(int), g_pinc.stream), "object count");
 			pinc_check(pinc_hip_obj_flag(p, s, o->dInside, o->sy, o->sz, o->nNodes, dv->flags,
 			                             dv->chunkCount + dv->chunkBase[s], o->dCount, g_pinc.stream),
 			           "object flag");
 			long nRem = 0;
-			long neCount[PINC_NNE];
+			long neCount[PINC_NE_CODES];
 			int rc = pinc_hip_extract(p, s, dv->flags, dv->chunkCount + dv->chunkBase[s], 13, PINC_NNE, dv->ws[s],
 			                          &nRem, neCount, g_pinc.stream);
 			if (rc == PINC_ERR_CAPACITY && attempt == 0) {
@@ -378,6 +450,9 @@ void pinc_obj_collect(PincObj *o, Population *pop, int discard) {
 			pinc_check(rc, "object collect");
 			pinc_check(pinc_hip_d2h(hc, o->dCount, K * sizeof(int), g_pinc.stream), "object count");
 			pop->iStop[s] -= nRem;
+			/* removals reorder the tail: cell counts and sorted prefix */
+			if (nRem && dv->sorted) dv->cntValid[s] = 0;
+			if (nRem && dv->tiled && dv->cellValid[s] > first - pop->iStart[s]) dv->cellValid[s] = first - pop->iStart[s];
 			/* chargeCounter[a] += charge[s] per particle (object.c:497) */
 			for (int a = 0; a < K; a++) cnt[a] += pop->charge[s] * (double)hc[a];
 			break;

@@ -22,7 +22,7 @@ static void ws_alloc(pinc_extract_ws_t *ws, long cap) {
 	pinc_check(pinc_hip_malloc((void **)&ws->tail, (cap + 2) * sizeof(int)), "ws");
 	pinc_check(pinc_hip_malloc((void **)&ws->holes, (cap + 2) * sizeof(int)), "ws");
 	pinc_check(pinc_hip_malloc((void **)&ws->order, (cap + 2) * sizeof(int)), "ws");
-	pinc_check(pinc_hip_malloc((void **)&ws->blockHist, (27 * (cap / 1024 + 2)) * sizeof(int)), "ws");
+	pinc_check(pinc_hip_malloc((void **)&ws->blockHist, (PINC_NE_CODES * (cap / 1024 + 2)) * sizeof(int)), "ws");
 	pinc_check(pinc_hip_malloc((void **)&ws->scratch, 128 * sizeof(int)), "ws");
 	pinc_check(pinc_hip_malloc((void **)&ws->buf, 6 * cap * sizeof(double)), "ws");
 	pinc_check(pinc_hip_malloc((void **)&ws->bufNe, cap + 16), "ws");

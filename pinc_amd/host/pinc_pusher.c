@@ -325,6 +325,20 @@ static int push_all(Population *pop, Grid *E, double *const *xout) {
 		a.tileWidth = dv->tileWidth;
 		pinc_check(pinc_hip_memset(a.chunkCount, 0, chunks * sizeof(int), g_pinc.stream), "chunk counts");
 		if (adaptive) a.moved = dv->movedCnt + s;
+		if (dv->objInside && dv->objHi[0] >= dv->objLo[0]) { /* (empty box: no object node in this slab) */
+			a.objInside = dv->objInside;
+			a.objSy = dv->objSy;
+			a.objSz = dv->objSz;
+			a.objNodes = dv->objNodes;
+			a.objCount = dv->objCount + (long)s * dv->objK;
+			for (int d = 0; d < 3; d++) {
+				a.objLo[d] = dv->objLo[d];
+				a.objHi[d] = dv->objHi[d];
+			}
+		}
+		if (dv->objCount)
+			pinc_check(pinc_hip_memset(dv->objCount + (long)s * dv->objK, 0, dv->objK * sizeof(int), g_pinc.stream),
+			           "object counts");
 		/* a species left in order by a sorting push still goes to the
 		 * alternate arrays (swapped for all species), perm = identity */
 		if (sortNow && !sortS[s]) pinc_check(pinc_hip_iota(dv->perm + pop->iStart[s], np, g_pinc.stream), "perm");
@@ -421,6 +435,10 @@ static void classify(Population *pop, int doMove) {
 					                                g_pinc.stream),
 					           "unsort velocities");
 		dv->pending = dv->pendingSorted = 0;
+		/* its object counts go with it */
+		if (dv->objCount)
+			pinc_check(pinc_hip_memset(dv->objCount, 0, (long)PINC_MAX_SPECIES * dv->objK * sizeof(int), g_pinc.stream),
+			           "object counts");
 	}
 	if (doMove && dv->pending) {
 		/* the fused puAcc already moved, classified and deposited */
@@ -482,6 +500,9 @@ static void extract(Population *pop, MpiInfo *m) {
 			break;
 		}
 		pop->iStop[s] -= dv->nEmig[s];
+		/* particles the fused push collected into an object are extracted
+		 * last (PINC_NE_SINK) and not migrated */
+		dv->nEmig[s] -= dv->neCount[s][PINC_NE_SINK];
 		if (dv->depValid) dv->depEnd[s] = pop->iStop[s];
 		if (dv->tiled && dv->cellValid[s] > pop->iStop[s] - pop->iStart[s])
 			dv->cellValid[s] = pop->iStop[s] - pop->iStart[s];

@@ -93,6 +93,7 @@ static PincSim *sim_build(dictionary *ini, const PincSimOpts *opts) {
 	S->solverFree = (void (*)(void *))solverFree;
 	S->spectral = solve == (void (*)())sSolve;
 	S->obj = pinc_obj_create(ini, S->rho);
+	if (S->obj) pinc_obj_attach(S->obj, S->pop);
 	if (S->opts.literal) {
 		/* main.c:226,232 fold rho's ghosts twice; see literal_ghost_weights */
 		S->pop->dev->geom.literal = 1;

@@ -26,16 +26,26 @@ def _sphere(T, c, r):
     return (((x - c[0]) ** 2 + (y - c[1]) ** 2 + (z - c[2]) ** 2) <= r * r).astype(float)
 
 
-@pytest.mark.parametrize("T,sphere,layout", [((16, 16, 16), (8.0, 8.0, 8.0, 2.5), "reference"),
-                                             ((32, 16, 16), (20.3, 7.6, 9.1, 3.2), "reference"),
-                                             ((32, 16, 16), (20.3, 7.6, 9.1, 3.2), "tiled")])
-def test_object_steps_match_checker(built, T, sphere, layout):
+@pytest.mark.parametrize("T,sphere,layout,fused", [((16, 16, 16), (8.0, 8.0, 8.0, 2.5), "reference", 0),
+                                                   ((32, 16, 16), (20.3, 7.6, 9.1, 3.2), "reference", 0),
+                                                   ((32, 16, 16), (20.3, 7.6, 9.1, 3.2), "tiled", 0),
+                                                   ((16, 16, 16), (8.0, 8.0, 8.0, 2.5), "reference", 1),
+                                                   ((32, 16, 16), (20.3, 7.6, 9.1, 3.2), "tiled", 1),
+                                                   ((32, 16, 16), (30.5, 7.6, 15.2, 3.2), "reference", 1)])
+def test_object_steps_match_checker(built, T, sphere, layout, fused):
+    """fused = 1: the push tests the particles that stay against the object
+    and flags them for the next extract (PINC_NE_SINK), the flag pass runs
+    on the immigrants only; removal order differs from the checker's two
+    back-fills (extract, then collect), so particles compare as sets.  The
+    third fused case puts the sphere across the periodic x and z boundaries
+    (immigrants land in it)."""
     from pinc_amd import Sim
     cfg = configs.config("cold3d", true_size=T, nsub=(1, 1, 1))
     cfg["multigrid"]["mgLevels"] = "3"
     cfg["population"]["fused"] = "0"
     cfg["objects"] = {"sphere": ",".join(map(str, sphere))}
     ini = configs.write_ini(cfg)
+    cfg["population"]["fused"] = str(fused)
     if layout == "tiled":
         cfg["population"]["layout"] = "tiled"
         cfg["population"]["sortInterval"] = "2"
@@ -63,7 +73,7 @@ def test_object_steps_match_checker(built, T, sphere, layout):
         for sp in range(2):
             pg, vg = s.particles(sp)
             po, vo, _ = w.particles(sp)
-            if layout == "tiled":
+            if layout == "tiled" or fused:
                 # sorted by tile: compare as sets (positions to 1e-9)
                 def order(p, v):
                     k = np.lexsort(np.round(p * 1e6).T[::-1])
@@ -105,11 +115,16 @@ def test_object_mask_file_equals_sphere(built, tmp_path):
         assert abs(a - b) <= 1e-10 * abs(a)
 
 
-def test_object_two_slabs_match_one(built, tmp_path):
+@pytest.mark.parametrize("capacitance,fused", [("solve", 0), ("green", 0), ("solve", 1)])
+def test_object_two_slabs_match_one(built, tmp_path, capacitance, fused):
     """Two z-slabs (host transport, one GPU): the object's lookups are
     global, phi is read from the replicated solve's global view, charge
     corrections land in the owning slab and the collected charge is summed
-    over the ranks; counts and energies match a one-rank run."""
+    over the ranks; counts and energies match a one-rank run.  green: the
+    unit charge of the translated response sits on the rank holding global
+    node (0,0,0) and the response is read from the replicated potential.
+    fused: the push collects the particles that stay, the flag pass the
+    immigrants (the sphere straddles the slab boundary)."""
     import json
     import os
     import socket
@@ -124,8 +139,8 @@ def test_object_two_slabs_match_one(built, tmp_path):
     def cfg(nsub, T):
         c = configs.config("cold3d", true_size=T, nsub=nsub)
         c["multigrid"]["mgLevels"] = "3"
-        c["population"]["fused"] = "0"
-        c["objects"] = {"sphere": sphere}
+        c["population"]["fused"] = str(fused)
+        c["objects"] = {"sphere": sphere, "capacitance": capacitance}
         return configs.write_ini(c)
 
     one = {"energy": [], "counts": []}
