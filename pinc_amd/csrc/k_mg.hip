@@ -275,6 +275,9 @@ constexpr int kSwZ = 16;       // planes per workgroup
 // interiors in the same L2.  A bijection for any grid, placement only.
 // Measured neutral at C4 (k_gs_sweep4 0.192 ms either way: the march is
 // latency-bound, not L2-miss bound), so off by default.
+#ifndef PINC_MG_S4_SPLIT
+#define PINC_MG_S4_SPLIT 1
+#endif
 #ifndef PINC_MG_SWEEP4C
 #define PINC_MG_SWEEP4C 1
 #endif
@@ -757,35 +760,44 @@ __global__ __launch_bounds__(NT) void k_gs_sweep4c(const double *__restrict__ ph
 #pragma unroll
 	for (int P = 0; P < 2; P++) {
 		r1n[P][0] = mknode(tid, 0, 3, P);
-		r1n[P][1] = mknode(tid + NT, 0, 3, P);
+		// the red 1st nodes beyond NT go to the last threads (the last wave
+		// has no red 2nd node), so no wave does more than three updates in
+		// the first phase of a step
+		r1n[P][1] = mknode(tid - (2 * NT - S::nodes(3)) + NT, 0, 3, P);
 		b1n[P] = mknode(tid, 1, 2, P);
 		r2n[P] = mknode(tid, 0, 1, P);
 	}
-	const bool r1second = tid + NT < S::nodes(3), b1ok = tid < S::nodes(2), r2ok = tid < S::nodes(1);
+	const bool r1second = tid >= 2 * NT - S::nodes(3), b1ok = tid < S::nodes(2), r2ok = tid < S::nodes(1);
 	// the output node (black, 2nd iteration): this thread's tile node
 	const int otx = tid % SX, oty = tid / SX;
 	const unsigned oli = lidx(otx + H, oty + H), olxm = lidx(otx + H - 1, oty + H);
 	const unsigned ooff = (unsigned)((x0 + otx) + (y0 + oty) * TX) * 8u;
 	const int oblack0 = (x0 + otx + y0 + oty) & 1;  // black on even planes
-	// phi halo fetch: region element i = tid + NT k (row-major, HX wide)
+	// phi halo fetch: region element i = tid + NT k (row-major, HX wide);
+	// the third slot's elements on the last threads (those with the fewer
+	// black 1st nodes)
 	unsigned foff[3], fli[3];
 #pragma unroll
 	for (int k = 0; k < 3; k++) {
-		int i = tid + NT * k;
-		if (i >= PL) i = 0;
+		int i = k < 2 ? tid + NT * k : tid - (3 * NT - PL) + 2 * NT;
+		if (i >= PL || i < 0) i = 0;
 		foff[k] = poff(x0 + i % HX - H, y0 + i / HX - H);
 		fli[k] = lidx(i % HX, i / HX);
 	}
-	const bool f2ok = tid + 2 * NT < PL;
+	const bool f2ok = tid >= 3 * NT - PL;
 	auto at = [](const double *base, unsigned byteOff) {
 		return *(const double *)((const char *)base + byteOff);
 	};
 	auto plane = [&](const double *a, int q) { return a + (long)wrapi(q, TZ) * sz; };
+	// every load below is issued unconditionally (idle lanes and steps past
+	// the end load a valid element they do not use): with loads under a
+	// branch the compiler's vmcnt waits cannot count the newer loads in
+	// flight and wait for the prefetch just issued
 	auto fetch = [&](int q, double *f) {
 		const double *b = plane(phiIn, q);
 		f[0] = at(b, foff[0]);
 		f[1] = at(b, foff[1]);
-		if (f2ok) f[2] = at(b, foff[2]);
+		f[2] = at(b, foff[2]);
 	};
 	auto putPhi = [&](int slot, const double *f) {
 		L[slot * PL + fli[0]] = f[0];
@@ -799,16 +811,30 @@ __global__ __launch_bounds__(NT) void k_gs_sweep4c(const double *__restrict__ ph
 	auto fetchRho = [&](int t, int PT, Rho &R) {
 		const double *b3 = plane(rho, t + 3), *b2p = plane(rho, t + 2), *b0 = plane(rho, t), *bm = plane(rho, t - 2);
 		R.r1[0] = at(b3, r1n[PT ^ 1][0].roff);
-		if (r1second) R.r1[1] = at(b3, r1n[PT ^ 1][1].roff);
+		R.r1[1] = at(b3, r1n[PT ^ 1][1].roff);
 		R.b1 = at(b2p, b1n[PT].roff);
 		R.r2 = at(b0, r2n[PT].roff);
 		R.b2 = at(bm, ooff);
 	};
-	// GS update of node n on ring slot SL (neighbours on slots SM, SP)
+	// GS update of node n on ring slot SL (neighbours on slots SM, SP).
+	// PINC_MG_S4_SPLIT: the second read of each neighbour pair goes through
+	// an index the compiler cannot relate to the first (an empty asm), so
+	// the pairs stay two ds_read_b64 (2 LDS cycles each) instead of merging
+	// into ds_read2_b64 / ds_read2st64_b64 (8 cycles, half the rate)
 	auto upd = [&](int SL, int SM, int SP, unsigned li, unsigned lxm, double r) {
+#if PINC_MG_S4_SPLIT
+		unsigned ixp = lxm + 1, iyp = li + HX, izp = li;
+		asm volatile("" : "+v"(ixp));
+		asm volatile("" : "+v"(iyp));
+		asm volatile("" : "+v"(izp));
+		const double xm = L[SL * PL + lxm], xp = L[SL * PL + ixp];
+		const double ym = L[SL * PL + li - HX], yp = L[SL * PL + iyp];
+		const double zm = L[SM * PL + li], zp = L[SP * PL + izp];
+#else
 		const double xm = L[SL * PL + lxm], xp = L[SL * PL + lxm + 1];
 		const double ym = L[SL * PL + li - HX], yp = L[SL * PL + li + HX];
 		const double zm = L[SM * PL + li], zp = L[SP * PL + li];
+#endif
 		return (1. / 6.) * (xp + xm + yp + ym + zp + zm + r);
 	};
 
@@ -820,23 +846,27 @@ __global__ __launch_bounds__(NT) void k_gs_sweep4c(const double *__restrict__ ph
 		putPhi(q & 7, F[0]);
 	}
 	fetch(z0 - 1, F[1]);
-	Rho RA, RB, RC;
-	fetchRho(z0 - 6, 0, RA);
-	fetchRho(z0 - 5, 1, RB);
+	// rho of step k in R[k % 3], loaded two steps ahead; the unroll over 24
+	// steps keeps the rotation in register names (a copy of a set just
+	// loaded would wait for its loads every step)
+	Rho R[3];
+	fetchRho(z0 - 6, 0, R[0]);
+	fetchRho(z0 - 5, 1, R[1]);
 	__syncthreads();
 	const int zEnd = z0 + zPlanes;  // outputs z0 .. zEnd-1
-	// steps s = z0-6 .. zEnd+1: zPlanes + 8 of them, in blocks of 8 starting
-	// at s = 2 (mod 8), so plane s+d sits in slot (2 + k + d) & 7
-	for (int s0 = z0 - 6; s0 <= zEnd + 1; s0 += 8) {
+	// steps s = z0-6 .. zEnd+1: zPlanes + 8 of them (a multiple of 24), in
+	// blocks of 24 starting at s = 2 (mod 8), so plane s+d sits in slot
+	// (2 + k + d) & 7
+	for (int s0 = z0 - 6; s0 <= zEnd + 1; s0 += 24) {
 #pragma unroll
-		for (int k = 0; k < 8; k++) {
+		for (int k = 0; k < 24; k++) {
 			const int s = s0 + k;
 			const int P = k & 1;  // parity of s (s0 even)
 			auto sl = [&](int d) { return (2 + k + d) & 7; };
-			if (s <= zEnd) {  // two steps ahead of their use
-				fetch(s + 6, F[P]);
-				fetchRho(s + 2, P, RC);
-			}
+			Rho &RA = R[k % 3];
+			// two steps ahead of their use (the last step's loads are unused)
+			fetch(s + 6, F[P]);
+			fetchRho(s + 2, P, R[(k + 2) % 3]);
 			if (s + 3 <= zEnd + 2) {  // red, 1st iteration, plane s+3 (parity P^1)
 				const S4Node &a = r1n[P ^ 1][0], &b = r1n[P ^ 1][1];
 				const double va = upd(sl(3), sl(2), sl(4), a.li, a.lxm, RA.r1[0]);
@@ -849,10 +879,12 @@ __global__ __launch_bounds__(NT) void k_gs_sweep4c(const double *__restrict__ ph
 				const S4Node &a = r2n[P];
 				L[sl(0) * PL + a.li] = upd(sl(0), sl(-1), sl(1), a.li, a.lxm, RA.r2);
 			}
-			if (s - 2 >= z0 && s - 2 < zEnd) {  // black, 2nd, plane s-2: out
+			{  // black, 2nd, plane s-2: out.  Before the first output plane the
+			   // store goes to plane z0, rewritten with its value later (the
+			   // store is unconditional for the same reason as the loads)
 				double v = L[sl(-2) * PL + oli];
 				if (oblack0 ^ P) v = upd(sl(-2), sl(-3), sl(-1), oli, olxm, RA.b2);
-				*(double *)((char *)plane(phiOut, s - 2) + ooff) = v;
+				*(double *)((char *)plane(phiOut, s - 2 >= z0 ? s - 2 : z0) + ooff) = v;
 			}
 			__syncthreads();
 			if (s + 2 >= z0 - 2 && s + 2 <= zEnd + 1 && b1ok) {  // black, 1st, plane s+2
@@ -862,8 +894,6 @@ __global__ __launch_bounds__(NT) void k_gs_sweep4c(const double *__restrict__ ph
 			// phi s+5 into the slot of s-3 (last read by the black output above)
 			putPhi(sl(5), F[P ^ 1]);
 			__syncthreads();
-			RA = RB;
-			RB = RC;
 		}
 	}
 }
@@ -1231,8 +1261,8 @@ extern "C" int pinc_hip_gs_sweep2x(const double *phiIn, double *phiOut, const do
 	long cols = (long)(L.T[0] / 32) * (L.T[1] / 8);
 	int zp = 16;
 	for (int z = 64; z > 16; z /= 2)
-		if (L.T[2] % z == 0 && cols * (L.T[2] / z) >= 1024) {
-			zp = z;
+		if (L.T[2] % z == 0 && cols * (L.T[2] / z) >= 1024 && (!PINC_MG_SWEEP4C || (z + 8) % 24 == 0)) {
+			zp = z;  // k_gs_sweep4c marches in blocks of 24 steps: zPlanes + 8 = 24 m
 			break;
 		}
 	unsigned nb = (unsigned)(cols * (L.T[2] / zp));
