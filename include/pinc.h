@@ -214,6 +214,8 @@ SpectralSolver *sAlloc(const dictionary *ini, Grid *rho, Grid *phi);
 void sFree(SpectralSolver *solver);
 void sSolve(SpectralSolver *solver, Grid *rho, Grid *phi, const MpiInfo *mpiInfo);
 long sSolveCount(const SpectralSolver *solver);
+/* 1 if the solve is slab-distributed (several ranks, 3-D), 0 if gathered */
+int sSolveDistributed(const SpectralSolver *solver);
 
 /* ------------------------------------------------ immersed objects -- */
 /* object.c on the device (pinc_obj.c): objects
@@ -284,6 +286,7 @@ long pinc_sim_cycles(const PincSim *sim);
 int pinc_sim_mg_limit(PincSim *sim, long maxCycles, long histCap);
 int pinc_sim_mg_levels(PincSim *sim);  /* levels of the multigrid hierarchy in use */
 int pinc_sim_mg_shard(PincSim *sim);   /* mgShardHalo of the solver (0: replicated or spectral) */
+int pinc_sim_spectral_distributed(PincSim *sim); /* sSolveDistributed (0 for multigrid) */
 long pinc_sim_mg_history(PincSim *sim, double *out, long cap);
 int pinc_sim_nspecies(const PincSim *sim);
 int pinc_sim_ndims(const PincSim *sim);

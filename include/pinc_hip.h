@@ -386,6 +386,25 @@ int pinc_hip_fft_create(pinc_fft_t **plan, int nd, const int *T, void *stream);
 int pinc_hip_fft_poisson(pinc_fft_t *plan, const double *rhoGlobal, double *phiGlobal, void *stream);
 void pinc_hip_fft_destroy(pinc_fft_t *plan);
 
+/* Slab-distributed 3-D spectral solve (several ranks,
+ * z-slabs of nloc planes, Ty divisible by the rank count): the same operator
+ * as pinc_hip_fft_poisson without gathering rho.
+ *   forward   rho slab (nloc planes, x fastest) -> batched 2-D r2c -> the
+ *             send buffer S, blocks [q][zl][yl][kx] (block q: ky rows
+ *             [q Ty/P, (q+1) Ty/P))
+ *   (host)    block q of S to rank q into block r of B on rank q
+ *   kspace    B = [z][yl][kx]: c2c along z, the k-space factor, inverse c2c
+ *   (host)    block q of B (z rows of slab q) to rank q into block r of S
+ *   backward  S -> unpack -> batched 2-D c2r -> phi slab (nloc planes)
+ * buffers: S and B device pointers, bytes per block (P blocks each). */
+typedef struct pinc_fft_slab_s pinc_fft_slab_t;
+int pinc_hip_fft_slab_create(pinc_fft_slab_t **plan, const int *T, int nloc, int nranks, int rank, void *stream);
+int pinc_hip_fft_slab_buffers(pinc_fft_slab_t *plan, void **S, void **B, long *blockBytes);
+int pinc_hip_fft_slab_forward(pinc_fft_slab_t *plan, const double *rhoSlab, void *stream);
+int pinc_hip_fft_slab_kspace(pinc_fft_slab_t *plan, void *stream);
+int pinc_hip_fft_slab_backward(pinc_fft_slab_t *plan, double *phiSlab, void *stream);
+void pinc_hip_fft_slab_destroy(pinc_fft_slab_t *plan);
+
 /* ------------------------------------------------------------ comm -- */
 /* RCCL communicator over xGMI (one process per GPU).  id is the 128-byte
  * ncclUniqueId produced by pinc_hip_comm_unique_id on rank 0 and

@@ -166,3 +166,229 @@ extern "C" void pinc_hip_fft_destroy(pinc_fft_t *f) {
 		g_rocfft_ready = false;
 	}
 }
+
+// --------------------------------------------------- slab-distributed 3-D ---
+// the 3-D solve over P z-slabs without gathering rho.  Rank
+// r holds planes [r nloc, (r+1) nloc).
+//   1. batched 2-D r2c over its planes:        A [zl][y][kx]   (kx < Mx)
+//   2. pack by destination ky block (Ty/P rows): S [q][zl][yl][kx]
+//   3. all-to-all (host: pinc_comm_exchange):  B [p][zl][yl][kx] = [z][yl][kx],
+//      rank r now holds ky in [r Tyl, (r+1) Tyl) for every z
+//   4. 1-D c2c along z (stride Tyl Mx), the factor of k_spectral_scale at
+//      the global (kx, ky, kz), inverse c2c along z
+//   5. all-to-all back (B's z blocks to their slabs) into S, unpack into A,
+//      batched 2-D c2r into the phi slab.
+// The same operator as the single-plan solve; the transforms are split, so
+// results agree to FFT round-off, not bit for bit.
+struct pinc_fft_slab_s {
+	int T[3], nloc, P, rank, Tyl, Mx;
+	long nBlock;      // complex values per (rank pair) block: nloc * Tyl * Mx
+	rocfft_plan fwd2, inv2, zfwd, zinv;
+	rocfft_execution_info info;
+	void *work;
+	double *rin;
+	double2 *A, *S, *B;
+};
+
+namespace {
+
+__global__ void k_slab_pack(const double2 *__restrict__ A, double2 *__restrict__ S, int nloc, int Ty, int Tyl, int Mx,
+                            int P) {
+	// S [q][zl][yl][kx] <- A [zl][q Tyl + yl][kx]
+	const long n = (long)P * nloc * Tyl * Mx;
+	for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+		const int kx = (int)(i % Mx);
+		long r = i / Mx;
+		const int yl = (int)(r % Tyl);
+		r /= Tyl;
+		const int zl = (int)(r % nloc);
+		const int q = (int)(r / nloc);
+		S[i] = A[((long)zl * Ty + (long)q * Tyl + yl) * Mx + kx];
+	}
+}
+
+__global__ void k_slab_unpack(const double2 *__restrict__ S, double2 *__restrict__ A, int nloc, int Ty, int Tyl,
+                              int Mx, int P) {
+	// A [zl][p Tyl + yl][kx] <- S [p][zl][yl][kx]
+	const long n = (long)P * nloc * Tyl * Mx;
+	for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+		const int kx = (int)(i % Mx);
+		long r = i / Mx;
+		const int yl = (int)(r % Tyl);
+		r /= Tyl;
+		const int zl = (int)(r % nloc);
+		const int p = (int)(r / nloc);
+		A[((long)zl * Ty + (long)p * Tyl + yl) * Mx + kx] = S[i];
+	}
+}
+
+// B [z][yl][kx] *= factor at (kx, ky = y0 + yl, kz = z): k_spectral_scale's 3-D
+// branch
+__global__ void k_slab_scale(double2 *__restrict__ B, int Tx, int Ty, int Tz, int Tyl, int y0, double Ntot) {
+	const int Mx = Tx / 2 + 1;
+	const long n = (long)Tz * Tyl * Mx;
+	for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+		const int ix = (int)(i % Mx);
+		long r = i / Mx;
+		const int iy = y0 + (int)(r % Tyl);
+		const int iz = (int)(r / Tyl);
+		double f;
+		if (ix == 0 && iy == 0 && iz == 0) {
+			f = 0.0;  // charge neutrality (spectral.c:103-104)
+		} else {
+			const int ny = iy <= Ty / 2 ? iy : iy - Ty;
+			const int nz = iz <= Tz / 2 ? iz : iz - Tz;
+			const double kx = 2 * M_PI * ix / Tx, ky = 2 * M_PI * ny / Ty, kz = 2 * M_PI * nz / Tz;
+			f = 1.0 / (kx * kx + ky * ky + kz * kz);
+			f /= Ntot;
+		}
+		double2 v = B[i];
+		v.x *= f;
+		v.y *= f;
+		B[i] = v;
+	}
+}
+
+unsigned slab_blocks(long n) {
+	long b = (n + 255) / 256;
+	return (unsigned)(b > 8192 ? 8192 : (b < 1 ? 1 : b));
+}
+
+}  // namespace
+
+extern "C" void pinc_hip_fft_slab_destroy(pinc_fft_slab_t *f) {
+	if (!f) return;
+	if (f->fwd2) rocfft_plan_destroy(f->fwd2);
+	if (f->inv2) rocfft_plan_destroy(f->inv2);
+	if (f->zfwd) rocfft_plan_destroy(f->zfwd);
+	if (f->zinv) rocfft_plan_destroy(f->zinv);
+	if (f->info) rocfft_execution_info_destroy(f->info);
+	(void)hipFree(f->work);
+	(void)hipFree(f->rin);
+	(void)hipFree(f->A);
+	(void)hipFree(f->S);
+	(void)hipFree(f->B);
+	free(f);
+	if (--g_rocfft_plans == 0 && g_rocfft_ready) {
+		(void)rocfft_cleanup();
+		g_rocfft_ready = false;
+	}
+}
+
+extern "C" int pinc_hip_fft_slab_create(pinc_fft_slab_t **out, const int *T, int nloc, int nranks, int rank,
+                                        void *stream) {
+	(void)stream;
+	*out = nullptr;
+	if (T[0] % 2 || nranks < 1 || T[1] % nranks || T[2] != nloc * nranks || rank < 0 || rank >= nranks)
+		return set_error(hipErrorInvalidValue, "fft_slab_create: even Tx, Ty divisible by the ranks, Tz = nloc ranks");
+	if (!g_rocfft_ready) {
+		if (int rc = fft_error(rocfft_setup(), "rocfft_setup")) return rc;
+		g_rocfft_ready = true;
+	}
+	pinc_fft_slab_t *f = (pinc_fft_slab_t *)calloc(1, sizeof(pinc_fft_slab_t));
+	g_rocfft_plans++;
+	for (int d = 0; d < 3; d++) f->T[d] = T[d];
+	f->nloc = nloc;
+	f->P = nranks;
+	f->rank = rank;
+	f->Tyl = T[1] / nranks;
+	f->Mx = T[0] / 2 + 1;
+	f->nBlock = (long)nloc * f->Tyl * f->Mx;
+	const long nSpec = f->nBlock * nranks;  // = nloc Ty Mx = Tz Tyl Mx
+	size_t len2[2] = {(size_t)T[0], (size_t)T[1]};
+	rocfft_status s = rocfft_plan_create(&f->fwd2, rocfft_placement_notinplace, rocfft_transform_type_real_forward,
+	                                     rocfft_precision_double, 2, len2, (size_t)nloc, nullptr);
+	if (s == rocfft_status_success)
+		s = rocfft_plan_create(&f->inv2, rocfft_placement_notinplace, rocfft_transform_type_real_inverse,
+		                       rocfft_precision_double, 2, len2, (size_t)nloc, nullptr);
+	// along z: length Tz, stride Tyl Mx, one transform per (yl, kx)
+	rocfft_plan_description desc = nullptr;
+	if (s == rocfft_status_success) s = rocfft_plan_description_create(&desc);
+	size_t lenz[1] = {(size_t)T[2]}, strz[1] = {(size_t)f->Tyl * f->Mx};
+	if (s == rocfft_status_success)
+		s = rocfft_plan_description_set_data_layout(desc, rocfft_array_type_complex_interleaved,
+		                                            rocfft_array_type_complex_interleaved, nullptr, nullptr, 1, strz, 1, 1,
+		                                            strz, 1);
+	if (s == rocfft_status_success)
+		s = rocfft_plan_create(&f->zfwd, rocfft_placement_inplace, rocfft_transform_type_complex_forward,
+		                       rocfft_precision_double, 1, lenz, strz[0], desc);
+	if (s == rocfft_status_success)
+		s = rocfft_plan_create(&f->zinv, rocfft_placement_inplace, rocfft_transform_type_complex_inverse,
+		                       rocfft_precision_double, 1, lenz, strz[0], desc);
+	if (desc) rocfft_plan_description_destroy(desc);
+	size_t w = 0;
+	rocfft_plan plans[4] = {f->fwd2, f->inv2, f->zfwd, f->zinv};
+	for (int k = 0; k < 4 && s == rocfft_status_success; k++) {
+		size_t wk = 0;
+		s = rocfft_plan_get_work_buffer_size(plans[k], &wk);
+		if (wk > w) w = wk;
+	}
+	if (s == rocfft_status_success) s = rocfft_execution_info_create(&f->info);
+	if (s != rocfft_status_success) {
+		pinc_hip_fft_slab_destroy(f);
+		return fft_error(s, "fft_slab_create: plans");
+	}
+	hipError_t e = hipSuccess;
+	if (w) e = hipMalloc(&f->work, w);
+	if (e == hipSuccess) e = hipMalloc((void **)&f->rin, (size_t)nloc * T[0] * T[1] * sizeof(double));
+	if (e == hipSuccess) e = hipMalloc((void **)&f->A, nSpec * sizeof(double2));
+	if (e == hipSuccess) e = hipMalloc((void **)&f->S, nSpec * sizeof(double2));
+	if (e == hipSuccess) e = hipMalloc((void **)&f->B, nSpec * sizeof(double2));
+	if (e != hipSuccess) {
+		pinc_hip_fft_slab_destroy(f);
+		return set_error(e, "fft_slab_create: buffers");
+	}
+	if (w && (s = rocfft_execution_info_set_work_buffer(f->info, f->work, w)) != rocfft_status_success) {
+		pinc_hip_fft_slab_destroy(f);
+		return fft_error(s, "fft_slab_create: work buffer");
+	}
+	*out = f;
+	return 0;
+}
+
+extern "C" int pinc_hip_fft_slab_buffers(pinc_fft_slab_t *f, void **S, void **B, long *blockBytes) {
+	*S = f->S;
+	*B = f->B;
+	*blockBytes = f->nBlock * (long)sizeof(double2);
+	return 0;
+}
+
+extern "C" int pinc_hip_fft_slab_forward(pinc_fft_slab_t *f, const double *rhoSlab, void *stream) {
+	hipStream_t st = (hipStream_t)stream;
+	hipError_t e = hipMemcpyAsync(f->rin, rhoSlab, (size_t)f->nloc * f->T[0] * f->T[1] * sizeof(double),
+	                              hipMemcpyDeviceToDevice, st);
+	if (e != hipSuccess) return set_error(e, "fft_slab_forward: copy");
+	rocfft_status s = rocfft_execution_info_set_stream(f->info, st);
+	void *in[1] = {f->rin}, *out[1] = {f->A};
+	if (s == rocfft_status_success) s = rocfft_execute(f->fwd2, in, out, f->info);
+	if (s != rocfft_status_success) return fft_error(s, "fft_slab_forward: r2c");
+	hipLaunchKernelGGL(k_slab_pack, dim3(slab_blocks(f->nBlock * f->P)), dim3(256), 0, st, f->A, f->S, f->nloc,
+	                   f->T[1], f->Tyl, f->Mx, f->P);
+	return check_launch("fft_slab_forward: pack");
+}
+
+extern "C" int pinc_hip_fft_slab_kspace(pinc_fft_slab_t *f, void *stream) {
+	hipStream_t st = (hipStream_t)stream;
+	rocfft_status s = rocfft_execution_info_set_stream(f->info, st);
+	void *io[1] = {f->B};
+	if (s == rocfft_status_success) s = rocfft_execute(f->zfwd, io, nullptr, f->info);
+	if (s != rocfft_status_success) return fft_error(s, "fft_slab_kspace: z forward");
+	hipLaunchKernelGGL(k_slab_scale, dim3(slab_blocks(f->nBlock * f->P)), dim3(256), 0, st, f->B, f->T[0], f->T[1],
+	                   f->T[2], f->Tyl, f->rank * f->Tyl, (double)f->T[0] * f->T[1] * f->T[2]);
+	if (int rc = check_launch("fft_slab_kspace: scale")) return rc;
+	s = rocfft_execute(f->zinv, io, nullptr, f->info);
+	if (s != rocfft_status_success) return fft_error(s, "fft_slab_kspace: z inverse");
+	return 0;
+}
+
+extern "C" int pinc_hip_fft_slab_backward(pinc_fft_slab_t *f, double *phiSlab, void *stream) {
+	hipStream_t st = (hipStream_t)stream;
+	hipLaunchKernelGGL(k_slab_unpack, dim3(slab_blocks(f->nBlock * f->P)), dim3(256), 0, st, f->S, f->A, f->nloc,
+	                   f->T[1], f->Tyl, f->Mx, f->P);
+	if (int rc = check_launch("fft_slab_backward: unpack")) return rc;
+	rocfft_status s = rocfft_execution_info_set_stream(f->info, st);
+	void *in[1] = {f->A}, *out[1] = {phiSlab};
+	if (s == rocfft_status_success) s = rocfft_execute(f->inv2, in, out, f->info);
+	if (s != rocfft_status_success) return fft_error(s, "fft_slab_backward: c2r");
+	return 0;
+}

@@ -56,9 +56,9 @@ void pinc_comm_exchange(int nOps, const int *sendPeer, void *const *sendbuf, con
 	long tot = 0;
 	for (int i = 0; i < nOps; i++) tot += sendBytes[i] + recvBytes[i];
 	unsigned char *h = stage(tot);
-	const void *hs[8];
-	void *hr[8];
-	if (nOps > 8) msg(ERROR, "host transport: too many exchange ops");
+	const void **hs = malloc(nOps * sizeof(*hs));
+	void **hr = malloc(nOps * sizeof(*hr));
+	if (!hs || !hr) msg(ERROR, "host transport: out of memory");
 	long off = 0;
 	for (int i = 0; i < nOps; i++) {
 		hs[i] = h + off;
@@ -73,6 +73,8 @@ void pinc_comm_exchange(int nOps, const int *sendPeer, void *const *sendbuf, con
 		msg(ERROR, "host transport exchange failed (%s)", what);
 	for (int i = 0; i < nOps; i++)
 		if (recvBytes[i]) pinc_check(pinc_hip_h2d(recvbuf[i], hr[i], recvBytes[i], g_pinc.stream), what);
+	free(hs);
+	free(hr);
 }
 
 void pinc_comm_allgather(const double *send, double *recv, long count, const char *what) {

@@ -303,6 +303,7 @@ void gHaloOp(funPtr sliceOp, Grid *grid, const MpiInfo *mpiInfo, opDirection dir
 			           "halo");
 		}
 		dv->ghostsValid = 1;
+		if (dv->ext == dv->d) dv->extStale = 0; /* the slab is the extended view */
 		return;
 	}
 	msg(ERROR, "gHaloOp: unsupported slice operation / direction on the device path");
@@ -321,7 +322,9 @@ void gFinDiff1st(const Grid *scalar, Grid *field) {
 		g.T[g.nd - 1] = scalar->dev->extPlanes;
 		g.off = scalar->dev->extOff;
 		pinc_check(pinc_hip_efield(scalar->dev->ext, g, field->dev->d, g_pinc.stream), "efield");
-		field->dev->ghostsValid = 1;
+		/* a halo of one plane gives E on the true planes only: its ghost
+		 * planes then come from the neighbours (TOHALO) */
+		field->dev->ghostsValid = sv->extOff >= 2;
 		return;
 	}
 	const double *phi = scalar->dev->global ? scalar->dev->global : scalar->dev->d + scalar->dev->planeSize;
@@ -445,10 +448,12 @@ void gSyncToDevice(Grid *grid) {
 	free(tmp);
 	if (dv->ext) {
 		/* sharded multigrid: the owned planes of the extended slab (its halo
-		 * is refreshed before every smoothing chunk) */
+		 * is refreshed before every smoothing chunk); distributed spectral:
+		 * the slab itself */
 		long ps = dv->planeSize;
-		pinc_check(pinc_hip_d2d(dv->ext + (long)dv->extOff * ps, dv->d + ps, ps * dv->geom.nloc * sizeof(double),
-		                        g_pinc.stream), "gSyncToDevice ext");
+		if (dv->ext != dv->d)
+			pinc_check(pinc_hip_d2d(dv->ext + (long)dv->extOff * ps, dv->d + ps, ps * dv->geom.nloc * sizeof(double),
+			                        g_pinc.stream), "gSyncToDevice ext");
 		dv->ghostsValid = 0;
 		dv->extStale = 1;
 		return;

@@ -112,6 +112,11 @@ class Sim:
         """Halo planes of the sharded multigrid level 0 (0: replicated solve)."""
         return HOST.pinc_sim_mg_shard(self._h)
 
+    @property
+    def spectral_distributed(self) -> bool:
+        """The spectral solve is slab-distributed (no gather of rho)."""
+        return bool(HOST.pinc_sim_spectral_distributed(self._h))
+
     def mg_history(self) -> np.ndarray:
         """RMS residual after each V-cycle of the last solve (mgHistory)."""
         n = HOST.pinc_sim_mg_history(self._h, None, 0)

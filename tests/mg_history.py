@@ -41,7 +41,8 @@ def make_rho(size: int, seed: int, amp: float) -> np.ndarray:
     return out
 
 
-def ini_for(size: int, levels: int, native: bool, nranks: int = 1, shard: str | None = None) -> str:
+def ini_for(size: int, levels: int, native: bool, nranks: int = 1, shard: str | None = None,
+            spectral: bool = False) -> str:
     from pinc_amd import configs
     cfg = configs.config("warm", true_size=(size, size, size // nranks), nsub=(1, 1, nranks), ppc=1, nalloc_pc=2,
                          levels=levels)
@@ -49,6 +50,8 @@ def ini_for(size: int, levels: int, native: bool, nranks: int = 1, shard: str | 
         cfg["multigrid"]["native"] = "1"
     if shard is not None:
         cfg["multigrid"]["shard"] = shard
+    if spectral:
+        cfg["methods"]["poisson"] = "sSolver"
     return configs.write_ini(cfg)
 
 

@@ -26,6 +26,7 @@ def main() -> int:
     ap.add_argument("--solves", type=int, default=2)
     ap.add_argument("--seed", type=int, default=20261016)
     ap.add_argument("--out", required=True)
+    ap.add_argument("--spectral", action="store_true", help="sSolver (slab-distributed) instead of the multigrid")
     args = ap.parse_args()
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     import torch.distributed as dist
@@ -33,17 +34,21 @@ def main() -> int:
     import mg_history
     from pinc_amd import Sim
     from pinc_amd.transport import GlooTransport
-    ini = mg_history.ini_for(args.size, args.levels, True, nranks=world, shard="1")
+    ini = mg_history.ini_for(args.size, args.levels, True, nranks=world, shard="1", spectral=args.spectral)
     rho = mg_history.rank_slab(mg_history.make_rho(args.size, args.seed, 1.0), rank, world)
     out = {}
     try:
         with Sim(ini, rank=rank, nranks=world, device=0, transport=GlooTransport(), perturb=False) as s:
-            s.mg_limit(args.cycles, args.cycles)
-            out["halo"] = np.array(s.mg_shard)
+            if args.spectral:
+                out["distributed"] = np.array(s.spectral_distributed)
+            else:
+                s.mg_limit(args.cycles, args.cycles)
+                out["halo"] = np.array(s.mg_shard)
             for k in range(args.solves):
                 s.set_grid(0, rho)
                 s.op("solve")
-                out[f"hist{k}"] = s.mg_history()
+                if not args.spectral:
+                    out[f"hist{k}"] = s.mg_history()
             out["phi"] = s.grid(1)[..., 0].copy()
             s.op("efield")
             out["E"] = s.grid(2).copy()
