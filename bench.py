@@ -326,7 +326,7 @@ def main() -> int:
     ROCPROF_NAMES["push"] = "k_push<3, true, true, *>"
     if args.mg == "native":
         # two red-black iterations per launch (24 B per point: phi R+W, rho R)
-        ROCPROF_NAMES["gs_pass"] = "k_gs_sweep4<32, 8, 256>"
+        ROCPROF_NAMES["gs_pass"] = "k_gs_sweep4c<32, 8, 256>"
     for k, p in probes.items():
         if p["samples"] == 0 or p["mean_ms"] <= 0:
             continue
