@@ -187,6 +187,14 @@ def main() -> int:
     if world != args.gpus:
         print(f"WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
         return 2
+    # the result line goes to the real stdout; with several ranks, fd 1 is
+    # pointed at stderr for everything else, because gloo's C++ layer prints
+    # its connection messages to stdout (and flushes them at exit)
+    out = sys.stdout
+    if world > 1:
+        sys.stdout.flush()
+        out = os.fdopen(os.dup(1), "w")
+        os.dup2(2, 1)
 
     import torch
     if args.host_transport:
@@ -422,7 +430,7 @@ def main() -> int:
         result["cpu_baseline"] = _cpu_baseline(S if c2 else args.cpu_size, args.ppc, args.cpu_steps,
                                                args.mg == "native", args.workload if args.workload != "c5" else "c4")
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        print(json.dumps(result), file=out, flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

@@ -59,37 +59,37 @@ def test_one_rank_shard_matches_native_oracle(size):
     assert np.max(np.abs(g["phi"] - o["phi"])) <= 1e-9 * np.max(np.abs(o["phi"]))
 
 
-def _two_ranks(size, levels, tmp_path, fused_min=None, cycles=60, solves=2):
+def _two_ranks(size, levels, tmp_path, fused_min=None, cycles=60, solves=2, world=2):
     out = tmp_path / "shard"
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2")
     if fused_min is not None:
         env["PINC_MG_FUSED_MIN"] = str(fused_min)
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr=127.0.0.1", f"--master-port={_port()}", str(ROOT / "tests" / "shard_worker.py"),
            "--size", str(size), "--levels", str(levels), "--cycles", str(cycles), "--solves", str(solves),
            "--out", str(out)]
     p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
-    return [dict(np.load(f"{out}_r{r}.npz")) for r in range(2)]
+    return [dict(np.load(f"{out}_r{r}.npz")) for r in range(world)]
 
 
-def _oracle_two_ranks(size, levels, cycles=60, solves=2):
+def _oracle_two_ranks(size, levels, cycles=60, solves=2, world=2):
     import orc
-    ini = mg_history.ini_for(size, levels, True, nranks=2)
+    ini = mg_history.ini_for(size, levels, True, nranks=world)
     rho = mg_history.make_rho(size, 20261016, 1.0)
     try:
         w = orc.World(ini)
-        assert w.nranks == 2
+        assert w.nranks == world
         w.mg_limit(cycles, cycles)
         hists = []
         for _ in range(solves):
-            for r in range(2):
-                w.set_grid(0, mg_history.rank_slab(rho, r, 2), rank=r)
+            for r in range(world):
+                w.set_grid(0, mg_history.rank_slab(rho, r, world), rank=r)
             w.op("solve")
             hists.append(w.mg_history())
-        phi = [w.grid(1, rank=r)[..., 0].copy() for r in range(2)]
+        phi = [w.grid(1, rank=r)[..., 0].copy() for r in range(world)]
         w.op("efield")
-        E = [w.grid(2, rank=r).copy() for r in range(2)]
+        E = [w.grid(2, rank=r).copy() for r in range(world)]
         w.close()
     finally:
         os.unlink(ini)
@@ -114,6 +114,21 @@ def test_two_ranks_shard_matches_oracle(tmp_path, size, levels, fused_min):
         escale = max(np.max(np.abs(e[inner])) for e in Eo)
         assert np.max(np.abs(g[r]["E"][inner] - Eo[r][inner])) <= 1e-8 * escale
     assert g[0]["hist0"][-1] <= 1e-10
+
+
+def test_four_ranks_shard_matches_oracle(tmp_path):
+    """Four z-slabs of 32 planes at 128^3 -- one rank's level-0 geometry at
+    C4 on 8 GPUs (24 halo planes, 80-plane extended slab), and distinct
+    z-1 / z+1 neighbours -- against the oracle's four-rank native solve."""
+    world = 4
+    g = _two_ranks(128, 5, tmp_path, world=world)
+    ho, po, Eo = _oracle_two_ranks(128, 5, world=world)
+    scale = max(np.max(np.abs(p[1:-1])) for p in po)
+    for r in range(world):
+        assert int(g[r]["halo"]) == 24
+        for k in range(2):
+            _check_hist(g[r][f"hist{k}"], ho[k])
+        assert np.max(np.abs(g[r]["phi"][1:-1] - po[r][1:-1])) <= 1e-9 * scale
 
 
 def test_shard_off_below_threshold(tmp_path):
