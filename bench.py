@@ -139,8 +139,8 @@ def _cpu_baseline(size: int, ppc: int, steps: int, native: bool, workload: str =
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=8)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="c4", choices=["c4", "c3", "c5", "c2"],
                     help="c4: warm 3-D plasma, 256^3, 64 ppc, multigrid (BASELINE.json metric, default); "
                          "c3: Maxwellian 128^3, 32 ppc, spectral (rocFFT) Poisson solve; "
