@@ -36,6 +36,23 @@ def main() -> int:
     assert t.struct.exchange(None, 2, sp, sb, snb, rp, rb, rnb) == 0
     assert np.all(r0 == 100.0 * dn + 1), (r, r0)
     assert np.all(r1 == 100.0 * up + 2), (r, r1)
+    # all-to-all as the slab-distributed spectral solve drives it
+    # (pinc_spectral.c all_to_all): op i sends block (r+i)%P to rank (r+i)%P
+    # and receives block (r-i)%P from rank (r-i)%P, P-1 ops, tag i
+    n = P - 1
+    if n > 0:
+        blk = 6
+        src = np.concatenate([np.full(blk, 1000.0 * r + q) for q in range(P)])
+        dst = np.zeros(blk * P)
+        sp = (C.c_int * n)(*[(r + i) % P for i in range(1, P)])
+        rp = (C.c_int * n)(*[(r - i + P) % P for i in range(1, P)])
+        sb = (C.c_void_p * n)(*[src.ctypes.data + ((r + i) % P) * blk * 8 for i in range(1, P)])
+        rb = (C.c_void_p * n)(*[dst.ctypes.data + ((r - i + P) % P) * blk * 8 for i in range(1, P)])
+        nb = (C.c_long * n)(*([blk * 8] * n))
+        assert t.struct.exchange(None, n, sp, sb, nb, rp, rb, nb) == 0
+        dst[r * blk:(r + 1) * blk] = src[r * blk:(r + 1) * blk]
+        # block p of dst is what rank p sent for this rank: value 1000 p + r
+        assert np.array_equal(dst, np.concatenate([np.full(blk, 1000.0 * p + r) for p in range(P)])), (r, dst)
     # allgather of one slab per rank
     cnt = 4
     a = np.arange(cnt, dtype=np.float64) + 10.0 * r
