@@ -63,10 +63,11 @@ __global__ __launch_bounds__(kThreads) void k_gs_pass(double *__restrict__ phi,
 	double acc = 0.;
 	for (long q = (long)blockIdx.x * blockDim.x + threadIdx.x; q < nPairs; q += (long)gridDim.x * blockDim.x) {
 		int c[3];
-		long r = q / half;
-		int i = (int)(q - r * half);
-		c[1] = (int)(r % L.T[1]);
-		c[2] = (int)(r / L.T[1]);
+		const unsigned uq = (unsigned)q, uh = (unsigned)half, t1 = (unsigned)L.T[1];
+		const unsigned r = uq / uh;  // 32-bit index arithmetic (levels hold < 2^31 points)
+		int i = (int)(uq - r * uh);
+		c[1] = (int)(r % t1);
+		c[2] = (int)(r / t1);
 		int par = (pass + c[1] + c[2]) & 1;
 		c[0] = 2 * i + par;            // point of the colour being updated
 		int xo = 2 * i + 1 - par;      // point of the other colour
@@ -105,9 +106,10 @@ __global__ void k_gs_materialize(double *__restrict__ phi, pinc_lvl_t Lp, int la
 	long n = (long)L.T[0] * L.T[1] * L.T[2];
 	double a = muA ? *muA : 0.0, b = *muB;
 	for (long g = (long)blockIdx.x * blockDim.x + threadIdx.x; g < n; g += (long)gridDim.x * blockDim.x) {
-		int x = (int)(g % L.T[0]);
-		long r = g / L.T[0];
-		int y = (int)(r % L.T[1]), z = (int)(r / L.T[1]);
+		const unsigned u = (unsigned)g, t0 = (unsigned)L.T[0], t1 = (unsigned)L.T[1];
+		const unsigned r = u / t0;
+		int x = (int)(u - r * t0);
+		int y = (int)(r % t1), z = (int)(r / t1);
 		if (((x + y + z) & 1) == lastPass) phi[g] = phi[g] - b;
 		else phi[g] = (phi[g] - a) - b;
 	}
@@ -137,10 +139,13 @@ __global__ void k_residual(double *__restrict__ res, const double *__restrict__ 
 	long n = (long)L.T[0] * L.T[1] * L.T[2];
 	for (long g = (long)blockIdx.x * blockDim.x + threadIdx.x; g < n; g += (long)gridDim.x * blockDim.x) {
 		int c[3];
-		c[0] = (int)(g % L.T[0]);
-		long r = g / L.T[0];
-		c[1] = (int)(r % L.T[1]);
-		c[2] = (int)(r / L.T[1]);
+		{  // 32-bit index arithmetic (levels hold < 2^31 points, checked on the host)
+			const unsigned u = (unsigned)g, t0 = (unsigned)L.T[0], t1 = (unsigned)L.T[1];
+			const unsigned r = u / t0;
+			c[0] = (int)(u - r * t0);
+			c[1] = (int)(r % t1);
+			c[2] = (int)(r / t1);
+		}
 		res[g] = residual_at<ND>(phi, rho, L, c, g);
 	}
 }
@@ -156,10 +161,13 @@ __global__ __launch_bounds__(kThreads) void k_residual_sumsq(const double *__res
 	double acc = 0.;
 	for (long g = (long)blockIdx.x * blockDim.x + threadIdx.x; g < n; g += (long)gridDim.x * blockDim.x) {
 		int c[3];
-		c[0] = (int)(g % L.T[0]);
-		long r = g / L.T[0];
-		c[1] = (int)(r % L.T[1]);
-		c[2] = (int)(r / L.T[1]);
+		{  // 32-bit index arithmetic (levels hold < 2^31 points, checked on the host)
+			const unsigned u = (unsigned)g, t0 = (unsigned)L.T[0], t1 = (unsigned)L.T[1];
+			const unsigned r = u / t0;
+			c[0] = (int)(u - r * t0);
+			c[1] = (int)(r % t1);
+			c[2] = (int)(r / t1);
+		}
 		double v = residual_at<ND>(phi, rho, L, c, g);
 		acc += v * v;
 	}
@@ -176,10 +184,13 @@ __global__ void k_restrict(const double *__restrict__ fine, double *__restrict__
 	long n = (long)C.T[0] * C.T[1] * C.T[2];
 	for (long gc = (long)blockIdx.x * blockDim.x + threadIdx.x; gc < n; gc += (long)gridDim.x * blockDim.x) {
 		int cc[3], cf[3] = {0, 0, 0};
-		cc[0] = (int)(gc % C.T[0]);
-		long r = gc / C.T[0];
-		cc[1] = (int)(r % C.T[1]);
-		cc[2] = (int)(r / C.T[1]);
+		{  // 32-bit index arithmetic (levels hold < 2^31 points, checked on the host)
+			const unsigned u = (unsigned)gc, t0 = (unsigned)C.T[0], t1 = (unsigned)C.T[1];
+			const unsigned r = u / t0;
+			cc[0] = (int)(u - r * t0);
+			cc[1] = (int)(r % t1);
+			cc[2] = (int)(r / t1);
+		}
 		long gf = 0;
 		for (int d = 0; d < ND; d++) {
 			cf[d] = 2 * cc[d];
@@ -231,10 +242,13 @@ __global__ void k_prolong_add(double *__restrict__ phiF, const double *__restric
 	long n = (long)F.T[0] * F.T[1] * F.T[2];
 	for (long g = (long)blockIdx.x * blockDim.x + threadIdx.x; g < n; g += (long)gridDim.x * blockDim.x) {
 		int cf[3];
-		cf[0] = (int)(g % F.T[0]);
-		long r = g / F.T[0];
-		cf[1] = (int)(r % F.T[1]);
-		cf[2] = (int)(r / F.T[1]);
+		{  // 32-bit index arithmetic (levels hold < 2^31 points, checked on the host)
+			const unsigned u = (unsigned)g, t0 = (unsigned)F.T[0], t1 = (unsigned)F.T[1];
+			const unsigned r = u / t0;
+			cf[0] = (int)(u - r * t0);
+			cf[1] = (int)(r % t1);
+			cf[2] = (int)(r / t1);
+		}
 		phiF[g] += prol_low<ND, 0>(phiC, C, cf);
 	}
 }
@@ -937,36 +951,63 @@ __device__ void blk_neutralize(double *a, long n, double *wred) {
 	__syncthreads();
 }
 
+// (the coarse levels hold at most 5500 points: 32-bit index arithmetic)
 __device__ __forceinline__ void blk_coords(const Lv &L, long g, int *c) {
-	c[0] = (int)(g % L.T[0]);
-	long r = g / L.T[0];
-	c[1] = (int)(r % L.T[1]);
-	c[2] = (int)(r / L.T[1]);
+	const int gi = (int)g, T0 = L.T[0], T1 = L.T[1];
+	c[0] = gi % T0;
+	const int r = gi / T0;
+	c[1] = r % T1;
+	c[2] = r / T1;
 }
 
+// one GS update of point c (linear index g) of a coarse level, the
+// expression order of mgGS3D / mgGSND
+template <int ND>
+__device__ __forceinline__ void blk_update(double *phi, const double *rho, const Lv &L, const int *c, long g,
+                                           bool gs3d) {
+	double v;
+	if (ND == 3 && gs3d) {
+		double xp = phi[g + nb_up(L, c, 0)], xm = phi[g + nb_dn(L, c, 0)];
+		double yp = phi[g + nb_up(L, c, 1)], ym = phi[g + nb_dn(L, c, 1)];
+		double zp = phi[g + nb_up(L, c, 2)], zm = phi[g + nb_dn(L, c, 2)];
+		v = (1. / 6.) * (xp + xm + yp + ym + zp + zm + rho[g]);
+	} else {
+		v = 0;
+#pragma unroll
+		for (int d = 0; d < ND; d++) v += phi[g + nb_up(L, c, d)] + phi[g + nb_dn(L, c, d)];
+		v += rho[g];
+		v *= 1. / (2 * ND);
+	}
+	phi[g] = v;
+}
+
+// red-black iterations.  Even x extent (every level of a power-of-two
+// grid): each colour pass visits only its own points (point 2i + parity of
+// row (y, z)); otherwise all points, skipping the other colour.  The
+// updates of one colour are independent: the same result either way.
 template <int ND>
 __device__ void blk_smooth(double *phi, const double *rho, const Lv &L, int nIter, bool gs3d) {
-	long n = (long)L.T[0] * L.T[1] * L.T[2];
+	const int T0 = L.T[0], T1 = L.T[1], n = T0 * T1 * L.T[2];
+	const int half = T0 >> 1, nPairs = half * T1 * L.T[2];
+	const bool even = (T0 & 1) == 0;
 	for (int it = 0; it < nIter; it++) {
 		for (int pass = 0; pass < 2; pass++) {
-			for (long g = threadIdx.x; g < n; g += blockDim.x) {
-				int c[3];
-				blk_coords(L, g, c);
-				if (((c[0] + c[1] + c[2]) & 1) != pass) continue;
-				double v;
-				if (ND == 3 && gs3d) {
-					double xp = phi[g + nb_up(L, c, 0)], xm = phi[g + nb_dn(L, c, 0)];
-					double yp = phi[g + nb_up(L, c, 1)], ym = phi[g + nb_dn(L, c, 1)];
-					double zp = phi[g + nb_up(L, c, 2)], zm = phi[g + nb_dn(L, c, 2)];
-					v = (1. / 6.) * (xp + xm + yp + ym + zp + zm + rho[g]);
-				} else {
-					v = 0;
-#pragma unroll
-					for (int d = 0; d < ND; d++) v += phi[g + nb_up(L, c, d)] + phi[g + nb_dn(L, c, d)];
-					v += rho[g];
-					v *= 1. / (2 * ND);
+			if (even) {
+				for (int q = threadIdx.x; q < nPairs; q += blockDim.x) {
+					const int r = q / half, i = q - r * half;
+					int c[3];
+					c[1] = r % T1;
+					c[2] = r / T1;
+					c[0] = 2 * i + ((pass + c[1] + c[2]) & 1);
+					blk_update<ND>(phi, rho, L, c, (long)c[0] + (long)c[1] * L.s[1] + (long)c[2] * L.s[2], gs3d);
 				}
-				phi[g] = v;
+			} else {
+				for (int g = threadIdx.x; g < n; g += blockDim.x) {
+					int c[3];
+					blk_coords(L, g, c);
+					if (((c[0] + c[1] + c[2]) & 1) != pass) continue;
+					blk_update<ND>(phi, rho, L, c, g, gs3d);
+				}
 			}
 			__syncthreads();
 		}
@@ -1095,10 +1136,13 @@ __global__ __launch_bounds__(kThreads) void k_residual_slab(double *__restrict__
 	for (long q = (long)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (long)gridDim.x * blockDim.x) {
 		const long g = (long)zlo * ps + q;
 		int c[3];
-		c[0] = (int)(g % L.T[0]);
-		long r = g / L.T[0];
-		c[1] = (int)(r % L.T[1]);
-		c[2] = (int)(r / L.T[1]);
+		{  // 32-bit index arithmetic (levels hold < 2^31 points, checked on the host)
+			const unsigned u = (unsigned)g, t0 = (unsigned)L.T[0], t1 = (unsigned)L.T[1];
+			const unsigned r = u / t0;
+			c[0] = (int)(u - r * t0);
+			c[1] = (int)(r % t1);
+			c[2] = (int)(r / t1);
+		}
 		double v = -6. * phi[g];
 		v += phi[g + nb_up(L, c, 0)] + phi[g + nb_dn(L, c, 0)] + phi[g + nb_up(L, c, 1)] + phi[g + nb_dn(L, c, 1)] +
 		     phi[g + ps] + phi[g - ps];
@@ -1122,10 +1166,13 @@ __global__ void k_restrict_slab(const double *__restrict__ fine, pinc_lvl_t Lfp,
 	const long n = (long)C.T[0] * C.T[1] * C.T[2];
 	for (long gc = (long)blockIdx.x * blockDim.x + threadIdx.x; gc < n; gc += (long)gridDim.x * blockDim.x) {
 		int cc[3];
-		cc[0] = (int)(gc % C.T[0]);
-		long r = gc / C.T[0];
-		cc[1] = (int)(r % C.T[1]);
-		cc[2] = (int)(r / C.T[1]);
+		{  // 32-bit index arithmetic (levels hold < 2^31 points, checked on the host)
+			const unsigned u = (unsigned)gc, t0 = (unsigned)C.T[0], t1 = (unsigned)C.T[1];
+			const unsigned r = u / t0;
+			cc[0] = (int)(u - r * t0);
+			cc[1] = (int)(r % t1);
+			cc[2] = (int)(r / t1);
+		}
 		int cf[3] = {2 * cc[0], 2 * cc[1], zf0 + 2 * cc[2]};
 		const long gf = (long)cf[0] + (long)cf[1] * F.s[1] + (long)cf[2] * ps;
 		double v;
@@ -1166,6 +1213,7 @@ __global__ void k_prolong_add_slab(double *__restrict__ phiX, pinc_lvl_t Lxp, in
 
 extern "C" int pinc_hip_gs_pass(double *phi, const double *rho, pinc_lvl_t L, int pass, int nd3,
                                 const double *muPrev, double *partial, int *nBlocks, void *stream) {
+	if (npts(L) >= (1L << 31)) return set_error(hipErrorInvalidValue, "gs_pass: level too large for 32-bit indexing");
 	long nPairs = npts(L) / 2;
 	unsigned nb = blocks_for(nPairs);
 	*nBlocks = (int)nb;
@@ -1183,6 +1231,7 @@ extern "C" int pinc_hip_gs_pass(double *phi, const double *rho, pinc_lvl_t L, in
 
 extern "C" int pinc_hip_gs_materialize(double *phi, pinc_lvl_t L, int lastPass, const double *muA,
                                        const double *muB, void *stream) {
+	if (npts(L) >= (1L << 31)) return set_error(hipErrorInvalidValue, "gs_materialize: level too large for 32-bit indexing");
 	hipLaunchKernelGGL(k_gs_materialize, dim3(blocks_for(npts(L))), dim3(kThreads), 0,
 	                   (hipStream_t)stream, phi, L, lastPass, muA, muB);
 	return check_launch("gs_materialize");
@@ -1190,6 +1239,7 @@ extern "C" int pinc_hip_gs_materialize(double *phi, pinc_lvl_t L, int lastPass, 
 
 extern "C" int pinc_hip_residual(double *res, const double *phi, const double *rho, pinc_lvl_t L,
                                  void *stream) {
+	if (npts(L) >= (1L << 31)) return set_error(hipErrorInvalidValue, "residual: level too large for 32-bit indexing");
 	hipStream_t st = (hipStream_t)stream;
 	unsigned nb = blocks_for(npts(L));
 	if (L.nd == 3) hipLaunchKernelGGL(k_residual<3>, dim3(nb), dim3(kThreads), 0, st, res, phi, rho, L);
@@ -1200,6 +1250,7 @@ extern "C" int pinc_hip_residual(double *res, const double *phi, const double *r
 
 extern "C" int pinc_hip_residual_sumsq(const double *phi, const double *rho, pinc_lvl_t L,
                                        double *partial, int *nBlocks, void *stream) {
+	if (npts(L) >= (1L << 31)) return set_error(hipErrorInvalidValue, "residual_sumsq: level too large for 32-bit indexing");
 	hipStream_t st = (hipStream_t)stream;
 	unsigned nb = blocks_for(npts(L));
 	*nBlocks = (int)nb;
@@ -1210,6 +1261,7 @@ extern "C" int pinc_hip_residual_sumsq(const double *phi, const double *rho, pin
 }
 
 extern "C" int pinc_hip_restrict(const double *fine, double *coarse, pinc_lvl_t Lc, int nd3, void *stream) {
+	if (npts(Lc) >= (1L << 31)) return set_error(hipErrorInvalidValue, "restrict: level too large for 32-bit indexing");
 	hipStream_t st = (hipStream_t)stream;
 	unsigned nb = blocks_for(npts(Lc));
 	if (Lc.nd == 3 && nd3) hipLaunchKernelGGL((k_restrict<3, true>), dim3(nb), dim3(kThreads), 0, st, fine, coarse, Lc);
@@ -1220,6 +1272,7 @@ extern "C" int pinc_hip_restrict(const double *fine, double *coarse, pinc_lvl_t 
 }
 
 extern "C" int pinc_hip_prolong_add(double *phiF, const double *phiC, pinc_lvl_t Lf, void *stream) {
+	if (npts(Lf) >= (1L << 31)) return set_error(hipErrorInvalidValue, "prolong_add: level too large for 32-bit indexing");
 	hipStream_t st = (hipStream_t)stream;
 	unsigned nb = blocks_for(npts(Lf));
 	if (Lf.nd == 3) hipLaunchKernelGGL(k_prolong_add<3>, dim3(nb), dim3(kThreads), 0, st, phiF, phiC, Lf);
@@ -1311,6 +1364,7 @@ extern "C" int pinc_hip_mg_coarse(const double *rho, double *phi, int nLevels, c
 
 extern "C" int pinc_hip_residual_slab(double *res, const double *phi, const double *rho, pinc_lvl_t Lx, int zlo,
                                       int zhi, void *stream) {
+	if (npts(Lx) >= (1L << 31)) return set_error(hipErrorInvalidValue, "residual_slab: level too large for 32-bit indexing");
 	if (Lx.nd != 3 || zlo < 1 || zhi > Lx.T[2] - 1 || zhi <= zlo)
 		return set_error(hipErrorInvalidValue, "residual_slab: planes must have both z neighbours in the slab");
 	long n = (long)Lx.T[0] * Lx.T[1] * (zhi - zlo);
@@ -1321,6 +1375,7 @@ extern "C" int pinc_hip_residual_slab(double *res, const double *phi, const doub
 
 extern "C" int pinc_hip_residual_sumsq_slab(const double *phi, const double *rho, pinc_lvl_t Lx, int zlo, int zhi,
                                             double *partial, int *nBlocks, void *stream) {
+	if (npts(Lx) >= (1L << 31)) return set_error(hipErrorInvalidValue, "residual_sumsq_slab: level too large for 32-bit indexing");
 	if (Lx.nd != 3 || zlo < 1 || zhi > Lx.T[2] - 1 || zhi <= zlo)
 		return set_error(hipErrorInvalidValue, "residual_sumsq_slab: planes must have both z neighbours in the slab");
 	long n = (long)Lx.T[0] * Lx.T[1] * (zhi - zlo);
@@ -1333,6 +1388,7 @@ extern "C" int pinc_hip_residual_sumsq_slab(const double *phi, const double *rho
 
 extern "C" int pinc_hip_restrict_slab(const double *fineX, pinc_lvl_t Lx, int zf0, double *coarse, pinc_lvl_t Lc,
                                       int nd3, void *stream) {
+	if (npts(Lc) >= (1L << 31)) return set_error(hipErrorInvalidValue, "restrict_slab: level too large for 32-bit indexing");
 	if (Lx.nd != 3 || Lc.nd != 3 || 2 * Lc.T[0] != Lx.T[0] || 2 * Lc.T[1] != Lx.T[1] || zf0 < 1 ||
 	    zf0 + 2 * Lc.T[2] > Lx.T[2])
 		return set_error(hipErrorInvalidValue, "restrict_slab: geometry");
