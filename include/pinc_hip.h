@@ -131,6 +131,8 @@ typedef struct {
 	int *perm;
 	unsigned long long *moved; /* if set: += particles that stay and changed cell */
 	unsigned long long *tstamp; /* if set: 8 phase timestamps per block (diagnostics) */
+	unsigned long long *diag;   /* if set: [0] += items of a sorting push given a global slot one by
+	                             * one (outside its LDS boxes; diagnostics) */
 	/* immersed objects (fused collection, oCollectObjectCharge's test at
 	 * object.c:489-494 on the moved position): if objInside is set, a
 	 * particle that stays and whose cell's lower node has an object id > 0

@@ -905,6 +905,10 @@ struct TileGeo {
 	int nt[3];      // tiles per dimension (cell index (int)p is in [0, T+1])
 	long ts[3];     // tile index stride per dimension
 	int cmax[3];    // largest admissible cell index
+	// bricks of the push's sort: tw^(nd-1) consecutive cell keys of a tile
+	// (tw x tw x 1 in 3-D), bs[d] = log2 of the brick's extent along d (all
+	// 0: bricks of one cell)
+	int bs[3];
 };
 
 // sort key: tile index (tiles in x-fastest order) then the cell inside the
@@ -1226,6 +1230,7 @@ struct PushArgs {
 	int *perm;           // perm[i] = destination of particle i
 	unsigned long long *moved;  // += particles that stay but changed cell (nullable)
 	unsigned long long *tstamp;  // 8 phase timestamps per block (diagnostics, nullable)
+	unsigned long long *diag;    // [0] += sorting-push items given a global slot one by one (nullable)
 	const unsigned char *objIn;  // object ids of the padded nodes (nullable: no objects)
 	long objSy, objSz, objN;
 	int *objCount;
@@ -1503,6 +1508,105 @@ __device__ __forceinline__ int tile_key_cells(const TileGeo &tg, const int *cin)
 	return (int)(tile * cs + cell);
 }
 
+// Bricks (TileGeo::bs) of a cell box: brick coordinates = clamped cell >> bs.
+// A brick's cells have consecutive keys, so the sorting push reserves one
+// range per brick and block from the cursor of the brick's first cell (the
+// counts and the scan stay per cell; the other cells' cursors go unused).
+struct BrickBox {
+	int lo[3], n[3];
+	int vol;
+};
+template <int ND>
+__device__ __forceinline__ int clamp_cell(const TileGeo &tg, int d, int c) {
+	return c < 0 ? 0 : (c > tg.cmax[d] ? tg.cmax[d] : c);
+}
+// brick box of a cell box (at most as many entries as the cell box)
+template <int ND>
+__device__ __forceinline__ BrickBox make_brick_box(const TileGeo &tg, const Box &b) {
+	BrickBox r;
+	r.vol = b.vol > 0 ? 1 : 0;
+#pragma unroll
+	for (int d = 0; d < 3; d++) {
+		r.lo[d] = d < ND ? clamp_cell<ND>(tg, d, b.lo[d]) >> tg.bs[d] : 0;
+		r.n[d] = d < ND ? (clamp_cell<ND>(tg, d, b.lo[d] + b.n[d] - 1) >> tg.bs[d]) - r.lo[d] + 1 : 1;
+		r.vol *= r.n[d];
+	}
+	return r;
+}
+// Brick box of the cells within `reach` of the block's mean cell (clipped to
+// its extent clo..chi), trimmed to at most cap bricks -- the widest dimension
+// first, from its side farther from the mean -- but never inside `core`.
+template <int ND>
+__device__ __forceinline__ BrickBox wide_brick_box(const TileGeo &tg, const int *clo, const int *chi, const int *mid,
+                                                   int reach, int cap, const BrickBox &core) {
+	int lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0}, m[3] = {0, 0, 0}, flo[3] = {0, 0, 0}, fhi[3] = {0, 0, 0};
+#pragma unroll
+	for (int d = 0; d < ND; d++) {
+		int l = max(clo[d], mid[d] - reach), h = min(chi[d], mid[d] + reach);
+		if (l > h) l = h = mid[d];
+		m[d] = clamp_cell<ND>(tg, d, mid[d]) >> tg.bs[d];
+		flo[d] = core.vol ? core.lo[d] : m[d];
+		fhi[d] = core.vol ? core.lo[d] + core.n[d] - 1 : m[d];
+		lo[d] = min(clamp_cell<ND>(tg, d, l) >> tg.bs[d], flo[d]);
+		hi[d] = max(clamp_cell<ND>(tg, d, h) >> tg.bs[d], fhi[d]);
+	}
+	int v = 0;
+#pragma unroll 1
+	for (int it = 0; it < 128; it++) {
+		v = 1;
+		for (int d = 0; d < ND; d++) v *= hi[d] - lo[d] + 1;
+		if (v <= cap) break;
+		int w = -1;
+		for (int d = 0; d < ND; d++)
+			if ((lo[d] < flo[d] || hi[d] > fhi[d]) && (w < 0 || hi[d] - lo[d] > hi[w] - lo[w])) w = d;
+		if (w < 0) break;
+		if (hi[w] > fhi[w] && (lo[w] >= flo[w] || hi[w] - m[w] >= m[w] - lo[w])) hi[w]--;
+		else lo[w]++;
+	}
+	// block-uniform: scalar registers
+	BrickBox b;
+#pragma unroll
+	for (int d = 0; d < 3; d++) {
+		b.lo[d] = __builtin_amdgcn_readfirstlane(lo[d]);
+		b.n[d] = __builtin_amdgcn_readfirstlane(hi[d] - lo[d] + 1);
+	}
+	b.vol = __builtin_amdgcn_readfirstlane(v <= cap ? v : 0);
+	return b;
+}
+// index in the brick box of the brick holding cell c, or -1 outside it
+template <int ND>
+__device__ __forceinline__ int brick_inside(const TileGeo &tg, const BrickBox &bb, const int *c) {
+	int l = 0, s = 1;
+	bool in = bb.vol > 0;
+#pragma unroll
+	for (int d = 0; d < ND; d++) {
+		const int r = (clamp_cell<ND>(tg, d, c[d]) >> tg.bs[d]) - bb.lo[d];
+		in &= (unsigned)r < (unsigned)bb.n[d];
+		l += mul24(r, s);
+		s *= bb.n[d];
+	}
+	return in ? l : -1;
+}
+// key of the first cell of the brick holding cell c
+template <int ND>
+__device__ __forceinline__ int brick_first_key(const TileGeo &tg, const int *c) {
+	int f[3] = {0, 0, 0};
+#pragma unroll
+	for (int d = 0; d < ND; d++) f[d] = (clamp_cell<ND>(tg, d, c[d]) >> tg.bs[d]) << tg.bs[d];
+	return tile_key_cells<ND>(tg, f);
+}
+// key of the first cell of brick l of a brick box
+template <int ND>
+__device__ __forceinline__ int brick_key(const TileGeo &tg, const BrickBox &bb, int l) {
+	int c[3] = {0, 0, 0};
+#pragma unroll
+	for (int d = 0; d < ND; d++) {
+		c[d] = (bb.lo[d] + l % bb.n[d]) << tg.bs[d];
+		l /= bb.n[d];
+	}
+	return tile_key_cells<ND>(tg, c);
+}
+
 typedef double dvec2 __attribute__((ext_vector_type(2)));
 
 // OBJ: the object test of the fused collection (separate instances, so the
@@ -1649,6 +1753,16 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	const Box rB = !empty ? make_box(clo, chi, cmid, 1, 2, ND, kRhoBoxCap) : Box{{0, 0, 0}, {1, 1, 1}, 0};
 	const Box iB = (SORT && !empty) ? make_box(clo, chi, cmid, 0, 0, ND, kInCellCap) : Box{{0, 0, 0}, {1, 1, 1}, 0};
 	const Box oB = (a.cntNext && !empty) ? make_box(clo, chi, cmid, 1, 1, ND, kOutCellCap) : Box{{0, 0, 0}, {1, 1, 1}, 0};
+	// sorting push: the items of the cell box iB are ranked by cell, the
+	// others inside the wide brick box ib by brick (one run of each brick per
+	// block, the brick's own items first); only items outside both take a
+	// global slot one by one.  The brick counters live in cntOut, which a
+	// sorting push does not use (it never counts).
+	const BrickBox ib = (SORT && !empty)
+	                        ? wide_brick_box<ND>(a.tg, clo, chi, cmid, 8, kInCellCap, make_brick_box<ND>(a.tg, iB))
+	                        : BrickBox{{0, 0, 0}, {1, 1, 1}, 0};
+	static_assert(kOutCellCap >= 2 * kInCellCap, "brick counters in cntOut");
+	int *const bCnt = cntOut, *const bBase = cntOut + kInCellCap;
 
 	PUSH_TS(1);
 	// ---- phase B: LDS setup (zero the accumulators, stage E)
@@ -1661,7 +1775,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	for (int t = threadIdx.x; t < (PINC_PUSH_COPIES ? nCopy * rStride : rB.vol); t += kPushThreads) rhoL[t] = 0.0;
 	if (SORT)
 		for (int t = threadIdx.x; t < iB.vol; t += kPushThreads) cntIn[t] = 0;
-	for (int t = threadIdx.x; t < oB.vol; t += kPushThreads) cntOut[t] = 0;
+	for (int t = threadIdx.x; t < (SORT ? kInCellCap : oB.vol); t += kPushThreads) cntOut[t] = 0;
 	if (KICK && !(PINC_PUSH_SKIP & 2)) {
 		for (int t = threadIdx.x; t < eB.vol; t += kPushThreads) {
 			int c[3] = {0, 0, 0};
@@ -1686,43 +1800,69 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	// LDS (the sort push is tight on VGPRs): rank in its cell << 8 | box cell,
 	// or ~global slot for an item outside the box.
 	if (SORT) {
-		static_assert(kInCellCap <= 256 && kPushChunk <= (1 << 23), "rank/cell packing");
+		static_assert(kInCellCap <= 256 && kPushChunk <= (1 << 22), "rank/cell packing");
+		// per item: rank << 9 | cell of iB, rank << 9 | 256 | brick of ib, or
+		// ~global slot (outside both: wave-aggregated)
+		int rl[kPushItems];
 #pragma unroll
 		for (int k = 0; k < kPushItems; k++) {
-			int lc = -1;
+			int lc = -1, lb = -1;
 			int c[3] = {0, 0, 0};
 #pragma unroll
 			for (int d = 0; d < ND; d++) c[d] = (int)p[k][d];
 			const bool ok = (valid >> k) & 1u;
 			if (ok && iB.inside(c, ND)) lc = iB.index(c, ND);
+			else if (ok) lb = brick_inside<ND>(a.tg, ib, c);
 			const int rank = lds_agg_add<true>(cntIn, lc < 0 ? 0 : lc, lc >= 0);
-			// outside the box: its global slot right away (wave-aggregated), as ~slot
-			const bool out = ok && lc < 0;
-			const int g = agg_add(a.cursor, out ? tile_key_cells<ND>(a.tg, c) : 0, out);
-			rlL[k * kPushThreads + threadIdx.x] = lc >= 0 ? (rank << 8 | lc) : ~g;
+			const int rankB = lds_agg_add<true>(bCnt, lb < 0 ? 0 : lb, lb >= 0);
+			const bool out = ok && lc < 0 && lb < 0;
+			const int g = agg_add(a.cursor, out ? brick_first_key<ND>(a.tg, c) : 0, out);
+			rl[k] = lc >= 0 ? (rank << 9 | lc) : lb >= 0 ? (rankB << 9 | 256 | lb) : (ok ? ~g : -1);
+		}
+#pragma unroll
+		for (int k = 0; k < kPushItems; k++) rlL[k * kPushThreads + threadIdx.x] = rl[k];
+		if (a.diag) {
+			int no = 0;
+#pragma unroll
+			for (int k = 0; k < kPushItems; k++) no += rl[k] < 0 && ((valid >> k) & 1u);
+			no = wave_sum(no);
+			if (lane == 0 && no) atomicAdd(&a.diag[0], (unsigned long long)no);
 		}
 		__syncthreads();
 		static_assert(kInCellCap <= kPushThreads, "one reservation per thread");
-		int m = 0;
+		// one global reservation per brick of ib: each cell of iB takes its
+		// place inside its brick's block run (LDS atomic, after the brick's
+		// own items), each brick one range of its first cell's cursor
+		int m = 0, lb = 0, bo = 0;
 		if ((int)threadIdx.x < iB.vol) {
 			m = cntIn[threadIdx.x];
 			if (m) {
 				int c[3] = {0, 0, 0};
 				iB.coords(threadIdx.x, c, ND);
-				cntIn[threadIdx.x] = atomicAdd(&a.cursor[tile_key_cells<ND>(a.tg, c)], m);
+				lb = brick_inside<ND>(a.tg, ib, c);  // (ib contains iB's bricks)
+				bo = atomicAdd(&bCnt[lb], m);
 			}
 		}
-		// block slot of each cell's run: exclusive scan of the counts
-		const int inc = wave_incl_scan(m);
+		__syncthreads();
+		const int bm = (int)threadIdx.x < ib.vol ? bCnt[threadIdx.x] : 0;
+		if (bm) bBase[threadIdx.x] = atomicAdd(&a.cursor[brick_key<ND>(a.tg, ib, threadIdx.x)], bm);
+		// block slot of each brick's run: exclusive scan of the brick counts
+		const int inc = wave_incl_scan(bm);
 		if (lane == 63) red[wv] = inc;
 		__syncthreads();
 		int off = 0;
 		for (int w = 0; w < wv; w++) off += red[w];
-		if ((int)threadIdx.x < iB.vol) locStart[threadIdx.x] = off + inc - m;
+		if ((int)threadIdx.x < ib.vol) bCnt[threadIdx.x] = off + inc - bm;
 		if (threadIdx.x == 0) {
 			int t = 0;
 			for (int w = 0; w < NW; w++) t += red[w];
-			cbox[0] = t;  // items in the box (the box bounds are in registers by now)
+			cbox[0] = t;  // items in the boxes (the box bounds are in registers by now)
+		}
+		__syncthreads();
+		// each cell of iB: global start and block slot of its run
+		if (m) {
+			cntIn[threadIdx.x] = bBase[lb] + bo;
+			locStart[threadIdx.x] = bCnt[lb] + bo;
 		}
 		__syncthreads();
 	}
@@ -1873,8 +2013,8 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 		if (SORT) {
 			// flag staged by block slot (outside the box: by item position)
 			const int r = rlL[k * kPushThreads + threadIdx.x];
-			const int t = r >= 0 ? locStart[r & 255] + (r >> 8)
-			                         : kPushChunk + k * kPushThreads + (int)threadIdx.x;
+			const int t = r >= 0 ? ((r & 256) ? bCnt[r & 255] : locStart[r & 255]) + (r >> 9)
+			                     : kPushChunk + k * kPushThreads + (int)threadIdx.x;
 			stageF[t] = (unsigned char)ne;
 		}
 		if (!SORT) a.flags[i] = (unsigned char)ne;
@@ -1925,9 +2065,10 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 				const long i = item(k);
 				const int r = rlL[k * kPushThreads + threadIdx.x];
 				if (r >= 0) {
-					const int lc = r & 255, rank = r >> 8;
-					slot[k] = locStart[lc] + rank;
-					const int o = cntIn[lc] + rank;
+					const int l = r & 255, rank = r >> 9;
+					const bool br = r & 256;
+					slot[k] = (br ? bCnt[l] : locStart[l]) + rank;
+					const int o = (br ? bBase[l] : cntIn[l]) + rank;
 					gdst[slot[k]] = o;
 					a.perm[i] = o;
 				} else {
@@ -2447,15 +2588,31 @@ extern "C" int pinc_hip_init_species(pinc_pop_t pop, int s, pinc_geom_t g, long 
 	return check_launch("init_species");
 }
 
+// PINC_SORT_BRICK: the sorting push reserves its output per brick of
+// tw^(nd-1) cells (tw x tw x 1 in 3-D, one block's worth at C4's 64 ppc)
+// instead of per cell: a few tens of runs per block instead of about a
+// hundred short scattered ones once the input order has decayed; inside a
+// brick run the block's particles stay grouped by cell.  (Tried: bricks
+// ordered along the slab dimension fastest, so that consecutive bricks are
+// neighbours -- the plain pushes got slower, 25 -> 31 ms per ion launch at
+// C4: the concurrently running blocks then touch scattered grid rows.)
+#ifndef PINC_SORT_BRICK
+#define PINC_SORT_BRICK 1
+#endif
+
 static TileGeo make_tile_geo(pinc_geom_t g, int tileWidth, long *nKeys) {
 	TileGeo tg;
 	long nt = 1, cpt = 1;
 	tg.tw = tileWidth;
+	int lw = 0;
+	while ((1 << lw) < tileWidth) lw++;
+	const bool brick = PINC_SORT_BRICK && (1 << lw) == tileWidth;
 	for (int d = 0; d < 3; d++) {
 		int T = d < g.nd ? (d == g.nd - 1 ? g.nloc : g.T[d]) : 1;
 		tg.cmax[d] = T + 1;
 		tg.nt[d] = d < g.nd ? (T + 1) / tileWidth + 1 : 1;
 		tg.ts[d] = nt;
+		tg.bs[d] = brick && d < g.nd - 1 ? lw : 0;
 		nt *= tg.nt[d];
 		if (d < g.nd) cpt *= tileWidth;
 	}
@@ -2570,6 +2727,7 @@ extern "C" int pinc_hip_push(pinc_pop_t pop, int s, pinc_geom_t g, const pinc_pu
 	a.perm = args->perm;
 	a.moved = args->moved;
 	a.tstamp = args->tstamp;
+	a.diag = args->diag;
 	a.objIn = args->objInside;
 	a.objSy = args->objSy;
 	a.objSz = args->objSz;

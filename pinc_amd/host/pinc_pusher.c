@@ -229,9 +229,12 @@ static void ensure_keys(Population *pop) {
 
 /* PINC_TRACE_SORT=2: mean per-block time of each push phase (s_memrealtime,
  * 100 MHz) and the kernel's span */
-static void push_phase_report(const unsigned long long *dts, int nb, int s, int sort, int count) {
+static void push_phase_report(const unsigned long long *dts, const unsigned long long *ddiag, int nb, int s, int sort,
+                              int count) {
 	unsigned long long *t = malloc((size_t)nb * 8 * sizeof(*t));
+	unsigned long long dg[1];
 	pinc_check(pinc_hip_d2h(t, dts, (size_t)nb * 8 * sizeof(*t), g_pinc.stream), "push timestamps");
+	pinc_check(pinc_hip_d2h(dg, ddiag, sizeof(dg), g_pinc.stream), "push diagnostics");
 	double ph[7] = {0};
 	unsigned long long t0 = ~0ull, t1 = 0;
 	for (int b = 0; b < nb; b++) {
@@ -240,9 +243,10 @@ static void push_phase_report(const unsigned long long *dts, int nb, int s, int 
 		if (t[b * 8 + 7] > t1) t1 = t[b * 8 + 7];
 	}
 	fprintf(stderr, "[pinc] push species %d%s%s: span %.2f ms, per block us: load+box %.2f, lds %.2f, rank %.2f, "
-	        "kick/drift %.2f, sorted stores %.2f, count %.2f, deposit %.2f\n", s, sort ? " sort" : "",
+	        "kick/drift %.2f, sorted stores %.2f, count %.2f, deposit %.2f; global slots %.3g per block\n", s,
+	        sort ? " sort" : "",
 	        count ? " count" : "", (t1 - t0) * 1e-5, ph[0] / nb * 1e-2, ph[1] / nb * 1e-2, ph[2] / nb * 1e-2,
-	        ph[3] / nb * 1e-2, ph[4] / nb * 1e-2, ph[5] / nb * 1e-2, ph[6] / nb * 1e-2);
+	        ph[3] / nb * 1e-2, ph[4] / nb * 1e-2, ph[5] / nb * 1e-2, ph[6] / nb * 1e-2, (double)dg[0] / nb);
 	free(t);
 }
 
@@ -360,13 +364,15 @@ static int push_all(Population *pop, Grid *E, double *const *xout) {
 		int nb = 0;
 		unsigned long long *ts = NULL;
 		if (g_pinc.traceSort > 1) {
-			pinc_check(pinc_hip_malloc((void **)&ts, (np / 1024 + 1) * 8 * sizeof(*ts)), "push timestamps");
+			pinc_check(pinc_hip_malloc((void **)&ts, ((np / 1024 + 1) * 8 + 2) * sizeof(*ts)), "push timestamps");
+			pinc_check(pinc_hip_memset(ts + (np / 1024 + 1) * 8, 0, sizeof(*ts), g_pinc.stream), "push diagnostics");
 			a.tstamp = ts;
+			a.diag = ts + (np / 1024 + 1) * 8;
 		}
 		int slot = E ? pinc_probe_begin(PINC_PROBE_PUSH) : -1;
 		pinc_check(pinc_hip_push(p, s, g, &a, &nb, g_pinc.stream), "push");
 		if (ts) {
-			push_phase_report(ts, nb, s, sortS[s], countNext);
+			push_phase_report(ts, a.diag, nb, s, sortS[s], countNext);
 			pinc_hip_free(ts);
 		}
 		/* pos R+W, vel R+W (32 B per dim per particle) + E R (8 B per value
