@@ -149,6 +149,9 @@ def main() -> int:
                          "c2: input/langmuir2D.ini at 128^2, 32 ppc (Langmuir perturbation, cold), multigrid")
     ap.add_argument("--size", type=int, default=None, help="global cells per dimension (c4: 256, c3: 128)")
     ap.add_argument("--ppc", type=int, default=None, help="particles per cell per species (c4: 64, c3: 32)")
+    ap.add_argument("--mg-extrapolate", type=int, default=1,
+                    help="1: native multigrid starts each solve from 2 phi_n - phi_(n-1) instead of phi_n "
+                         "(multigrid:extrapolate; objects keep the plain warm start)")
     ap.add_argument("--mg", default="native", choices=["native", "reference"],
                     help="native: correction-scheme V-cycle with the coarse h^2 factor (default; the reference "
                          "algorithm does not converge at 256^3 with 5 levels, DESIGN.md section 6); reference: "
@@ -248,6 +251,7 @@ def main() -> int:
     if args.mg == "native":
         cfg["multigrid"]["native"] = "1"
         cfg["multigrid"]["shard"] = args.mg_shard
+        cfg["multigrid"]["extrapolate"] = str(args.mg_extrapolate)
     if c5:
         # a generated sphere (the reference's bepiColombo object file is not
         # available): centre of the grid, radius S/32
@@ -382,7 +386,9 @@ def main() -> int:
             "poisson": ("spectral (sSolver, rocFFT r2c/c2r, global grid)" if c3 else
                         f"multigrid mgVRecursive, {mg_levels} levels ({S}^{nd} down to {S >> (mg_levels - 1)}^{nd}), "
                         "RB Gauss-Seidel 10/10/10, "
-                        + ("native mode (correction scheme, coarse h^2 factor; the ini's 5 levels extended)"
+                        + ("native mode (correction scheme, coarse h^2 factor; the ini's 5 levels extended"
+                           + ("; initial guess 2 phi_n - phi_(n-1)" if args.mg_extrapolate and not c5 else "")
+                           + "; RMS residual <= 1e-10 as the reference)"
                            if args.mg == "native" else "reference algorithm (parity mode)")
                         + (f", level 0 sharded over the slabs ({mg_halo} halo planes per side), levels >= 1 "
                            "all-gathered" if mg_halo else (", replicated on every rank" if world > 1 else ""))),

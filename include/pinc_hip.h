@@ -366,6 +366,11 @@ int pinc_hip_gs_materialize(double *phi, pinc_lvl_t L, int lastPass, const doubl
                             const double *muB, void *stream);
 /* phi -= *mu over all points */
 int pinc_hip_sub_dev(double *a, long n, const double *mu, void *stream);
+/* multigrid:extrapolate (native mode, an extension): phi <- 2 phi - prev and
+ * prev <- old phi over n values, the initial guess of the next solve from the
+ * last two solutions (mgSolveRaw, multigrid.c:1688-1724, warm-starts from the
+ * last one) */
+int pinc_hip_extrapolate(double *phi, double *prev, long n, void *stream);
 /* mgResidual (multigrid.c:1385-1403): res = lap(phi) + rho */
 int pinc_hip_residual(double *res, const double *phi, const double *rho, pinc_lvl_t L,
                       void *stream);

@@ -197,6 +197,7 @@ void ow_spectral_solve(OWorld *w);
  * reference's algorithm): correction scheme with the coarse h^2 factor */
 ONative *on_alloc(int nd, const int *Tglobal, int nLevelsIni, int nd3);
 void on_free(ONative *S);
+void on_set_extrapolate(ONative *S, int on);
 int on_levels(const ONative *S);
 void ow_native_solve(OWorld *w);
 /* single-grid stencil primitives (exported for unit tests) */

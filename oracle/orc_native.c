@@ -38,6 +38,10 @@ struct ONative {
 	NLv L[ON_MAX_LEVELS];
 	double *rho[ON_MAX_LEVELS], *phi[ON_MAX_LEVELS], *res[ON_MAX_LEVELS];
 	int nd3;        /* 3-D GS / restriction forms (gaussSeidelRB, halfWeight) */
+	/* multigrid:extrapolate (pinc_mg.c): initial guess 2 phi_n - phi_{n-1}
+	 * once two solutions exist; prev holds phi_{n-1}, nSeen counts solves */
+	int extrap, nSeen;
+	double *prev;
 };
 
 static NLv mklv(int nd, const int *T){
@@ -71,8 +75,14 @@ ONative *on_alloc(int nd, const int *Tg, int nLevelsIni, int nd3){
 	return S;
 }
 
+void on_set_extrapolate(ONative *S, int on){
+	S->extrap = on;
+	if(on && !S->prev) S->prev = calloc(S->L[0].N, sizeof(double));
+}
+
 void on_free(ONative *S){
 	if(!S) return;
+	free(S->prev);
 	for(int q = 0; q < S->nLevels; q++){ free(S->rho[q]); free(S->phi[q]); free(S->res[q]); }
 	free(S);
 }
@@ -261,6 +271,13 @@ void ow_native_solve(OWorld *w){
 	ONative *S = w->native;
 	gather_scatter(w, S->rho[0], S->phi[0], 0);
 	long N = S->L[0].N;
+	if(S->extrap){
+		/* phi holds the last solution (the device's pinc_hip_extrapolate) */
+		if(S->nSeen >= 2){
+			for(long g = 0; g < N; g++){ double p = S->phi[0][g]; S->phi[0][g] = 2.0*p - S->prev[g]; S->prev[g] = p; }
+		} else if(S->nSeen == 1) memcpy(S->prev, S->phi[0], N*sizeof(double));
+		if(S->nSeen < 2) S->nSeen++;
+	}
 	double barRes = 2.;
 	long c = 0;
 	w->mgHistN = 0;

@@ -45,6 +45,16 @@ __global__ void k_sub_dev(double *a, long n, const double *mu) {
 		a[i] = a[i] - m;
 }
 
+// linear extrapolation in time: phi <- 2 phi - prev, prev <- phi (the
+// multigrid's initial guess from the last two solutions)
+__global__ void k_extrapolate(double *__restrict__ phi, double *__restrict__ prev, long n) {
+	for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+		const double p = phi[i];
+		phi[i] = 2.0 * p - prev[i];
+		prev[i] = p;
+	}
+}
+
 // plane p of a slab: plane size = product of the non-slab extents
 __global__ void k_add_plane(double *dst, const double *src, long planeSize) {
 	for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < planeSize; i += (long)gridDim.x * blockDim.x)
@@ -159,6 +169,12 @@ extern "C" int pinc_hip_sub_dev(double *a, long n, const double *mu, void *strea
 	if (n <= 0) return 0;
 	hipLaunchKernelGGL(k_sub_dev, dim3(grid_for(n)), dim3(kThreads), 0, (hipStream_t)stream, a, n, mu);
 	return check_launch("sub_dev");
+}
+
+extern "C" int pinc_hip_extrapolate(double *phi, double *prev, long n, void *stream) {
+	if (n <= 0) return 0;
+	hipLaunchKernelGGL(k_extrapolate, dim3(grid_for(n)), dim3(kThreads), 0, (hipStream_t)stream, phi, prev, n);
+	return check_launch("extrapolate");
 }
 
 static long plane_size(const pinc_geom_t &g) {

@@ -169,6 +169,10 @@ struct MultigridSolver {
 	double *hist;
 	long histCap, histN, maxCycles;
 	long fusedMin;     /* smallest level (points) smoothed by the fused sweeps */
+	/* multigrid:extrapolate: level-0 initial guess 2 phi_n - phi_{n-1} (prev
+	 * holds phi_{n-1}; havePrev counts the solves seen, up to 2) */
+	int extrap, havePrev;
+	double *phiPrev;
 	/* sharded level 0 (native mode, multigrid:shard):
 	 * rho[0]/phi[0]/res[0] are this rank's z-slab with hz halo planes on
 	 * each side (L[0], N[0] = that extended slab), levels >= 1 global */

@@ -137,6 +137,13 @@ MultigridSolver *mgAllocSolver(const dictionary *ini, Grid *rho, Grid *phi) {
 	 * C4, the gaps between dependent kernels are GPU-side) */
 	S->useGraph = S->native && iniHas(ini, "multigrid:graph") && iniGetInt(ini, "multigrid:graph");
 	S->cycleGraph = NULL;
+	/* initial guess extrapolated from the last two solutions (native mode,
+	 * opt-in; objects solve twice per step and for the capacitance matrix,
+	 * so they keep the plain warm start) */
+	S->extrap = S->native && iniHas(ini, "multigrid:extrapolate") && iniGetInt(ini, "multigrid:extrapolate") &&
+	            !iniHas(ini, "objects:sphere") && !iniHas(ini, "objects:file");
+	S->havePrev = 0;
+	S->phiPrev = NULL;
 	/* native mode: levels of at least fusedMin points smooth with the
 	 * z-marching fused sweeps (two iterations per launch), smaller ones
 	 * colour by colour (PINC_MG_FUSED_MIN overrides, experiments) */
@@ -194,6 +201,7 @@ MultigridSolver *mgAllocSolver(const dictionary *ini, Grid *rho, Grid *phi) {
 		pinc_check(pinc_hip_malloc((void **)&S->res[q], S->N[q] * sizeof(double)), "mg level");
 	}
 	if (S->shard) phi->dev->ext = S->phi[0];
+	if (S->extrap) pinc_check(pinc_hip_malloc((void **)&S->phiPrev, S->N[0] * sizeof(double)), "mg extrapolation");
 	S->rhoGrid = rho;
 	S->phiGrid = phi;
 	return S;
@@ -202,6 +210,7 @@ MultigridSolver *mgAllocSolver(const dictionary *ini, Grid *rho, Grid *phi) {
 void mgFreeSolver(MultigridSolver *S) {
 	if (!S) return;
 	pinc_hip_graph_destroy(S->cycleGraph);
+	pinc_hip_free(S->phiPrev);
 	free(S->hist);
 	for (int q = 0; q < S->nLevels; q++) {
 		if (q > 0 || S->shard) {
@@ -430,6 +439,16 @@ void mgSolve(MultigridSolver *S, Grid *rho, Grid *phi, const MpiInfo *mpiInfo) {
 	} else if (g_pinc.nranks > 1) {
 		long ps = rho->dev->planeSize;
 		pinc_comm_allgather(rho->dev->d + ps, rho->dev->global, ps * rho->dev->geom.nloc, "gather rho");
+	}
+	if (S->extrap) {
+		/* phi[0] holds the last solution: the initial guess becomes
+		 * 2 phi_n - phi_{n-1} once two solutions exist (the first solve starts
+		 * from whatever phi held, the second from the first solution) */
+		if (S->havePrev >= 2)
+			pinc_check(pinc_hip_extrapolate(S->phi[0], S->phiPrev, S->N[0], g_pinc.stream), "mg extrapolation");
+		else if (S->havePrev == 1)
+			pinc_check(pinc_hip_d2d(S->phiPrev, S->phi[0], S->N[0] * sizeof(double), g_pinc.stream), "mg extrapolation");
+		if (S->havePrev < 2) S->havePrev++;
 	}
 	if (S->nLevels > 1) {
 		/* the reference loops until converged (multigrid.c:1698); PINC_MG_MAX_CYCLES

@@ -125,3 +125,50 @@ def test_nd_solve_matches_oracle(name, native):
     if native:
         assert len(hg) <= 12
     assert np.max(np.abs(pg - po)) <= 1e-9 * np.max(np.abs(po))
+
+
+@pytest.mark.parametrize("layout", ["reference", "tiled"])
+def test_extrapolated_guess_matches_oracle(layout):
+    """multigrid:extrapolate (native mode, an extension: each solve starts
+    from 2 phi_n - phi_(n-1) instead of phi_n, pinc_hip_extrapolate) on a
+    warm 32^3 plasma: the device follows the oracle's restatement
+    (oracle/orc_native.c) step by step -- energies to 1e-8, the V-cycle
+    count per solve +-1 -- and needs no more cycles in total than the plain
+    warm start of the same run."""
+    import orc
+    from pinc_amd import Sim, configs
+    cfg = configs.config("warm", true_size=(32, 32, 32), ppc=8, nalloc_pc=16, levels=3)
+    cfg["multigrid"]["native"] = "1"
+    ini_plain = configs.write_ini(cfg)
+    cfg["multigrid"]["extrapolate"] = "1"
+    ini_o = configs.write_ini(cfg)
+    if layout == "tiled":
+        cfg["population"]["layout"] = "tiled"
+        cfg["population"]["sortInterval"] = "2"
+    ini_g = configs.write_ini(cfg)
+    steps = 8
+    try:
+        w = orc.World(ini_o)
+        w.init(perturb=False, maxwell=True, seed=5)
+        w.init_fields()
+        with Sim(ini_g, maxwell=True, perturb=False, seed=5) as s, Sim(ini_plain, maxwell=True, perturb=False,
+                                                                        seed=5) as p:
+            s.init()
+            p.init()
+            c0, co0, cp0 = s.cycles, w.cycles, p.cycles
+            for n in range(steps):
+                cs, co = s.cycles, w.cycles
+                s.step()
+                w.step()
+                p.step()
+                assert abs((s.cycles - cs) - (w.cycles - co)) <= 1, (n, s.cycles - cs, w.cycles - co)
+                ke, pe, _ = s.energy()
+                ke_o, pe_o = w.energy()
+                assert abs(ke - ke_o) <= 1e-8 * abs(ke_o), (n, ke, ke_o)
+                assert abs(pe - pe_o) <= 1e-8 * abs(pe_o), (n, pe, pe_o)
+            assert s.cycles - c0 <= p.cycles - cp0, (s.cycles - c0, p.cycles - cp0)
+            assert abs((s.cycles - c0) - (w.cycles - co0)) <= steps // 4 + 1
+        w.close()
+    finally:
+        for f in (ini_plain, ini_o, ini_g):
+            os.unlink(f)
