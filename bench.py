@@ -149,6 +149,8 @@ def main() -> int:
                          "c2: input/langmuir2D.ini at 128^2, 32 ppc (Langmuir perturbation, cold), multigrid")
     ap.add_argument("--size", type=int, default=None, help="global cells per dimension (c4: 256, c3: 128)")
     ap.add_argument("--ppc", type=int, default=None, help="particles per cell per species (c4: 64, c3: 32)")
+    ap.add_argument("--mg-graph", type=int, default=0,
+                    help="1: native multigrid replays each V-cycle as a captured HIP graph (multigrid:graph)")
     ap.add_argument("--mg-extrapolate", type=int, default=1,
                     help="1: native multigrid starts each solve from 2 phi_n - phi_(n-1) instead of phi_n "
                          "(multigrid:extrapolate; objects keep the plain warm start)")
@@ -252,6 +254,7 @@ def main() -> int:
         cfg["multigrid"]["native"] = "1"
         cfg["multigrid"]["shard"] = args.mg_shard
         cfg["multigrid"]["extrapolate"] = str(args.mg_extrapolate)
+        cfg["multigrid"]["graph"] = str(args.mg_graph)
     if c5:
         # a generated sphere (the reference's bepiColombo object file is not
         # available): centre of the grid, radius S/32
