@@ -153,7 +153,7 @@ def main() -> int:
                     help="1: native multigrid replays each V-cycle as a captured HIP graph (multigrid:graph)")
     ap.add_argument("--mg-extrapolate", type=int, default=1,
                     help="1: native multigrid starts each solve from 2 phi_n - phi_(n-1) instead of phi_n "
-                         "(multigrid:extrapolate; objects keep the plain warm start)")
+                         "(multigrid:extrapolate; with an object, the two solves of a step from their own histories)")
     ap.add_argument("--mg", default="native", choices=["native", "reference"],
                     help="native: correction-scheme V-cycle with the coarse h^2 factor (default; the reference "
                          "algorithm does not converge at 256^3 with 5 levels, DESIGN.md section 6); reference: "
@@ -390,7 +390,9 @@ def main() -> int:
                         f"multigrid mgVRecursive, {mg_levels} levels ({S}^{nd} down to {S >> (mg_levels - 1)}^{nd}), "
                         "RB Gauss-Seidel 10/10/10, "
                         + ("native mode (correction scheme, coarse h^2 factor; the ini's 5 levels extended"
-                           + ("; initial guess 2 phi_n - phi_(n-1)" if args.mg_extrapolate and not c5 else "")
+                           + (("; initial guesses extrapolated: the first solve of a step from the last two "
+                               "steps' first solutions, the second from the first + the last correction response"
+                               if c5 else "; initial guess 2 phi_n - phi_(n-1)") if args.mg_extrapolate else "")
                            + "; RMS residual <= 1e-10 as the reference)"
                            if args.mg == "native" else "reference algorithm (parity mode)")
                         + (f", level 0 sharded over the slabs ({mg_halo} halo planes per side), levels >= 1 "

@@ -204,6 +204,17 @@ long mgHistory(const MultigridSolver *solver, double *out, long cap);
 int mgLevels(const MultigridSolver *solver);
 /* halo planes of the sharded level 0 (multigrid:shard), 0 for a replicated solve */
 int mgShardHalo(const MultigridSolver *solver);
+/* multigrid:extrapolate with objects (two solves per step, main.c:230-238):
+ * the initial guess of the NEXT solve only -- FIRST: extrapolated from the
+ * first solutions of the last two steps; SECOND: this step's first solution
+ * plus the last step's correction response; WARM: the reference's warm
+ * start (any solve not announced, e.g. the capacitance matrix's).  Runs
+ * without objects extrapolate every solve (SERIES) and ignore this. */
+#define PINC_MG_GUESS_WARM 0
+#define PINC_MG_GUESS_SERIES 1
+#define PINC_MG_GUESS_FIRST 2
+#define PINC_MG_GUESS_SECOND 3
+void mgGuessNext(MultigridSolver *solver, int role);
 
 /* ---------------------------------------------------------- spectral -- */
 /* spectral.c:14-115; N-D extension of the reference's 1-D solver on rocFFT */

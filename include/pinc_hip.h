@@ -371,6 +371,8 @@ int pinc_hip_sub_dev(double *a, long n, const double *mu, void *stream);
  * last two solutions (mgSolveRaw, multigrid.c:1688-1724, warm-starts from the
  * last one) */
 int pinc_hip_extrapolate(double *phi, double *prev, long n, void *stream);
+/* out = a x + b y over n values (out may alias x or y) */
+int pinc_hip_lincomb(double *out, const double *x, double a, const double *y, double b, long n, void *stream);
 /* mgResidual (multigrid.c:1385-1403): res = lap(phi) + rho */
 int pinc_hip_residual(double *res, const double *phi, const double *rho, pinc_lvl_t L,
                       void *stream);

@@ -197,7 +197,13 @@ void ow_spectral_solve(OWorld *w);
  * reference's algorithm): correction scheme with the coarse h^2 factor */
 ONative *on_alloc(int nd, const int *Tglobal, int nLevelsIni, int nd3);
 void on_free(ONative *S);
-void on_set_extrapolate(ONative *S, int on);
+/* initial-guess roles (include/pinc.h PINC_MG_GUESS_*) */
+#define ON_GUESS_WARM 0
+#define ON_GUESS_SERIES 1
+#define ON_GUESS_FIRST 2
+#define ON_GUESS_SECOND 3
+void on_set_extrapolate(ONative *S, int on, int objects);
+void on_guess_next(ONative *S, int role);
 int on_levels(const ONative *S);
 void ow_native_solve(OWorld *w);
 /* single-grid stencil primitives (exported for unit tests) */

@@ -38,10 +38,13 @@ struct ONative {
 	NLv L[ON_MAX_LEVELS];
 	double *rho[ON_MAX_LEVELS], *phi[ON_MAX_LEVELS], *res[ON_MAX_LEVELS];
 	int nd3;        /* 3-D GS / restriction forms (gaussSeidelRB, halfWeight) */
-	/* multigrid:extrapolate (pinc_mg.c): initial guess 2 phi_n - phi_{n-1}
-	 * once two solutions exist; prev holds phi_{n-1}, nSeen counts solves */
-	int extrap, nSeen;
-	double *prev;
+	/* multigrid:extrapolate (pinc_mg.c guess_begin / guess_end): without
+	 * objects 2 phi_n - phi_{n-1} once two solutions exist (prev holds
+	 * phi_{n-1}, nSeen counts solves); with objects the first solve of a
+	 * step from the first solutions of the last two steps (A, B), the
+	 * second as the first plus the last step's correction response (D) */
+	int extrap, nSeen, objects, role, haveCorr;
+	double *prev, *A, *B, *D;
 };
 
 static NLv mklv(int nd, const int *T){
@@ -75,14 +78,24 @@ ONative *on_alloc(int nd, const int *Tg, int nLevelsIni, int nd3){
 	return S;
 }
 
-void on_set_extrapolate(ONative *S, int on){
+void on_set_extrapolate(ONative *S, int on, int objects){
+	long N = S->L[0].N;
 	S->extrap = on;
-	if(on && !S->prev) S->prev = calloc(S->L[0].N, sizeof(double));
+	S->objects = objects;
+	S->role = objects ? ON_GUESS_WARM : ON_GUESS_SERIES;
+	if(on && !objects && !S->prev) S->prev = calloc(N, sizeof(double));
+	if(on && objects && !S->A){
+		S->A = calloc(N, sizeof(double));
+		S->B = calloc(N, sizeof(double));
+		S->D = calloc(N, sizeof(double));
+	}
 }
+
+void on_guess_next(ONative *S, int role){ if(S->objects) S->role = role; }
 
 void on_free(ONative *S){
 	if(!S) return;
-	free(S->prev);
+	free(S->prev); free(S->A); free(S->B); free(S->D);
 	for(int q = 0; q < S->nLevels; q++){ free(S->rho[q]); free(S->phi[q]); free(S->res[q]); }
 	free(S);
 }
@@ -271,12 +284,19 @@ void ow_native_solve(OWorld *w){
 	ONative *S = w->native;
 	gather_scatter(w, S->rho[0], S->phi[0], 0);
 	long N = S->L[0].N;
-	if(S->extrap){
-		/* phi holds the last solution (the device's pinc_hip_extrapolate) */
+	/* phi holds the last solution (the device's pinc_hip_extrapolate /
+	 * pinc_hip_lincomb, same expressions) */
+	const int role = S->extrap ? S->role : ON_GUESS_WARM;
+	double *ph = S->phi[0];
+	if(role == ON_GUESS_SERIES){
 		if(S->nSeen >= 2){
-			for(long g = 0; g < N; g++){ double p = S->phi[0][g]; S->phi[0][g] = 2.0*p - S->prev[g]; S->prev[g] = p; }
-		} else if(S->nSeen == 1) memcpy(S->prev, S->phi[0], N*sizeof(double));
+			for(long g = 0; g < N; g++){ double p = ph[g]; ph[g] = 2.0*p - S->prev[g]; S->prev[g] = p; }
+		} else if(S->nSeen == 1) memcpy(S->prev, ph, N*sizeof(double));
 		if(S->nSeen < 2) S->nSeen++;
+	} else if(role == ON_GUESS_FIRST && S->nSeen >= 2){
+		for(long g = 0; g < N; g++) ph[g] = 2.0*S->A[g] + -1.0*S->B[g];
+	} else if(role == ON_GUESS_SECOND && S->haveCorr){
+		for(long g = 0; g < N; g++) ph[g] = 1.0*ph[g] + 1.0*S->D[g];
 	}
 	double barRes = 2.;
 	long c = 0;
@@ -300,6 +320,15 @@ void ow_native_solve(OWorld *w){
 		if(w->mgCap > 0 && ++c >= w->mgCap) break;
 		if(!isfinite(barRes)) orc_die("native multigrid diverged (residual %g)", barRes);
 	}
+	if(role == ON_GUESS_FIRST){
+		double *t = S->B; S->B = S->A; S->A = t;
+		memcpy(S->A, ph, N*sizeof(double));
+		if(S->nSeen < 2) S->nSeen++;
+	} else if(role == ON_GUESS_SECOND && S->nSeen >= 1){
+		for(long g = 0; g < N; g++) S->D[g] = 1.0*ph[g] + -1.0*S->A[g];
+		S->haveCorr = 1;
+	}
+	if(S->objects) S->role = ON_GUESS_WARM;
 	gather_scatter(w, NULL, S->phi[0], 1);
 	OGrid *phi[256];
 	for(int r = 0; r < w->P; r++) phi[r] = &w->r[r].phi;

@@ -219,7 +219,10 @@ void oo_capacitance(OObj *o, OWorld *w) {
 		for (long i = 0; i < n; i++) {
 			og_zero(rho);
 			rho->val[sf[i]] = 1.0;
-			ow_mg_solve(w);
+			/* the run's multigrid, as the device (pinc_obj_capacitance):
+			 * native mode when configured, with the warm start */
+			if (w->native) ow_native_solve(w);
+			else ow_mg_solve(w);
 			for (long k = 0; k < n; k++) P[k * n + i] = phi->val[sf[k]];
 		}
 		invert(P, o->capInv + o->capOff[a], n);

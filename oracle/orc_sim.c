@@ -246,9 +246,9 @@ OWorld *ow_create(OIni *ini, int literal){
 		int Tg[3] = {1, 1, 1};
 		for(int d = 0; d < nd; d++) Tg[d] = w->r[0].rho.trueSize[d+1]*w->r[0].mpi.nSubdomains[d];
 		w->native = on_alloc(nd, Tg, w->nLevels, w->restrictor == ORC_RESTR_3D);
-		/* multigrid:extrapolate, as pinc_mg.c (not with objects) */
-		on_set_extrapolate(w->native, oini_has(ini, "multigrid:extrapolate") && oini_int(ini, "multigrid:extrapolate") &&
-		                              !oini_has(ini, "objects:sphere") && !oini_has(ini, "objects:file"));
+		/* multigrid:extrapolate, as pinc_mg.c */
+		on_set_extrapolate(w->native, oini_has(ini, "multigrid:extrapolate") && oini_int(ini, "multigrid:extrapolate"),
+		                   oini_has(ini, "objects:sphere") || oini_has(ini, "objects:file"));
 	}
 	else if(nd == 1 && w->P == 1){
 		int N = w->r[0].rho.trueSize[1];
@@ -442,8 +442,10 @@ void oo_step(OWorld *w, OObj *o){
 		OGrid *rho[1] = {&w->r[0].rho};
 		ow_halo(w, rho, OP_ADD, FROMHALO);
 	}
+	if(w->native) on_guess_next(w->native, ON_GUESS_FIRST);
 	do_solve(w);
 	oo_apply(o, w, NULL);
+	if(w->native) on_guess_next(w->native, ON_GUESS_SECOND);
 	do_solve(w);
 	do_efield(w, 1);
 	do_acc(w);

@@ -55,6 +55,11 @@ __global__ void k_extrapolate(double *__restrict__ phi, double *__restrict__ pre
 	}
 }
 
+__global__ void k_lincomb(double *out, const double *x, double a, const double *y, double b, long n) {
+	for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+		out[i] = a * x[i] + b * y[i];
+}
+
 // plane p of a slab: plane size = product of the non-slab extents
 __global__ void k_add_plane(double *dst, const double *src, long planeSize) {
 	for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < planeSize; i += (long)gridDim.x * blockDim.x)
@@ -175,6 +180,13 @@ extern "C" int pinc_hip_extrapolate(double *phi, double *prev, long n, void *str
 	if (n <= 0) return 0;
 	hipLaunchKernelGGL(k_extrapolate, dim3(grid_for(n)), dim3(kThreads), 0, (hipStream_t)stream, phi, prev, n);
 	return check_launch("extrapolate");
+}
+
+extern "C" int pinc_hip_lincomb(double *out, const double *x, double a, const double *y, double b, long n,
+                                void *stream) {
+	if (n <= 0) return 0;
+	hipLaunchKernelGGL(k_lincomb, dim3(grid_for(n)), dim3(kThreads), 0, (hipStream_t)stream, out, x, a, y, b, n);
+	return check_launch("lincomb");
 }
 
 static long plane_size(const pinc_geom_t &g) {

@@ -169,10 +169,15 @@ struct MultigridSolver {
 	double *hist;
 	long histCap, histN, maxCycles;
 	long fusedMin;     /* smallest level (points) smoothed by the fused sweeps */
-	/* multigrid:extrapolate: level-0 initial guess 2 phi_n - phi_{n-1} (prev
-	 * holds phi_{n-1}; havePrev counts the solves seen, up to 2) */
-	int extrap, havePrev;
-	double *phiPrev;
+	/* multigrid:extrapolate: level-0 initial guesses (pinc_mg.c guess_*).
+	 * Runs without objects: 2 phi_n - phi_{n-1} (phiPrev holds phi_{n-1};
+	 * havePrev counts the solves seen, up to 2).  Runs with objects (two
+	 * solves per step, mgGuessNext): the first from the first solves of the
+	 * last two steps (phiA, phiB), the second as the first plus the last
+	 * step's correction response (dCorr = its second minus its first
+	 * solution); any other solve keeps the warm start. */
+	int extrap, havePrev, objects, role, haveCorr;
+	double *phiPrev, *phiA, *phiB, *dCorr;
 	/* sharded level 0 (native mode, multigrid:shard):
 	 * rho[0]/phi[0]/res[0] are this rank's z-slab with hz halo planes on
 	 * each side (L[0], N[0] = that extended slab), levels >= 1 global */

@@ -137,13 +137,13 @@ MultigridSolver *mgAllocSolver(const dictionary *ini, Grid *rho, Grid *phi) {
 	 * C4, the gaps between dependent kernels are GPU-side) */
 	S->useGraph = S->native && iniHas(ini, "multigrid:graph") && iniGetInt(ini, "multigrid:graph");
 	S->cycleGraph = NULL;
-	/* initial guess extrapolated from the last two solutions (native mode,
-	 * opt-in; objects solve twice per step and for the capacitance matrix,
-	 * so they keep the plain warm start) */
-	S->extrap = S->native && iniHas(ini, "multigrid:extrapolate") && iniGetInt(ini, "multigrid:extrapolate") &&
-	            !iniHas(ini, "objects:sphere") && !iniHas(ini, "objects:file");
-	S->havePrev = 0;
-	S->phiPrev = NULL;
+	/* initial guesses extrapolated from earlier solutions (native mode,
+	 * opt-in; guess_begin) */
+	S->extrap = S->native && iniHas(ini, "multigrid:extrapolate") && iniGetInt(ini, "multigrid:extrapolate");
+	S->objects = iniHas(ini, "objects:sphere") || iniHas(ini, "objects:file");
+	S->havePrev = S->haveCorr = 0;
+	S->role = S->objects ? PINC_MG_GUESS_WARM : PINC_MG_GUESS_SERIES;
+	S->phiPrev = S->phiA = S->phiB = S->dCorr = NULL;
 	/* native mode: levels of at least fusedMin points smooth with the
 	 * z-marching fused sweeps (two iterations per launch), smaller ones
 	 * colour by colour (PINC_MG_FUSED_MIN overrides, experiments) */
@@ -201,7 +201,13 @@ MultigridSolver *mgAllocSolver(const dictionary *ini, Grid *rho, Grid *phi) {
 		pinc_check(pinc_hip_malloc((void **)&S->res[q], S->N[q] * sizeof(double)), "mg level");
 	}
 	if (S->shard) phi->dev->ext = S->phi[0];
-	if (S->extrap) pinc_check(pinc_hip_malloc((void **)&S->phiPrev, S->N[0] * sizeof(double)), "mg extrapolation");
+	if (S->extrap && !S->objects)
+		pinc_check(pinc_hip_malloc((void **)&S->phiPrev, S->N[0] * sizeof(double)), "mg extrapolation");
+	if (S->extrap && S->objects) {
+		pinc_check(pinc_hip_malloc((void **)&S->phiA, S->N[0] * sizeof(double)), "mg extrapolation");
+		pinc_check(pinc_hip_malloc((void **)&S->phiB, S->N[0] * sizeof(double)), "mg extrapolation");
+		pinc_check(pinc_hip_malloc((void **)&S->dCorr, S->N[0] * sizeof(double)), "mg extrapolation");
+	}
 	S->rhoGrid = rho;
 	S->phiGrid = phi;
 	return S;
@@ -211,6 +217,9 @@ void mgFreeSolver(MultigridSolver *S) {
 	if (!S) return;
 	pinc_hip_graph_destroy(S->cycleGraph);
 	pinc_hip_free(S->phiPrev);
+	pinc_hip_free(S->phiA);
+	pinc_hip_free(S->phiB);
+	pinc_hip_free(S->dCorr);
 	free(S->hist);
 	for (int q = 0; q < S->nLevels; q++) {
 		if (q > 0 || S->shard) {
@@ -227,6 +236,44 @@ void mgFreeSolver(MultigridSolver *S) {
 }
 
 long mgCycleCount(const MultigridSolver *S) { return S->cycles; }
+
+void mgGuessNext(MultigridSolver *S, int role) {
+	if (S && S->objects) S->role = role;
+}
+
+/* initial guess of a solve (multigrid:extrapolate); phi[0] holds the last
+ * solution of this solver when a solve starts */
+static void guess_begin(MultigridSolver *S, int role) {
+	long n = S->N[0];
+	double *phi = S->phi[0];
+	if (role == PINC_MG_GUESS_SERIES) {
+		/* 2 phi_n - phi_{n-1} once two solutions exist (the first solve
+		 * starts from whatever phi held, the second from the first solution) */
+		if (S->havePrev >= 2) pinc_check(pinc_hip_extrapolate(phi, S->phiPrev, n, g_pinc.stream), "mg extrapolation");
+		else if (S->havePrev == 1) pinc_check(pinc_hip_d2d(S->phiPrev, phi, n * sizeof(double), g_pinc.stream), "mg extrapolation");
+		if (S->havePrev < 2) S->havePrev++;
+	} else if (role == PINC_MG_GUESS_FIRST && S->havePrev >= 2) {
+		/* from the first solutions of the last two steps */
+		pinc_check(pinc_hip_lincomb(phi, S->phiA, 2.0, S->phiB, -1.0, n, g_pinc.stream), "mg extrapolation");
+	} else if (role == PINC_MG_GUESS_SECOND && S->haveCorr) {
+		/* this step's first solution + the last step's correction response */
+		pinc_check(pinc_hip_lincomb(phi, phi, 1.0, S->dCorr, 1.0, n, g_pinc.stream), "mg extrapolation");
+	}
+}
+
+static void guess_end(MultigridSolver *S, int role) {
+	long n = S->N[0];
+	if (role == PINC_MG_GUESS_FIRST) {
+		double *t = S->phiB;
+		S->phiB = S->phiA;
+		S->phiA = t;
+		pinc_check(pinc_hip_d2d(S->phiA, S->phi[0], n * sizeof(double), g_pinc.stream), "mg extrapolation");
+		if (S->havePrev < 2) S->havePrev++;
+	} else if (role == PINC_MG_GUESS_SECOND && S->havePrev >= 1) {
+		pinc_check(pinc_hip_lincomb(S->dCorr, S->phi[0], 1.0, S->phiA, -1.0, n, g_pinc.stream), "mg extrapolation");
+		S->haveCorr = 1;
+	}
+}
 
 void mgSetLimit(MultigridSolver *S, long maxCycles, long histCap) {
 	S->maxCycles = maxCycles > 0 ? maxCycles : 0;
@@ -440,16 +487,8 @@ void mgSolve(MultigridSolver *S, Grid *rho, Grid *phi, const MpiInfo *mpiInfo) {
 		long ps = rho->dev->planeSize;
 		pinc_comm_allgather(rho->dev->d + ps, rho->dev->global, ps * rho->dev->geom.nloc, "gather rho");
 	}
-	if (S->extrap) {
-		/* phi[0] holds the last solution: the initial guess becomes
-		 * 2 phi_n - phi_{n-1} once two solutions exist (the first solve starts
-		 * from whatever phi held, the second from the first solution) */
-		if (S->havePrev >= 2)
-			pinc_check(pinc_hip_extrapolate(S->phi[0], S->phiPrev, S->N[0], g_pinc.stream), "mg extrapolation");
-		else if (S->havePrev == 1)
-			pinc_check(pinc_hip_d2d(S->phiPrev, S->phi[0], S->N[0] * sizeof(double), g_pinc.stream), "mg extrapolation");
-		if (S->havePrev < 2) S->havePrev++;
-	}
+	const int role = S->extrap ? S->role : PINC_MG_GUESS_WARM;
+	guess_begin(S, role);
 	if (S->nLevels > 1) {
 		/* the reference loops until converged (multigrid.c:1698); PINC_MG_MAX_CYCLES
 		 * caps a solve for diagnostics (stops with a warning) */
@@ -520,6 +559,8 @@ void mgSolve(MultigridSolver *S, Grid *rho, Grid *phi, const MpiInfo *mpiInfo) {
 			smooth(S, 0, S->nCoarse, S->coarse3d);
 		}
 	}
+	guess_end(S, role);
+	if (S->objects) S->role = PINC_MG_GUESS_WARM; /* mgGuessNext holds for one solve */
 	phi->dev->ghostsValid = 0;
 	if (S->shard) {
 		/* the slab with its ghost planes (exact: within hz - 2 chunk of the

@@ -166,8 +166,10 @@ static void sim_step(PincSim *S) {
 		 * loop), solve, capacitance correction, solve */
 		pinc_obj_add_rho(S->obj, S->rho);
 		if (S->opts.literal) gHaloOp((funPtr)addSlice, S->rho, S->mpi, FROMHALO);
+		if (!S->spectral) mgGuessNext(S->solver, PINC_MG_GUESS_FIRST);
 		S->solve(S->solver, S->rho, S->phi, S->mpi);
 		pinc_obj_apply(S->obj, S->rho, S->phi);
+		if (!S->spectral) mgGuessNext(S->solver, PINC_MG_GUESS_SECOND);
 	} else if (S->opts.literal) {
 		gHaloOp((funPtr)addSlice, S->rho, S->mpi, FROMHALO);
 		S->solve(S->solver, S->rho, S->phi, S->mpi);

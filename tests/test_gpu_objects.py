@@ -311,3 +311,47 @@ def test_reference_masks_64_green_equals_solve(built, name):
     assert (a0, a1) == (b0, b1)
     assert ia == 0 and ib == 0
     assert abs(ka - kb) <= 1e-7 * abs(ka) and abs(pa - pb) <= 1e-7 * abs(pa)
+
+
+@pytest.mark.parametrize("fused", [0, 1])
+def test_object_extrapolated_guesses_match_checker(built, fused):
+    """multigrid:extrapolate with an object (native mode, an extension;
+    mgGuessNext): the first solve of each step starts
+    from the first solutions of the last two steps, the second from this
+    step's first solution plus the last step's correction response; the
+    capacitance matrix's solves keep the warm start.  The checker restates
+    the same guesses (oracle/orc_native.c): counts exact, energies and phi
+    to 1e-7, V-cycles per step within 2."""
+    from pinc_amd import Sim
+    T, sphere = (32, 16, 16), (20.3, 7.6, 9.1, 3.2)
+    cfg = configs.config("cold3d", true_size=T, nsub=(1, 1, 1))
+    cfg["multigrid"]["mgLevels"] = "3"
+    cfg["multigrid"]["native"] = "1"
+    cfg["multigrid"]["extrapolate"] = "1"
+    cfg["population"]["fused"] = "0"
+    cfg["objects"] = {"sphere": ",".join(map(str, sphere))}
+    ini = configs.write_ini(cfg)
+    cfg["population"]["fused"] = str(fused)
+    ini_dev = configs.write_ini(cfg)
+    w = orc.World(ini)
+    w.init()
+    ob = orc.Objects(w, _sphere(T, sphere[:3], sphere[3]))
+    ob.capacitance()
+    ob.init_collect()
+    w.init_fields()
+    with Sim(ini_dev) as s:
+        s.init()
+        for k in range(6):
+            cs, co = s.cycles, w.cycles
+            ob.step()
+            s.step()
+            assert abs((s.cycles - cs) - (w.cycles - co)) <= 2, (k, s.cycles - cs, w.cycles - co)
+            ke_o, pe_o = w.energy()
+            ke, pe, _ = s.energy()
+            for sp in range(2):
+                assert s.count(sp) == w.count(sp), (k, sp)
+            assert abs(ke - ke_o) <= 1e-7 * abs(ke_o), (k, ke, ke_o)
+            assert abs(pe - pe_o) <= 1e-7 * abs(pe_o), (k, pe, pe_o)
+        phi_g = s.grid(1)[1:-1, 1:-1, 1:-1]
+        phi_o = w.grid(1)[1:-1, 1:-1, 1:-1]
+        assert np.max(np.abs(phi_g - phi_o)) <= 1e-7 * np.abs(phi_o).max()
