@@ -12,3 +12,14 @@ timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 
 python3 -c "
 import json; r=json.load(open('$O/bench4.json'))
 print('n_gpus', r['n_gpus'], 'value %.4g ms/step %.2f solve %.2f' % (r['value'], r['ms_per_step'], r['poisson_ms_per_step']), r['config']['poisson'][-90:])"
+# eight ranks (the driver's N=8 slab geometry at 256^3, 8 ppc, shard auto; 128^3
+# slabs of 16 planes break the reference's trueSize % 2^mgLevels rule) and two
+# ranks of C5 (object, replicated solve), both with the extrapolated guesses
+timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 8 --steps 3 --warmup 2 --size 256 --ppc 8 --host-transport --no-cpu-baseline > $O/bench8.json 2> $O/bench8.err || { tail -30 $O/bench8.err; exit 1; }
+python3 -c "
+import json; r=json.load(open('$O/bench8.json'))
+print('n_gpus', r['n_gpus'], 'value %.4g ms/step %.2f solve %.2f cycles %.2f' % (r['value'], r['ms_per_step'], r['poisson_ms_per_step'], r['mg_cycles_per_solve']), r['config']['poisson'][-90:])"
+timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29535 bench.py --gpus 2 --workload c5 --steps 3 --warmup 2 --size 128 --host-transport --no-cpu-baseline > $O/bench2_c5.json 2> $O/bench2_c5.err || { tail -30 $O/bench2_c5.err; exit 1; }
+python3 -c "
+import json; r=json.load(open('$O/bench2_c5.json'))
+print('c5 n_gpus', r['n_gpus'], 'value %.4g ms/step %.2f solve %.2f cycles %.2f' % (r['value'], r['ms_per_step'], r['poisson_ms_per_step'], r['mg_cycles_per_solve']))"
