@@ -75,7 +75,8 @@ def _cpu_threads() -> int:
     return max(1, min(aff, int(os.environ.get("OMP_NUM_THREADS", aff))))
 
 
-def _cpu_baseline(size: int, ppc: int, steps: int, native: bool, workload: str = "c4") -> dict:
+def _cpu_baseline(size: int, ppc: int, steps: int, native: bool, workload: str = "c4",
+                  extrapolate: int = 0) -> dict:
     """The oracle (plain-C restatement of the reference) on the host cores,
     on a bounded sample of the same workload: the warm plasma at size^3 with
     ppc particles per cell per species, decomposed into one z-slab per
@@ -104,6 +105,7 @@ def _cpu_baseline(size: int, ppc: int, steps: int, native: bool, workload: str =
                              nsub=(1, 1, nsub), ppc=ppc, nalloc_pc=ppc + 8, levels=1 if native else 5)
     if native and cfg["methods"]["poisson"] == "mgSolver":
         cfg["multigrid"]["native"] = "1"
+        cfg["multigrid"]["extrapolate"] = str(extrapolate)
     ini = configs.write_ini(cfg)
     t_init = time.perf_counter()
     w = orc.World(ini)
@@ -128,7 +130,9 @@ def _cpu_baseline(size: int, ppc: int, steps: int, native: bool, workload: str =
                       f"{threads} threads) on the same {workload.upper()} workload at {size}^{nd}, {ppc} ppc x 2 "
                       f"species ({n} particles), {steps} steps; "
                       + ("spectral solve (naive DFT restatement)" if cfg["methods"]["poisson"] == "sSolver" else
-                         "multigrid " + ("native mode as the GPU line" if native else "reference algorithm")
+                         "multigrid " + ("native mode as the GPU line" + (" (extrapolated initial guess)"
+                                                                           if extrapolate else "")
+                                         if native else "reference algorithm")
                          + f", {levels} levels, {cyc:.0f} V-cycles/solve"),
             "seconds": dt, "init_s": t_init,
             "push_deposit_updates_per_s": n / (push_ms * 1e-3) if push_ms > 0 else None,
@@ -439,7 +443,8 @@ def main() -> int:
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = _cpu_baseline(S if c2 else args.cpu_size, args.ppc, args.cpu_steps,
-                                               args.mg == "native", args.workload if args.workload != "c5" else "c4")
+                                               args.mg == "native", args.workload if args.workload != "c5" else "c4",
+                                               args.mg_extrapolate)
     if rank == 0:
         print(json.dumps(result), file=out, flush=True)
     if dist is not None:
