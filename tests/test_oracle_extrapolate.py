@@ -1,0 +1,78 @@
+"""The checker's restatement of multigrid:extrapolate (oracle/orc_native.c,
+the device's pinc_mg.c guess_begin / guess_end), on the
+CPU: the extrapolated initial guesses change how many V-cycles a solve
+takes, not what it converges to.  Each case runs in a few seconds.
+"""
+import numpy as np
+
+import orc
+from pinc_amd import configs
+
+
+def _sphere(T, c, r):
+    z, y, x = np.meshgrid(*[np.arange(t, dtype=float) for t in (T[2], T[1], T[0])], indexing="ij")
+    return (((x - c[0]) ** 2 + (y - c[1]) ** 2 + (z - c[2]) ** 2) <= r * r).astype(float)
+
+
+def _warm(extrapolate, objects=None):
+    cfg = configs.config("warm", true_size=(32, 32, 32), ppc=8, nalloc_pc=16, levels=3)
+    cfg["multigrid"]["native"] = "1"
+    cfg["multigrid"]["extrapolate"] = str(extrapolate)
+    if objects:
+        cfg["population"]["fused"] = "0"
+        cfg["objects"] = {"sphere": ",".join(map(str, objects))}
+    return configs.write_ini(cfg)
+
+
+def _cycles_per_step(w, step, steps):
+    c = [w.cycles]
+    for _ in range(steps):
+        step()
+        c.append(w.cycles)
+    return list(np.diff(c))
+
+
+def test_series_guess_same_run_fewer_cycles():
+    """No objects: 2 phi_n - phi_(n-1) from the third solve on.  Same
+    energies as the warm start to the solver tolerance, and no solve needs
+    more V-cycles (at this size: 4 each with the warm start, 3 from the
+    second step on)."""
+    runs = {}
+    for ex in (0, 1):
+        w = orc.World(_warm(ex))
+        w.init(perturb=False, maxwell=True, seed=5)
+        w.init_fields()
+        cyc = _cycles_per_step(w, w.step, 8)
+        runs[ex] = (cyc, w.energy())
+        w.close()
+    (c0, e0), (c1, e1) = runs[0], runs[1]
+    assert all(b <= a for a, b in zip(c0, c1)), (c0, c1)
+    assert sum(c1) < sum(c0)
+    for a, b in zip(e0, e1):
+        assert abs(a - b) <= 1e-9 * abs(a)
+
+
+def test_object_guesses_same_run():
+    """With an object (two solves per step: FIRST from the last two steps'
+    first solutions, SECOND from this step's first plus the last correction
+    response; the capacitance matrix's solves keep the warm start): the same
+    particles and energies as the warm start to the solver tolerance, and
+    never more V-cycles in total."""
+    T, sp = (32, 32, 32), (16.3, 15.6, 17.1, 4.2)
+    runs = {}
+    for ex in (0, 1):
+        w = orc.World(_warm(ex, sp))
+        w.init(perturb=False, maxwell=True, seed=5)
+        ob = orc.Objects(w, _sphere(T, sp[:3], sp[3]))
+        ob.capacitance()
+        ob.init_collect()
+        w.init_fields()
+        cyc = _cycles_per_step(w, ob.step, 6)
+        runs[ex] = (cyc, w.energy(), [w.count(s) for s in range(2)], ob.collected(0))
+        ob.close()
+        w.close()
+    (c0, e0, n0, q0), (c1, e1, n1, q1) = runs[0], runs[1]
+    assert n0 == n1 and q0 == q1
+    assert sum(c1) <= sum(c0), (c0, c1)
+    for a, b in zip(e0, e1):
+        assert abs(a - b) <= 1e-7 * abs(a)
