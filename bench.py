@@ -169,6 +169,10 @@ def main() -> int:
     ap.add_argument("--layout", default="tiled", choices=["tiled", "reference"],
                     help="tiled: particles re-sorted by 4^3-cell tile every --sort-interval moves (default); "
                          "reference: the reference's particle order (bit-exact indices)")
+    ap.add_argument("--obj-second-guess", default="spectral", choices=["response", "spectral"],
+                    help="objects with --mg-extrapolate: the second solve of a step starts from the first solution "
+                         "plus the last step's correction response, or plus the exact discrete response to this "
+                         "step's correction charge (rocFFT; one rank)")
     ap.add_argument("--obj-capacitance", default="solve", choices=["solve", "green"],
                     help="c5: capacitance matrix by one solve per surface node (the reference's, default) or "
                          "by translating one periodic response (objects:capacitance = green)")
@@ -262,7 +266,8 @@ def main() -> int:
     if c5:
         # a generated sphere (the reference's bepiColombo object file is not
         # available): centre of the grid, radius S/32
-        cfg["objects"] = {"sphere": f"{S / 2},{S / 2},{S / 2},{S / 32}", "capacitance": args.obj_capacitance}
+        cfg["objects"] = {"sphere": f"{S / 2},{S / 2},{S / 2},{S / 32}", "capacitance": args.obj_capacitance,
+                          "secondGuess": args.obj_second_guess}
         cfg["population"]["fused"] = str(args.c5_fused)
     if args.layout == "tiled":
         cfg["population"]["layout"] = "tiled"
@@ -395,7 +400,9 @@ def main() -> int:
                         "RB Gauss-Seidel 10/10/10, "
                         + ("native mode (correction scheme, coarse h^2 factor; the ini's 5 levels extended"
                            + (("; initial guesses extrapolated: the first solve of a step from the last two "
-                               "steps' first solutions, the second from the first + the last correction response"
+                               "steps' first solutions, the second from the first + "
+                               + ("the exact discrete response to the correction charge (rocFFT)"
+                                  if args.obj_second_guess == "spectral" else "the last correction response")
                                if c5 else "; initial guess 2 phi_n - phi_(n-1)") if args.mg_extrapolate else "")
                            + "; RMS residual <= 1e-10 as the reference)"
                            if args.mg == "native" else "reference algorithm (parity mode)")

@@ -394,6 +394,11 @@ typedef struct pinc_fft_s pinc_fft_t;
 int pinc_hip_fft_create(pinc_fft_t **plan, int nd, const int *T, void *stream);
 int pinc_hip_fft_poisson(pinc_fft_t *plan, const double *rhoGlobal, double *phiGlobal, void *stream);
 void pinc_hip_fft_destroy(pinc_fft_t *plan);
+/* symbol of the plan's k-space factor: 0 the spectral solver's (above), 1
+ * the multigrid's 7-point (5-, 3-point) discrete Laplacian,
+ * 1/sum_d (2 - 2 cos(2 pi n_d/N_d))/N: the exact discrete solution the
+ * multigrid converges to (objects:secondGuess = spectral) */
+int pinc_hip_fft_set_symbol(pinc_fft_t *plan, int discrete);
 
 /* Slab-distributed 3-D spectral solve (several ranks,
  * z-slabs of nloc planes, Ty divisible by the rank count): the same operator

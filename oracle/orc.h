@@ -203,6 +203,8 @@ void on_free(ONative *S);
 #define ON_GUESS_FIRST 2
 #define ON_GUESS_SECOND 3
 void on_set_extrapolate(ONative *S, int on, int objects);
+void on_set_second_spectral(ONative *S, int on);
+void orc_discrete_poisson(int nd, const int *L, const double *rho, double *phi);
 void on_guess_next(ONative *S, int role);
 int on_levels(const ONative *S);
 void ow_native_solve(OWorld *w);

@@ -55,6 +55,7 @@ def _load() -> C.CDLL:
         "orc_world_mg_levels": (C.c_int, [vp]),
         "orc_world_timers": (None, [vp, vp]),
         "orc_world_nspecies": (C.c_int, [vp]),
+        "orc_discrete_poisson": (None, [C.c_int, vp, vp, vp]),
         "oo_create": (vp, [vp, vp]),
         "oo_free": (None, [vp]),
         "oo_capacitance": (None, [vp, vp]),

@@ -352,6 +352,35 @@ static void dft_axis(double *re, double *im, const int *L, int axis, int sign){
 	free(cr); free(ci); free(tr); free(ti);
 }
 
+/* phi = the exact solution of the multigrid's discrete Poisson problem
+ * -(sum of the 2 nd neighbours - 2 nd phi) = rho on a global periodic grid L
+ * (x fastest), DC dropped: phi = IDFT(DFT(rho) / sum_d (2 - 2 cos(2 pi
+ * n_d/L_d)) / N), the symbol of the device's pinc_hip_fft_set_symbol(plan,
+ * 1) (objects:secondGuess = spectral) */
+void orc_discrete_poisson(int nd, const int *Lin, const double *rho, double *phi){
+	int L[3] = {1, 1, 1};
+	for(int d = 0; d < nd; d++) L[d] = Lin[d];
+	long N = (long)L[0]*L[1]*L[2];
+	double *re = malloc(N*sizeof(double)), *im = calloc(N, sizeof(double));
+	memcpy(re, rho, N*sizeof(double));
+	for(int d = 0; d < nd; d++) dft_axis(re, im, L, d, -1);
+	for(long i = 0; i < N; i++){
+		long r = i;
+		double s = 0;
+		for(int d = 0; d < nd; d++){
+			int n = (int)(r % L[d]);
+			r /= L[d];
+			if(n > L[d]/2) n -= L[d];
+			s += 2.0 - 2.0*cos(2*M_PI*n/L[d]);
+		}
+		double f = i ? 1.0/s/N : 0.0;
+		re[i] *= f; im[i] *= f;
+	}
+	for(int d = 0; d < nd; d++) dft_axis(re, im, L, d, +1);
+	memcpy(phi, re, N*sizeof(double));
+	free(re); free(im);
+}
+
 /* global index <-> rank-local padded index (x fastest, ghosts g per side) */
 static long local_index(const OGrid *g, const int *p){
 	long i = 0;

@@ -45,6 +45,10 @@ struct ONative {
 	 * second as the first plus the last step's correction response (D) */
 	int extrap, nSeen, objects, role, haveCorr;
 	double *prev, *A, *B, *D;
+	/* objects:secondGuess = spectral: rho of the first solve, the exact
+	 * discrete response to the correction charge (orc_discrete_poisson) */
+	int secondSpectral;
+	double *rhoSave, *dphi;
 };
 
 static NLv mklv(int nd, const int *T){
@@ -93,9 +97,17 @@ void on_set_extrapolate(ONative *S, int on, int objects){
 
 void on_guess_next(ONative *S, int role){ if(S->objects) S->role = role; }
 
+void on_set_second_spectral(ONative *S, int on){
+	S->secondSpectral = on && S->extrap && S->objects;
+	if(S->secondSpectral && !S->rhoSave){
+		S->rhoSave = calloc(S->L[0].N, sizeof(double));
+		S->dphi = calloc(S->L[0].N, sizeof(double));
+	}
+}
+
 void on_free(ONative *S){
 	if(!S) return;
-	free(S->prev); free(S->A); free(S->B); free(S->D);
+	free(S->prev); free(S->A); free(S->B); free(S->D); free(S->rhoSave); free(S->dphi);
 	for(int q = 0; q < S->nLevels; q++){ free(S->rho[q]); free(S->phi[q]); free(S->res[q]); }
 	free(S);
 }
@@ -295,6 +307,10 @@ void ow_native_solve(OWorld *w){
 		if(S->nSeen < 2) S->nSeen++;
 	} else if(role == ON_GUESS_FIRST && S->nSeen >= 2){
 		for(long g = 0; g < N; g++) ph[g] = 2.0*S->A[g] + -1.0*S->B[g];
+	} else if(role == ON_GUESS_SECOND && S->secondSpectral && S->nSeen >= 1){
+		for(long g = 0; g < N; g++) S->rhoSave[g] = 1.0*S->rho[0][g] + -1.0*S->rhoSave[g];
+		orc_discrete_poisson(S->L[0].nd, S->L[0].T, S->rhoSave, S->dphi);
+		for(long g = 0; g < N; g++) ph[g] = 1.0*ph[g] + 1.0*S->dphi[g];
 	} else if(role == ON_GUESS_SECOND && S->haveCorr){
 		for(long g = 0; g < N; g++) ph[g] = 1.0*ph[g] + 1.0*S->D[g];
 	}
@@ -323,6 +339,7 @@ void ow_native_solve(OWorld *w){
 	if(role == ON_GUESS_FIRST){
 		double *t = S->B; S->B = S->A; S->A = t;
 		memcpy(S->A, ph, N*sizeof(double));
+		if(S->secondSpectral) memcpy(S->rhoSave, S->rho[0], N*sizeof(double));
 		if(S->nSeen < 2) S->nSeen++;
 	} else if(role == ON_GUESS_SECOND && S->nSeen >= 1){
 		for(long g = 0; g < N; g++) S->D[g] = 1.0*ph[g] + -1.0*S->A[g];

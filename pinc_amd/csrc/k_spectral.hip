@@ -29,6 +29,7 @@ struct pinc_fft_s {
 	void *work;
 	double *rin;      // private copy of rho
 	double2 *spec;    // half spectrum
+	int discrete;     // k-space factor of the discrete Laplacian (pinc_hip_fft_set_symbol)
 };
 
 namespace {
@@ -43,7 +44,7 @@ int fft_error(rocfft_status s, const char *where) {
 
 // spec[i] *= factor(i), spectral.c:29-37 (1-D) generalised to N-D
 __global__ void k_spectral_scale(double2 *__restrict__ spec, long n, int nd, int Tx, int Ty, int Tz,
-                                 double Ntot) {
+                                 double Ntot, int discrete) {
 	for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
 		int Mx = Tx / 2 + 1;
 		long r = i;
@@ -55,6 +56,14 @@ __global__ void k_spectral_scale(double2 *__restrict__ spec, long n, int nd, int
 		double f;
 		if (i == 0) {
 			f = 0.0;  // charge neutrality (spectral.c:103-104)
+		} else if (discrete) {
+			// -(sum of the 2 nd neighbours - 2 nd phi) = rho, mode by mode
+			int ny = iy <= Ty / 2 ? iy : iy - Ty;
+			int nz = iz <= Tz / 2 ? iz : iz - Tz;
+			double s = 2.0 - 2.0 * cos(2 * M_PI * ix / Tx);
+			if (nd > 1) s += 2.0 - 2.0 * cos(2 * M_PI * ny / Ty);
+			if (nd > 2) s += 2.0 - 2.0 * cos(2 * M_PI * nz / Tz);
+			f = 1.0 / s / Ntot;
 		} else if (nd == 1) {
 			f = Tx / (2 * M_PI * ix);  // size/(2*M_PI*n), squared, /size
 			f *= f;
@@ -142,10 +151,16 @@ extern "C" int pinc_hip_fft_poisson(pinc_fft_t *f, const double *rho, double *ph
 	long nb = (f->nSpec + 255) / 256;
 	if (nb > 8192) nb = 8192;
 	hipLaunchKernelGGL(k_spectral_scale, dim3((unsigned)nb), dim3(256), 0, st, f->spec, f->nSpec, f->nd, f->T[0],
-	                   f->T[1], f->T[2], (double)f->nReal);
+	                   f->T[1], f->T[2], (double)f->nReal, f->discrete);
 	if (int rc = check_launch("spectral scale")) return rc;
 	s = rocfft_execute(f->inv, sp, outp, f->info);
 	if (s != rocfft_status_success) return fft_error(s, "fft_poisson: inverse");
+	return 0;
+}
+
+extern "C" int pinc_hip_fft_set_symbol(pinc_fft_t *f, int discrete) {
+	if (!f) return set_error(hipErrorInvalidValue, "fft_set_symbol: no plan");
+	f->discrete = discrete != 0;
 	return 0;
 }
 

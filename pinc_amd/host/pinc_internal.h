@@ -178,6 +178,13 @@ struct MultigridSolver {
 	 * solution); any other solve keeps the warm start. */
 	int extrap, havePrev, objects, role, haveCorr;
 	double *phiPrev, *phiA, *phiB, *dCorr;
+	/* objects:secondGuess = spectral (one rank): the second solve of a step
+	 * starts from the first solution plus the exact discrete response to
+	 * the correction charge (rocFFT, the 7-point symbol); rhoSave holds the
+	 * first solve's rho */
+	int secondSpectral;
+	double *rhoSave, *dphi;
+	pinc_fft_t *fft;
 	/* sharded level 0 (native mode, multigrid:shard):
 	 * rho[0]/phi[0]/res[0] are this rank's z-slab with hz halo planes on
 	 * each side (L[0], N[0] = that extended slab), levels >= 1 global */

@@ -144,6 +144,9 @@ MultigridSolver *mgAllocSolver(const dictionary *ini, Grid *rho, Grid *phi) {
 	S->havePrev = S->haveCorr = 0;
 	S->role = S->objects ? PINC_MG_GUESS_WARM : PINC_MG_GUESS_SERIES;
 	S->phiPrev = S->phiA = S->phiB = S->dCorr = NULL;
+	S->secondSpectral = 0;
+	S->rhoSave = S->dphi = NULL;
+	S->fft = NULL;
 	/* native mode: levels of at least fusedMin points smooth with the
 	 * z-marching fused sweeps (two iterations per launch), smaller ones
 	 * colour by colour (PINC_MG_FUSED_MIN overrides, experiments) */
@@ -203,6 +206,20 @@ MultigridSolver *mgAllocSolver(const dictionary *ini, Grid *rho, Grid *phi) {
 	if (S->shard) phi->dev->ext = S->phi[0];
 	if (S->extrap && !S->objects)
 		pinc_check(pinc_hip_malloc((void **)&S->phiPrev, S->N[0] * sizeof(double)), "mg extrapolation");
+	if (S->extrap && S->objects && iniHas(ini, "objects:secondGuess")) {
+		char *v = iniGetStr(ini, "objects:secondGuess");
+		if (!strcmp(v, "spectral")) {
+			if (g_pinc.nranks == 1 && !S->shard) S->secondSpectral = 1;
+			else msg(WARNING, "objects:secondGuess = spectral needs one rank: the last correction response instead");
+		} else if (strcmp(v, "response")) msg(ERROR, "objects:secondGuess = %s (spectral | response)", v);
+		free(v);
+	}
+	if (S->secondSpectral) {
+		pinc_check(pinc_hip_malloc((void **)&S->rhoSave, S->N[0] * sizeof(double)), "mg second guess");
+		pinc_check(pinc_hip_malloc((void **)&S->dphi, S->N[0] * sizeof(double)), "mg second guess");
+		pinc_check(pinc_hip_fft_create(&S->fft, S->L[0].nd, S->L[0].T, g_pinc.stream), "mg second guess");
+		pinc_check(pinc_hip_fft_set_symbol(S->fft, 1), "mg second guess");
+	}
 	if (S->extrap && S->objects) {
 		pinc_check(pinc_hip_malloc((void **)&S->phiA, S->N[0] * sizeof(double)), "mg extrapolation");
 		pinc_check(pinc_hip_malloc((void **)&S->phiB, S->N[0] * sizeof(double)), "mg extrapolation");
@@ -220,6 +237,9 @@ void mgFreeSolver(MultigridSolver *S) {
 	pinc_hip_free(S->phiA);
 	pinc_hip_free(S->phiB);
 	pinc_hip_free(S->dCorr);
+	pinc_hip_free(S->rhoSave);
+	pinc_hip_free(S->dphi);
+	pinc_hip_fft_destroy(S->fft);
 	free(S->hist);
 	for (int q = 0; q < S->nLevels; q++) {
 		if (q > 0 || S->shard) {
@@ -255,6 +275,12 @@ static void guess_begin(MultigridSolver *S, int role) {
 	} else if (role == PINC_MG_GUESS_FIRST && S->havePrev >= 2) {
 		/* from the first solutions of the last two steps */
 		pinc_check(pinc_hip_lincomb(phi, S->phiA, 2.0, S->phiB, -1.0, n, g_pinc.stream), "mg extrapolation");
+	} else if (role == PINC_MG_GUESS_SECOND && S->secondSpectral && S->havePrev >= 1) {
+		/* this step's first solution + the exact discrete response to the
+		 * correction charge (rho now minus rho of the first solve) */
+		pinc_check(pinc_hip_lincomb(S->rhoSave, S->rho[0], 1.0, S->rhoSave, -1.0, n, g_pinc.stream), "mg second guess");
+		pinc_check(pinc_hip_fft_poisson(S->fft, S->rhoSave, S->dphi, g_pinc.stream), "mg second guess");
+		pinc_check(pinc_hip_lincomb(phi, phi, 1.0, S->dphi, 1.0, n, g_pinc.stream), "mg second guess");
 	} else if (role == PINC_MG_GUESS_SECOND && S->haveCorr) {
 		/* this step's first solution + the last step's correction response */
 		pinc_check(pinc_hip_lincomb(phi, phi, 1.0, S->dCorr, 1.0, n, g_pinc.stream), "mg extrapolation");
@@ -268,6 +294,8 @@ static void guess_end(MultigridSolver *S, int role) {
 		S->phiB = S->phiA;
 		S->phiA = t;
 		pinc_check(pinc_hip_d2d(S->phiA, S->phi[0], n * sizeof(double), g_pinc.stream), "mg extrapolation");
+		if (S->secondSpectral)
+			pinc_check(pinc_hip_d2d(S->rhoSave, S->rho[0], n * sizeof(double), g_pinc.stream), "mg second guess");
 		if (S->havePrev < 2) S->havePrev++;
 	} else if (role == PINC_MG_GUESS_SECOND && S->havePrev >= 1) {
 		pinc_check(pinc_hip_lincomb(S->dCorr, S->phi[0], 1.0, S->phiA, -1.0, n, g_pinc.stream), "mg extrapolation");

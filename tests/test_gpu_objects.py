@@ -313,12 +313,15 @@ def test_reference_masks_64_green_equals_solve(built, name):
     assert abs(ka - kb) <= 1e-7 * abs(ka) and abs(pa - pb) <= 1e-7 * abs(pa)
 
 
-@pytest.mark.parametrize("fused", [0, 1])
-def test_object_extrapolated_guesses_match_checker(built, fused):
+@pytest.mark.parametrize("fused,second", [(0, "response"), (1, "response"), (0, "spectral"), (1, "spectral")])
+def test_object_extrapolated_guesses_match_checker(built, fused, second):
     """multigrid:extrapolate with an object (native mode, an extension;
     mgGuessNext): the first solve of each step starts
     from the first solutions of the last two steps, the second from this
-    step's first solution plus the last step's correction response; the
+    step's first solution plus the last step's correction response
+    (objects:secondGuess = response) or plus the exact discrete response to
+    this step's correction charge (= spectral: rocFFT with the 7-point
+    symbol on the device, orc_discrete_poisson in the checker); the
     capacitance matrix's solves keep the warm start.  The checker restates
     the same guesses (oracle/orc_native.c): counts exact, energies and phi
     to 1e-7, V-cycles per step within 2."""
@@ -329,7 +332,7 @@ def test_object_extrapolated_guesses_match_checker(built, fused):
     cfg["multigrid"]["native"] = "1"
     cfg["multigrid"]["extrapolate"] = "1"
     cfg["population"]["fused"] = "0"
-    cfg["objects"] = {"sphere": ",".join(map(str, sphere))}
+    cfg["objects"] = {"sphere": ",".join(map(str, sphere)), "secondGuess": second}
     ini = configs.write_ini(cfg)
     cfg["population"]["fused"] = str(fused)
     ini_dev = configs.write_ini(cfg)
