@@ -172,7 +172,7 @@ def main() -> int:
     ap.add_argument("--obj-second-guess", default="spectral", choices=["response", "spectral"],
                     help="objects with --mg-extrapolate: the second solve of a step starts from the first solution "
                          "plus the last step's correction response, or plus the exact discrete response to this "
-                         "step's correction charge (rocFFT; one rank)")
+                         "step's correction charge (rocFFT)")
     ap.add_argument("--obj-capacitance", default="solve", choices=["solve", "green"],
                     help="c5: capacitance matrix by one solve per surface node (the reference's, default) or "
                          "by translating one periodic response (objects:capacitance = green)")

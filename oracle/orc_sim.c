@@ -249,7 +249,7 @@ OWorld *ow_create(OIni *ini, int literal){
 		/* multigrid:extrapolate, as pinc_mg.c */
 		on_set_extrapolate(w->native, oini_has(ini, "multigrid:extrapolate") && oini_int(ini, "multigrid:extrapolate"),
 		                   oini_has(ini, "objects:sphere") || oini_has(ini, "objects:file"));
-		if(oini_has(ini, "objects:secondGuess") && w->P == 1){
+		if(oini_has(ini, "objects:secondGuess")){
 			on_set_second_spectral(w->native, !strcmp(oini_raw(ini, "objects:secondGuess"), "spectral"));
 		}
 	}

@@ -208,9 +208,11 @@ MultigridSolver *mgAllocSolver(const dictionary *ini, Grid *rho, Grid *phi) {
 		pinc_check(pinc_hip_malloc((void **)&S->phiPrev, S->N[0] * sizeof(double)), "mg extrapolation");
 	if (S->extrap && S->objects && iniHas(ini, "objects:secondGuess")) {
 		char *v = iniGetStr(ini, "objects:secondGuess");
+		/* (objects: the solve is replicated, rho[0] and phi[0] global on
+		 * every rank, rho[0] gathered before guess_begin) */
 		if (!strcmp(v, "spectral")) {
-			if (g_pinc.nranks == 1 && !S->shard) S->secondSpectral = 1;
-			else msg(WARNING, "objects:secondGuess = spectral needs one rank: the last correction response instead");
+			if (!S->shard) S->secondSpectral = 1;
+			else msg(WARNING, "objects:secondGuess = spectral needs the replicated solve: the last correction response instead");
 		} else if (strcmp(v, "response")) msg(ERROR, "objects:secondGuess = %s (spectral | response)", v);
 		free(v);
 	}

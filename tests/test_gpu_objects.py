@@ -115,8 +115,9 @@ def test_object_mask_file_equals_sphere(built, tmp_path):
         assert abs(a - b) <= 1e-10 * abs(a)
 
 
-@pytest.mark.parametrize("capacitance,fused", [("solve", 0), ("green", 0), ("solve", 1)])
-def test_object_two_slabs_match_one(built, tmp_path, capacitance, fused):
+@pytest.mark.parametrize("capacitance,fused,guess", [("solve", 0, None), ("green", 0, None), ("solve", 1, None),
+                                                     ("solve", 1, "spectral")])
+def test_object_two_slabs_match_one(built, tmp_path, capacitance, fused, guess):
     """Two z-slabs (host transport, one GPU): the object's lookups are
     global, phi is read from the replicated solve's global view, charge
     corrections land in the owning slab and the collected charge is summed
@@ -124,7 +125,9 @@ def test_object_two_slabs_match_one(built, tmp_path, capacitance, fused):
     unit charge of the translated response sits on the rank holding global
     node (0,0,0) and the response is read from the replicated potential.
     fused: the push collects the particles that stay, the flag pass the
-    immigrants (the sphere straddles the slab boundary)."""
+    immigrants (the sphere straddles the slab boundary).  spectral: native
+    multigrid with the extrapolated guesses and the spectral second guess
+    (every rank transforms the gathered global rho)."""
     import json
     import os
     import socket
@@ -134,13 +137,17 @@ def test_object_two_slabs_match_one(built, tmp_path, capacitance, fused):
     from pinc_amd import Sim
     root = Path(__file__).resolve().parent.parent
     sphere = "8.2,7.7,8.4,3.3"   # straddles the slab boundary at z = 8
-    steps = 3
+    steps = 4 if guess else 3
 
     def cfg(nsub, T):
         c = configs.config("cold3d", true_size=T, nsub=nsub)
         c["multigrid"]["mgLevels"] = "3"
         c["population"]["fused"] = str(fused)
         c["objects"] = {"sphere": sphere, "capacitance": capacitance}
+        if guess:
+            c["multigrid"]["native"] = "1"
+            c["multigrid"]["extrapolate"] = "1"
+            c["objects"]["secondGuess"] = guess
         return configs.write_ini(c)
 
     one = {"energy": [], "counts": []}
