@@ -153,8 +153,9 @@ def main() -> int:
                          "c2: input/langmuir2D.ini at 128^2, 32 ppc (Langmuir perturbation, cold), multigrid")
     ap.add_argument("--size", type=int, default=None, help="global cells per dimension (c4: 256, c3: 128)")
     ap.add_argument("--ppc", type=int, default=None, help="particles per cell per species (c4: 64, c3: 32)")
-    ap.add_argument("--mg-graph", type=int, default=0,
-                    help="1: native multigrid replays each V-cycle as a captured HIP graph (multigrid:graph)")
+    ap.add_argument("--mg-graph", type=int, default=None,
+                    help="1: native multigrid replays each V-cycle as a captured HIP graph (multigrid:graph); "
+                         "default 1 for the launch-bound C2, 0 elsewhere (neutral at C4)")
     ap.add_argument("--mg-extrapolate", type=int, default=1,
                     help="1: native multigrid starts each solve from 2 phi_n - phi_(n-1) instead of phi_n "
                          "(multigrid:extrapolate; with an object, the two solves of a step from their own histories)")
@@ -262,6 +263,8 @@ def main() -> int:
         cfg["multigrid"]["native"] = "1"
         cfg["multigrid"]["shard"] = args.mg_shard
         cfg["multigrid"]["extrapolate"] = str(args.mg_extrapolate)
+        if args.mg_graph is None:
+            args.mg_graph = 1 if c2 else 0
         cfg["multigrid"]["graph"] = str(args.mg_graph)
     if c5:
         # a generated sphere (the reference's bepiColombo object file is not
