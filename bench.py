@@ -76,7 +76,7 @@ def _cpu_threads() -> int:
 
 
 def _cpu_baseline(size: int, ppc: int, steps: int, native: bool, workload: str = "c4",
-                  extrapolate: int = 0) -> dict:
+                  extrapolate: int = 0, spectral_coarse: int = 0) -> dict:
     """The oracle (plain-C restatement of the reference) on the host cores,
     on a bounded sample of the same workload: the warm plasma at size^3 with
     ppc particles per cell per species, decomposed into one z-slab per
@@ -106,6 +106,7 @@ def _cpu_baseline(size: int, ppc: int, steps: int, native: bool, workload: str =
     if native and cfg["methods"]["poisson"] == "mgSolver":
         cfg["multigrid"]["native"] = "1"
         cfg["multigrid"]["extrapolate"] = str(extrapolate)
+        cfg["multigrid"]["spectralCoarse"] = str(spectral_coarse)
     ini = configs.write_ini(cfg)
     t_init = time.perf_counter()
     w = orc.World(ini)
@@ -132,6 +133,9 @@ def _cpu_baseline(size: int, ppc: int, steps: int, native: bool, workload: str =
                       + ("spectral solve (naive DFT restatement)" if cfg["methods"]["poisson"] == "sSolver" else
                          "multigrid " + ("native mode as the GPU line" + (" (extrapolated initial guess)"
                                                                            if extrapolate else "")
+                                         + (" (level 1 solved exactly by DFT)" if spectral_coarse else
+                                            " (levels below 0 as the V-cycle: the GPU line solves level 1 "
+                                            "exactly by FFT, same cycle count)" if native else "")
                                          if native else "reference algorithm")
                          + f", {levels} levels, {cyc:.0f} V-cycles/solve"),
             "seconds": dt, "init_s": t_init,
@@ -156,6 +160,9 @@ def main() -> int:
     ap.add_argument("--mg-graph", type=int, default=None,
                     help="1: native multigrid replays each V-cycle as a captured HIP graph (multigrid:graph); "
                          "default 1 for the launch-bound C2, 0 elsewhere (neutral at C4)")
+    ap.add_argument("--mg-spectral-coarse", type=int, default=1,
+                    help="1: native multigrid solves level 1's correction exactly by FFT (multigrid:spectralCoarse) "
+                         "instead of recursing to the coarser levels")
     ap.add_argument("--mg-extrapolate", type=int, default=1,
                     help="1: native multigrid starts each solve from 2 phi_n - phi_(n-1) instead of phi_n "
                          "(multigrid:extrapolate; with an object, the two solves of a step from their own histories)")
@@ -263,6 +270,7 @@ def main() -> int:
         cfg["multigrid"]["native"] = "1"
         cfg["multigrid"]["shard"] = args.mg_shard
         cfg["multigrid"]["extrapolate"] = str(args.mg_extrapolate)
+        cfg["multigrid"]["spectralCoarse"] = str(args.mg_spectral_coarse)
         if args.mg_graph is None:
             args.mg_graph = 1 if c2 else 0
         cfg["multigrid"]["graph"] = str(args.mg_graph)
@@ -399,14 +407,18 @@ def main() -> int:
                                       f"their cell, at most {args.sort_max} steps apart)" if args.sort_fraction > 0 else
                                       f" (tile sort every {args.sort_interval} steps)") if args.layout == "tiled" else ""),
             "poisson": ("spectral (sSolver, rocFFT r2c/c2r, global grid)" if c3 else
-                        f"multigrid mgVRecursive, {mg_levels} levels ({S}^{nd} down to {S >> (mg_levels - 1)}^{nd}), "
-                        "RB Gauss-Seidel 10/10/10, "
+                        (f"multigrid mgVRecursive, 2 levels used ({S}^{nd}, {S // 2}^{nd} solved exactly), "
+                         if args.mg == "native" and args.mg_spectral_coarse else
+                         f"multigrid mgVRecursive, {mg_levels} levels ({S}^{nd} down to {S >> (mg_levels - 1)}^{nd}), ")
+                        + "RB Gauss-Seidel 10/10/10, "
                         + ("native mode (correction scheme, coarse h^2 factor; the ini's 5 levels extended"
                            + (("; initial guesses extrapolated: the first solve of a step from the last two "
                                "steps' first solutions, the second from the first + "
                                + ("the exact discrete response to the correction charge (rocFFT)"
                                   if args.obj_second_guess == "spectral" else "the last correction response")
                                if c5 else "; initial guess 2 phi_n - phi_(n-1)") if args.mg_extrapolate else "")
+                           + ("; two-grid: the level-1 correction solved exactly by rocFFT with the 7-point symbol"
+                              if args.mg_spectral_coarse else "")
                            + "; RMS residual <= 1e-10 as the reference)"
                            if args.mg == "native" else "reference algorithm (parity mode)")
                         + (f", level 0 sharded over the slabs ({mg_halo} halo planes per side), levels >= 1 "
@@ -454,7 +466,10 @@ def main() -> int:
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = _cpu_baseline(S if c2 else args.cpu_size, args.ppc, args.cpu_steps,
                                                args.mg == "native", args.workload if args.workload != "c5" else "c4",
-                                               args.mg_extrapolate)
+                                               # the oracle's exact coarse solve is a naive DFT (no FFT
+                                               # library here): the CPU keeps the V-cycle below level 1,
+                                               # which converges in as many cycles and is faster there
+                                               args.mg_extrapolate, 0)
     if rank == 0:
         print(json.dumps(result), file=out, flush=True)
     if dist is not None:

@@ -204,6 +204,7 @@ void on_free(ONative *S);
 #define ON_GUESS_SECOND 3
 void on_set_extrapolate(ONative *S, int on, int objects);
 void on_set_second_spectral(ONative *S, int on);
+void on_set_spectral_coarse(ONative *S, int on);
 void orc_discrete_poisson(int nd, const int *L, const double *rho, double *phi);
 void on_guess_next(ONative *S, int role);
 int on_levels(const ONative *S);

@@ -323,11 +323,15 @@ static void dft_axis(double *re, double *im, const int *L, int axis, int sign){
 	long outer = 1;
 	for(int d = 0; d < 3; d++) if(d != axis) outer *= L[d];
 	double *cr = malloc(n*sizeof(double)), *ci = malloc(n*sizeof(double));
-	double *tr = malloc(n*sizeof(double)), *ti = malloc(n*sizeof(double));
 	for(int k = 0; k < n; k++){
 		cr[k] = cos(2.0*M_PI*k/n);
 		ci[k] = sign*sin(2.0*M_PI*k/n);
 	}
+	/* lines are independent: OpenMP over them, bit-identical for any count */
+	#pragma omp parallel
+	{
+	double *tr = malloc(n*sizeof(double)), *ti = malloc(n*sizeof(double));
+	#pragma omp for schedule(static)
 	for(long o = 0; o < outer; o++){
 		/* base index of the line: decompose o over the other axes */
 		long base = 0, r = o, s = 1;
@@ -349,7 +353,9 @@ static void dft_axis(double *re, double *im, const int *L, int axis, int sign){
 		}
 		for(int k = 0; k < n; k++){ re[base + k*stride] = tr[k]; im[base + k*stride] = ti[k]; }
 	}
-	free(cr); free(ci); free(tr); free(ti);
+	free(tr); free(ti);
+	}
+	free(cr); free(ci);
 }
 
 /* phi = the exact solution of the multigrid's discrete Poisson problem

@@ -49,6 +49,7 @@ struct ONative {
 	 * discrete response to the correction charge (orc_discrete_poisson) */
 	int secondSpectral;
 	double *rhoSave, *dphi;
+	int spectralCoarse;  /* multigrid:spectralCoarse */
 };
 
 static NLv mklv(int nd, const int *T){
@@ -96,6 +97,8 @@ void on_set_extrapolate(ONative *S, int on, int objects){
 }
 
 void on_guess_next(ONative *S, int role){ if(S->objects) S->role = role; }
+
+void on_set_spectral_coarse(ONative *S, int on){ S->spectralCoarse = on && S->nLevels >= 2; }
 
 void on_set_second_spectral(ONative *S, int on){
 	S->secondSpectral = on && S->extrap && S->objects;
@@ -241,6 +244,13 @@ static void neutralize(double *a, long N){
 
 static void vrec(ONative *S, OWorld *w, int q){
 	int bottom = S->nLevels - 1;
+	if(S->spectralCoarse && q == 1){
+		/* multigrid:spectralCoarse: the level-1 correction solved exactly
+		 * (pinc_mg.c vrec, rocFFT with the 7-point symbol on the device) */
+		orc_discrete_poisson(S->L[1].nd, S->L[1].T, S->rho[1], S->phi[1]);
+		prolong_add(S, 0);
+		return;
+	}
 	int pre = w->preSmooth == ORC_SMOOTH_GS3D, post = w->postSmooth == ORC_SMOOTH_GS3D;
 	int coarse = w->coarseSolv == ORC_SMOOTH_GS3D;
 	if(q > 0) memset(S->phi[q], 0, S->L[q].N*sizeof(double));

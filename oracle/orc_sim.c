@@ -249,6 +249,8 @@ OWorld *ow_create(OIni *ini, int literal){
 		/* multigrid:extrapolate, as pinc_mg.c */
 		on_set_extrapolate(w->native, oini_has(ini, "multigrid:extrapolate") && oini_int(ini, "multigrid:extrapolate"),
 		                   oini_has(ini, "objects:sphere") || oini_has(ini, "objects:file"));
+		on_set_spectral_coarse(w->native, oini_has(ini, "multigrid:spectralCoarse") &&
+		                                  oini_int(ini, "multigrid:spectralCoarse"));
 		if(oini_has(ini, "objects:secondGuess")){
 			on_set_second_spectral(w->native, !strcmp(oini_raw(ini, "objects:secondGuess"), "spectral"));
 		}

@@ -185,6 +185,9 @@ struct MultigridSolver {
 	int secondSpectral;
 	double *rhoSave, *dphi;
 	pinc_fft_t *fft;
+	/* multigrid:spectralCoarse (native mode): level 1's correction solved
+	 * exactly (rocFFT, the 7-point symbol) instead of by the levels below */
+	pinc_fft_t *fftCoarse;
 	/* sharded level 0 (native mode, multigrid:shard):
 	 * rho[0]/phi[0]/res[0] are this rank's z-slab with hz halo planes on
 	 * each side (L[0], N[0] = that extended slab), levels >= 1 global */

@@ -216,6 +216,11 @@ MultigridSolver *mgAllocSolver(const dictionary *ini, Grid *rho, Grid *phi) {
 		} else if (strcmp(v, "response")) msg(ERROR, "objects:secondGuess = %s (spectral | response)", v);
 		free(v);
 	}
+	if (S->native && S->nLevels >= 2 && iniHas(ini, "multigrid:spectralCoarse") &&
+	    iniGetInt(ini, "multigrid:spectralCoarse")) {
+		pinc_check(pinc_hip_fft_create(&S->fftCoarse, S->L[1].nd, S->L[1].T, g_pinc.stream), "mg spectral coarse");
+		pinc_check(pinc_hip_fft_set_symbol(S->fftCoarse, 1), "mg spectral coarse");
+	}
 	if (S->secondSpectral) {
 		pinc_check(pinc_hip_malloc((void **)&S->rhoSave, S->N[0] * sizeof(double)), "mg second guess");
 		pinc_check(pinc_hip_malloc((void **)&S->dphi, S->N[0] * sizeof(double)), "mg second guess");
@@ -242,6 +247,7 @@ void mgFreeSolver(MultigridSolver *S) {
 	pinc_hip_free(S->rhoSave);
 	pinc_hip_free(S->dphi);
 	pinc_hip_fft_destroy(S->fft);
+	pinc_hip_fft_destroy(S->fftCoarse);
 	free(S->hist);
 	for (int q = 0; q < S->nLevels; q++) {
 		if (q > 0 || S->shard) {
@@ -474,6 +480,14 @@ static int coarse_start(const MultigridSolver *S) {
 
 static void vrec(MultigridSolver *S, int q) {
 	int bottom = S->nLevels - 1;
+	if (S->fftCoarse && q == 1) {
+		/* two-grid cycle with an exact coarse solve: the level-1 correction
+		 * equation -L phi1 = rho1 (rho1 the restricted residual, times 4)
+		 * solved by FFT with the 7-point symbol; DC dropped (neutral) */
+		pinc_check(pinc_hip_fft_poisson(S->fftCoarse, S->rho[1], S->phi[1], g_pinc.stream), "mg spectral coarse");
+		prolong_into(S, 0);
+		return;
+	}
 	int qc = coarse_start(S);
 	if (qc > 0 && q == qc) {
 		pinc_check(pinc_hip_mg_coarse(S->rho[q], S->phi[q], S->nLevels - q, &S->L[q], S->nPre, S->nPost, S->nCoarse,

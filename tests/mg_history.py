@@ -42,7 +42,7 @@ def make_rho(size: int, seed: int, amp: float) -> np.ndarray:
 
 
 def ini_for(size: int, levels: int, native: bool, nranks: int = 1, shard: str | None = None,
-            spectral: bool = False) -> str:
+            spectral: bool = False, spectral_coarse: bool = False) -> str:
     from pinc_amd import configs
     cfg = configs.config("warm", true_size=(size, size, size // nranks), nsub=(1, 1, nranks), ppc=1, nalloc_pc=2,
                          levels=levels)
@@ -52,6 +52,8 @@ def ini_for(size: int, levels: int, native: bool, nranks: int = 1, shard: str | 
         cfg["multigrid"]["shard"] = shard
     if spectral:
         cfg["methods"]["poisson"] = "sSolver"
+    if spectral_coarse:
+        cfg["multigrid"]["spectralCoarse"] = "1"
     return configs.write_ini(cfg)
 
 
@@ -63,10 +65,10 @@ def rank_slab(rho: np.ndarray, rank: int, nranks: int) -> np.ndarray:
 
 
 def run(side: str, size: int, levels: int, cycles: int, seed: int, amp: float, native: bool = False,
-        solves: int = 1, shard: str | None = None) -> dict:
+        solves: int = 1, shard: str | None = None, spectral_coarse: bool = False) -> dict:
     rho = make_rho(size, seed, amp)
     digest = hashlib.sha256(rho.tobytes()).hexdigest()
-    ini = ini_for(size, levels, native, shard=shard)
+    ini = ini_for(size, levels, native, shard=shard, spectral_coarse=spectral_coarse)
     halo = 0
     t0 = time.perf_counter()
     hists = []

@@ -127,18 +127,21 @@ def test_nd_solve_matches_oracle(name, native):
     assert np.max(np.abs(pg - po)) <= 1e-9 * np.max(np.abs(po))
 
 
-@pytest.mark.parametrize("layout", ["reference", "tiled"])
-def test_extrapolated_guess_matches_oracle(layout):
+@pytest.mark.parametrize("layout,coarse", [("reference", 0), ("tiled", 0), ("reference", 1), ("tiled", 1)])
+def test_extrapolated_guess_matches_oracle(layout, coarse):
     """multigrid:extrapolate (native mode, an extension: each solve starts
     from 2 phi_n - phi_(n-1) instead of phi_n, pinc_hip_extrapolate) on a
     warm 32^3 plasma: the device follows the oracle's restatement
     (oracle/orc_native.c) step by step -- energies to 1e-8, the V-cycle
     count per solve +-1 -- and needs no more cycles in total than the plain
-    warm start of the same run."""
+    warm start of the same run.  coarse = 1: multigrid:spectralCoarse, the
+    level-1 correction solved exactly (rocFFT with the 7-point symbol; the
+    oracle's orc_discrete_poisson) -- a two-grid cycle."""
     import orc
     from pinc_amd import Sim, configs
     cfg = configs.config("warm", true_size=(32, 32, 32), ppc=8, nalloc_pc=16, levels=3)
     cfg["multigrid"]["native"] = "1"
+    cfg["multigrid"]["spectralCoarse"] = str(coarse)
     ini_plain = configs.write_ini(cfg)
     cfg["multigrid"]["extrapolate"] = "1"
     ini_o = configs.write_ini(cfg)

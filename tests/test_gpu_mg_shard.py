@@ -59,6 +59,20 @@ def test_one_rank_shard_matches_native_oracle(size):
     assert np.max(np.abs(g["phi"] - o["phi"])) <= 1e-9 * np.max(np.abs(o["phi"]))
 
 
+@pytest.mark.parametrize("shard", ["1", "0"])
+def test_spectral_coarse_matches_native_oracle(shard):
+    """multigrid:spectralCoarse at 128^3 (the level-1 correction solved
+    exactly by rocFFT with the 7-point symbol; a two-grid cycle), on the
+    sharded extended slab (shard forced, one rank) and replicated, against
+    the oracle's restatement (orc_discrete_poisson): residual history per
+    cycle, phi to 1e-9 of its maximum."""
+    g = mg_history.run("gpu", 128, 5, 200, 20261016, 1.0, native=True, shard=shard, spectral_coarse=True)
+    o = mg_history.run("oracle", 128, 5, 200, 20261016, 1.0, native=True, spectral_coarse=True)
+    assert g["residual"][-1][-1] <= 1e-10 and o["residual"][-1][-1] <= 1e-10
+    _check_hist(g["residual"][-1], o["residual"][-1])
+    assert np.max(np.abs(g["phi"] - o["phi"])) <= 1e-9 * np.max(np.abs(o["phi"]))
+
+
 def _two_ranks(size, levels, tmp_path, fused_min=None, cycles=60, solves=2, world=2):
     out = tmp_path / "shard"
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2")

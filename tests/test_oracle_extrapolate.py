@@ -106,3 +106,24 @@ def test_object_guesses_same_run(second):
         assert sum(c1[1:]) <= sum(c0[1:]) - (len(c0) - 1), (c0, c1)
     for a, b in zip(e0, e1):
         assert abs(a - b) <= 1e-7 * abs(a)
+
+
+def test_spectral_coarse_same_run():
+    """multigrid:spectralCoarse (the level-1 correction solved exactly by
+    orc_discrete_poisson, a two-grid cycle): the same energies as the full
+    V-cycle to the solver tolerance, with no more V-cycles per solve."""
+    runs = {}
+    for sc in ("0", "1"):
+        cfg = configs.config("warm", true_size=(32, 32, 32), ppc=8, nalloc_pc=16, levels=3)
+        cfg["multigrid"]["native"] = "1"
+        cfg["multigrid"]["extrapolate"] = "1"
+        cfg["multigrid"]["spectralCoarse"] = sc
+        w = orc.World(configs.write_ini(cfg))
+        w.init(perturb=False, maxwell=True, seed=5)
+        w.init_fields()
+        runs[sc] = (_cycles_per_step(w, w.step, 6), w.energy())
+        w.close()
+    (c0, e0), (c1, e1) = runs["0"], runs["1"]
+    assert all(b <= a for a, b in zip(c0, c1)), (c0, c1)
+    for a, b in zip(e0, e1):
+        assert abs(a - b) <= 1e-9 * abs(a)
