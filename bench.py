@@ -134,7 +134,7 @@ def _cpu_baseline(size: int, ppc: int, steps: int, native: bool, workload: str =
                          "multigrid " + ("native mode as the GPU line" + (" (extrapolated initial guess)"
                                                                            if extrapolate else "")
                                          + (" (level 1 solved exactly by DFT)" if spectral_coarse else
-                                            " (levels below 0 as the V-cycle: the GPU line solves level 1 "
+                                            " (levels >= 1 recursively as a V-cycle: the GPU line solves level 1 "
                                             "exactly by FFT, same cycle count)" if native else "")
                                          if native else "reference algorithm")
                          + f", {levels} levels, {cyc:.0f} V-cycles/solve"),
