@@ -47,36 +47,62 @@ ROCPROF_NAMES = {
 }
 
 
-def _pmc_traffic(prefix: str):
+def _pmc_traffic(prefix: str, key: dict):
     """HBM bytes per launch of the kernels whose rocprof name starts with
-    `prefix`, from the newest profiles/*_hbm_traffic.json (rocprofv3 --pmc
-    FETCH_SIZE / WRITE_SIZE passes of this same bench command, summarised by
-    tools/pmc_summary.py), launch-weighted over the kernel's variants; None
-    if no profile covers it."""
+    `prefix`, from the newest profiles/*_hbm_traffic.json whose "config"
+    (written by tools/pmc_summary.py from the profiled bench line) is this
+    run's configuration `key` (workload, grid, ppc, GPU count, layout),
+    launch-weighted over the kernel's variants; None if no profile of this
+    configuration covers it."""
     files = sorted((ROOT / "profiles").glob("*_hbm_traffic.json"))
     for f in reversed(files):
         try:
-            ks = json.loads(f.read_text())["kernels"]
+            d = json.loads(f.read_text())
+            ks = d["kernels"]
         except (OSError, ValueError, KeyError):
+            continue
+        if d.get("config") != key:
             continue
         sel = [k for k in ks if k["name"].startswith(prefix) and k.get("traffic_bytes_per_launch_mean")
                and k["grid_size"] >= 1 << 20]
         if sel:
             n = sum(k["launches"] for k in sel)
             t = sum(k["traffic_bytes_per_launch_mean"] * k["launches"] for k in sel) / n
-            return {"bytes_per_launch": t, "source": f.name, "launches": n}
+            return {"bytes_per_launch": t, "source": f.name, "launches": n,
+                    "fetch_correction": sel[0].get("fetch_correction"), "calibration": d.get("calibration")}
     return None
 
 
-def _cpu_threads() -> int:
-    """Host threads the CPU baseline uses: the job's CPU share (the GPU box
-    sets OMP_NUM_THREADS to it), at most the CPUs this process may run on."""
+def _host_cpus() -> dict:
+    """The host CPUs this process owns: its affinity set, capped by the
+    cgroup's CPU quota where one is set (cpu.max: a box may pin a job to
+    many CPUs but grant it the time of fewer).  PINC_CPU_THREADS overrides."""
     aff = len(os.sched_getaffinity(0))
-    return max(1, min(aff, int(os.environ.get("OMP_NUM_THREADS", aff))))
+    quota = None
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    threads = aff if quota is None else max(1, min(aff, int(quota + 0.5)))
+    if os.environ.get("PINC_CPU_THREADS"):
+        threads = max(1, int(os.environ["PINC_CPU_THREADS"]))
+    return {"threads": threads, "affinity": aff, "cgroup_quota_cpus": quota, "nproc": os.cpu_count()}
+
+
+def _mem_available() -> int:
+    try:
+        for line in Path("/proc/meminfo").read_text().splitlines():
+            if line.startswith("MemAvailable:"):
+                return int(line.split()[1]) * 1024
+    except OSError:
+        pass
+    return 0
 
 
 def _cpu_baseline(size: int, ppc: int, steps: int, native: bool, workload: str = "c4",
-                  extrapolate: int = 0, spectral_coarse: int = 0) -> dict:
+                  extrapolate: int = 0, spectral_coarse: int = 0, size_note: str = "") -> dict:
     """The oracle (plain-C restatement of the reference) on the host cores,
     on a bounded sample of the same workload: the warm plasma at size^3 with
     ppc particles per cell per species, decomposed into one z-slab per
@@ -87,7 +113,8 @@ def _cpu_baseline(size: int, ppc: int, steps: int, native: bool, workload: str =
     sys.path.insert(0, str(ROOT / "oracle"))
     import orc  # test/baseline infrastructure only
     from pinc_amd import configs
-    threads = _cpu_threads()
+    cpus = _host_cpus()
+    threads = cpus["threads"]
     nsub = threads
     while nsub > 1 and (size % nsub or (size // nsub) % 2):
         nsub -= 1
@@ -101,7 +128,7 @@ def _cpu_baseline(size: int, ppc: int, steps: int, native: bool, workload: str =
         cfg["population"]["nAlloc"] = f"{ppc + 16} pc"
         cfg["multigrid"]["mgLevels"] = "1" if native else cfg["multigrid"]["mgLevels"]
     else:
-        cfg = configs.config("c3" if workload == "c3" else "warm", true_size=(size, size, size // nsub),
+        cfg = configs.config({"c3": "c3", "c4ts": "c4ts"}.get(workload, "warm"), true_size=(size, size, size // nsub),
                              nsub=(1, 1, nsub), ppc=ppc, nalloc_pc=ppc + 8, levels=1 if native else 5)
     if native and cfg["methods"]["poisson"] == "mgSolver":
         cfg["multigrid"]["native"] = "1"
@@ -113,7 +140,8 @@ def _cpu_baseline(size: int, ppc: int, steps: int, native: bool, workload: str =
     w.init(perturb=workload == "c2", maxwell=workload != "c2", seed=20260101)
     w.init_fields()
     t_init = time.perf_counter() - t_init
-    n = sum(w.count(s, rank=r) for r in range(w.nranks) for s in range(2))
+    ns = int(cfg["population"]["nSpecies"])
+    n = sum(w.count(s, rank=r) for r in range(w.nranks) for s in range(ns))
     c0 = w.cycles
     ph0 = w.timers()
     t0 = time.perf_counter()
@@ -126,10 +154,10 @@ def _cpu_baseline(size: int, ppc: int, steps: int, native: bool, workload: str =
     os.unlink(ini)
     push_ms = ph["move"] + ph["migrate"] + ph["deposit"] + ph["accelerate"]
     return {"value": n * steps / dt, "unit": "particle-updates/s", "cores": threads, "kind": "port",
-            "nproc": os.cpu_count(), "cpu_share": len(os.sched_getaffinity(0)),
+            "nproc": cpus["nproc"], "cpu_affinity": cpus["affinity"], "cgroup_quota_cpus": cpus["cgroup_quota_cpus"],
             "sample": f"oracle (C restatement of the reference, OpenMP over {nsub} emulated slab ranks, "
-                      f"{threads} threads) on the same {workload.upper()} workload at {size}^{nd}, {ppc} ppc x 2 "
-                      f"species ({n} particles), {steps} steps; "
+                      f"{threads} threads = the CPUs this process owns) on the same {workload.upper()} workload at "
+                      f"{size}^{nd}{size_note}, {ppc} ppc x {ns} species ({n} particles), {steps} steps; "
                       + ("spectral solve (naive DFT restatement)" if cfg["methods"]["poisson"] == "sSolver" else
                          "multigrid " + ("native mode as the GPU line" + (" (extrapolated initial guess)"
                                                                            if extrapolate else "")
@@ -138,6 +166,9 @@ def _cpu_baseline(size: int, ppc: int, steps: int, native: bool, workload: str =
                                             "exactly by FFT, same cycle count)" if native else "")
                                          if native else "reference algorithm")
                          + f", {levels} levels, {cyc:.0f} V-cycles/solve"),
+            "algorithm_note": "the CPU and GPU lines run the same discretisation and stopping rule; the GPU line's "
+                              "solver extensions (exact level-1 solve by FFT, spectral second guess with objects) "
+                              "have no FFT library on the CPU side, so value ratios compare algorithm + hardware",
             "seconds": dt, "init_s": t_init,
             "push_deposit_updates_per_s": n / (push_ms * 1e-3) if push_ms > 0 else None,
             "poisson_ms_per_step": ph["solve"], "mg_cycles_per_solve": cyc,
@@ -149,8 +180,10 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="c4", choices=["c4", "c3", "c5", "c2"],
+    ap.add_argument("--workload", default="c4", choices=["c4", "c3", "c5", "c2", "c4ts"],
                     help="c4: warm 3-D plasma, 256^3, 64 ppc, multigrid (BASELINE.json metric, default); "
+                         "c4ts: C4's two-stream variant (two electron beams, drift +-0.1 cells/step per component, "
+                         "plus ions, 43 ppc per species); "
                          "c3: Maxwellian 128^3, 32 ppc, spectral (rocFFT) Poisson solve; "
                          "c5: c4 plus an immersed sphere (object.c: charge collection in the fused push, "
                          "capacitance correction, second solve); "
@@ -195,8 +228,9 @@ def main() -> int:
     ap.add_argument("--sort-in-push", type=int, default=1,
                     help="1: the tile sort rides in every sort-interval-th push (default); 0: separate sort pass")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-size", type=int, default=128)
-    ap.add_argument("--cpu-steps", type=int, default=20)
+    ap.add_argument("--cpu-size", type=int, default=None,
+                    help="CPU baseline grid (default: the GPU line's, if the host has the memory, else 128)")
+    ap.add_argument("--cpu-steps", type=int, default=None, help="CPU baseline steps (default 3 at 256^3, 20 below)")
     ap.add_argument("--host-transport", action="store_true",
                     help="rehearsal only: N ranks share GPU 0 and the collectives go through the gloo host "
                          "transport (RCCL refuses two ranks on one device); never the measured configuration")
@@ -248,10 +282,11 @@ def main() -> int:
     c3 = args.workload == "c3"
     c5 = args.workload == "c5"
     c2 = args.workload == "c2"
+    ts = args.workload == "c4ts"
     if args.size is None:
         args.size = 128 if (c3 or c2) else 256
     if args.ppc is None:
-        args.ppc = 32 if (c3 or c2) else 64
+        args.ppc = 32 if (c3 or c2) else 43 if ts else 64
     S = args.size
     nd = 2 if c2 else 3
     if S % world:
@@ -264,8 +299,9 @@ def main() -> int:
         cfg["population"]["nParticles"] = f"{args.ppc} pc"
         cfg["population"]["nAlloc"] = f"{args.ppc + 16} pc"
     else:
-        cfg = configs.config("c3" if c3 else "warm", true_size=(S, S, S // world), nsub=(1, 1, world), ppc=args.ppc,
-                             nalloc_pc=args.ppc + 8)
+        cfg = configs.config("c3" if c3 else "c4ts" if ts else "warm", true_size=(S, S, S // world),
+                             nsub=(1, 1, world), ppc=args.ppc, nalloc_pc=args.ppc + 8)
+    nspecies = int(cfg["population"]["nSpecies"])
     if args.mg == "native":
         cfg["multigrid"]["native"] = "1"
         cfg["multigrid"]["shard"] = args.mg_shard
@@ -362,8 +398,13 @@ def main() -> int:
     if args.mg == "native":
         # two red-black iterations per launch (24 B per point: phi R+W, rho R)
         ROCPROF_NAMES["gs_pass"] = "k_gs_sweep4c<32, 8, 256>"
+    sub = {}
     for k, p in probes.items():
         if p["samples"] == 0 or p["mean_ms"] <= 0:
+            continue
+        if k in _lib.SUB_PROBES:
+            sub[k] = {"mean_launch_ms": p["mean_ms"], "launches": p["launches"], "samples": p["samples"],
+                      "achieved_GBs": p["mean_bytes"] / (p["mean_ms"] * 1e-3) / 1e9}
             continue
         gbs = p["mean_bytes"] / (p["mean_ms"] * 1e-3) / 1e9
         kernels[k] = {"rocprof_name": ROCPROF_NAMES[k], "mean_launch_ms": p["mean_ms"],
@@ -375,6 +416,13 @@ def main() -> int:
     # push+deposit against SURVEY.md 8(d): 144 B per particle-update (3-D)
     # 144 B per 3-D particle-update (96 B in 2-D) + 32 B per cell
     pd_bytes = (96.0 if c2 else 144.0) * n_local + 32.0 * S ** nd / world
+    if "push_plain" in sub:
+        for k in ("push_count", "push_sort"):
+            if k in sub:
+                sub[k]["vs_plain"] = sub[k]["mean_launch_ms"] / sub["push_plain"]["mean_launch_ms"]
+    # configuration key of the PMC traffic profiles (tools/pmc_summary.py)
+    traffic_key = {"workload": args.workload, "grid": [S] * nd, "ppc_per_species": args.ppc, "n_gpus": world,
+                   "layout": args.layout}
     pd_gbs = pd_bytes / (push_ms * 1e-3) / 1e9 if push_ms > 0 else 0.0
 
     result = {
@@ -395,12 +443,13 @@ def main() -> int:
                          f"species ({n_total} particles), 1D slab decomposition 1,{world}" if c2 else
                          ("C3 Maxwellian 3-D two-species plasma" if c3 else
                           f"C5 warm 3-D two-species plasma around an immersed sphere (radius {S / 32:g} cells)"
-                          if c5 else "C4 warm 3-D two-species plasma")
+                          if c5 else "C4 two-stream variant: two electron beams (drift +-0.1 cells/step on every "
+                          "component, population.c:385) and ions" if ts else "C4 warm 3-D two-species plasma")
                          + f", {S}^3 grid, {args.ppc} ppc per species "
                          f"({n_total} particles), 1D slab decomposition 1,1,{world}"),
             "grid": [S] * nd,
             "ppc_per_species": args.ppc,
-            "species": 2,
+            "species": nspecies,
             "particles": n_total,
             "decomposition": f"1,{world}" if c2 else f"1,1,{world}",
             "layout": args.layout + ((f" (per-species tile sort once {args.sort_fraction:g} of the particles left "
@@ -443,8 +492,9 @@ def main() -> int:
             "unit": "GB/s",
             "frac": dk["frac"],
             "traffic": None,
-            "traffic_note": "PMC HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md) from the "
-                            "committed rocprofv3 passes of this bench command, see profiles/",
+            "traffic_note": "PMC HBM bytes per launch (FETCH_SIZE with the calibrated read correction + WRITE_SIZE, "
+                            "MI355X_MICROARCH.md, profiles/*_pmc_calibration.json) from committed rocprofv3 passes "
+                            "of this same configuration; null if none was profiled",
             "bytes_per_launch": dk["bytes_per_launch"],
             "mean_launch_ms": dk["mean_launch_ms"],
             "samples": dk["samples"],
@@ -454,22 +504,34 @@ def main() -> int:
                                   "unit": "GB/s", "frac": pd_gbs / HBM_PEAK_GBS,
                                   "basis": "144 B per particle-update + 32 B per cell (SURVEY.md 8(d))"},
         "kernels": kernels,
+        "push_kinds": sub,
         "cpu_baseline": None,
     }
-    tr = _pmc_traffic(dk["rocprof_name"].rstrip("*").rstrip(" ,").split("*")[0])
+    result["config"]["traffic_key"] = traffic_key
+    tr = _pmc_traffic(dk["rocprof_name"].rstrip("*").rstrip(" ,").split("*")[0], traffic_key)
     if tr is not None:
         result["roofline"]["traffic"] = tr["bytes_per_launch"]
         result["roofline"]["traffic_source"] = tr["source"]
+        result["roofline"]["traffic_ratio"] = tr["bytes_per_launch"] / dk["bytes_per_launch"]
     sim.close()
     os.unlink(ini)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = _cpu_baseline(S if c2 else args.cpu_size, args.ppc, args.cpu_steps,
+        cpu_size, note = args.cpu_size, ""
+        if cpu_size is None:
+            # the full grid when the host holds the oracle's particles (AoS
+            # pos+vel at the allocation, ~56 B per particle with buffers)
+            need = 56.0 * (args.ppc + 8) * nspecies * S ** nd + 40.0 * 8 * S ** nd
+            cpu_size = S if (c2 or _mem_available() > 1.3 * need) else 128
+            if cpu_size != S:
+                note = f" (the host's {_mem_available() / 2**30:.0f} GiB cannot hold the {S}^{nd} particles)"
+        steps = args.cpu_steps if args.cpu_steps is not None else (3 if cpu_size >= 256 else 20)
+        result["cpu_baseline"] = _cpu_baseline(cpu_size, args.ppc, steps,
                                                args.mg == "native", args.workload if args.workload != "c5" else "c4",
                                                # the oracle's exact coarse solve is a naive DFT (no FFT
                                                # library here): the CPU keeps the V-cycle below level 1,
                                                # which converges in as many cycles and is faster there
-                                               args.mg_extrapolate, 0)
+                                               args.mg_extrapolate, 0, note)
     if rank == 0:
         print(json.dumps(result), file=out, flush=True)
     if dist is not None:

@@ -334,7 +334,11 @@ int pinc_sim_timers_reset(PincSim *sim);
 #define PINC_PROBE_SPECTRAL 5  /* spectral solve (r2c + scale + c2r) */
 #define PINC_PROBE_PUSH 6      /* fused kick + drift + classify + deposit */
 #define PINC_PROBE_CYCLE 7     /* one V-cycle replayed as a graph (multigrid:graph) */
-#define PINC_NPROBES 8
+/* the launches of PINC_PROBE_PUSH by kind (each also counts in PUSH) */
+#define PINC_PROBE_PUSH_PLAIN 8 /* fused push, output in input order */
+#define PINC_PROBE_PUSH_COUNT 9 /* ... that also counts its output cells (before a sort) */
+#define PINC_PROBE_PUSH_SORT 10 /* ... that writes its output in tile order */
+#define PINC_NPROBES 11
 #define PINC_PROBE_ALL (-1)
 int pinc_probe_start(int kernel, int maxSamples);
 int pinc_probe_read(int kernel, double *meanMs, double *meanBytes, int *samples, long *launches);

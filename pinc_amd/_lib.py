@@ -99,7 +99,10 @@ _sigs = {
     "pinc_probe_read": (C.c_int, [C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_int),
                                   C.POINTER(C.c_long)]),
 }
-PROBES = {"gs_pass": 0, "accelerate": 1, "move_classify": 2, "deposit": 3, "residual_sumsq": 4, "spectral": 5, "push": 6, "mg_cycle": 7}
+PROBES = {"gs_pass": 0, "accelerate": 1, "move_classify": 2, "deposit": 3, "residual_sumsq": 4, "spectral": 5, "push": 6,
+          "mg_cycle": 7, "push_plain": 8, "push_count": 9, "push_sort": 10}
+# probes that split another probe's launches by kind (not separate kernels)
+SUB_PROBES = {"push_plain": "push", "push_count": "push", "push_sort": "push"}
 
 
 def probe_start(kernel: str = "all", max_samples: int = 4096) -> None:

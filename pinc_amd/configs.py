@@ -13,6 +13,11 @@ the values of the reference inputs and the overrides of SURVEY.md 8(d):
   c3           input/maxwellian.ini family (config C3): 3-D Maxwellian,
                128^3, 32 ppc, v_th,e = 0.05 cells/step, spectral Poisson
                solve (methods:poisson = sSolver, spectral.c)
+  c4ts         the two-stream variant of C4: two electron
+               beams of half the density each, drift +d and -d, plus ions
+               (population:drift, population.c:367-392, which adds the
+               drift to every velocity component: the beams stream along
+               the (1,1,1) diagonal at d cells/step per component)
 """
 from __future__ import annotations
 
@@ -101,6 +106,27 @@ def _warm(true_size=(256, 256, 256), nsub=(1, 1, 1), ppc=64, nalloc_pc=72, vth=0
     }
 
 
+def _two_stream(true_size=(256, 256, 256), nsub=(1, 1, 1), ppc=43, nalloc_pc=51, vth=0.05, drift=0.1,
+                levels=5) -> dict:
+    """C4's grid with the electrons split into two counter-streaming beams
+    (species 0 and 1, density 5e10 each: semiSI normalises by species 0,
+    units.c:159-189) plus ions, ppc particles per cell for every species
+    (default 43: 129 per cell in all, C4's 2 x 64).  Equal counts put every
+    species on the same lattice sites (pPosLattice, population.c:172-240),
+    so the plasma starts neutral node by node.  v_th and drift are in
+    cells/step after normalisation."""
+    c = _warm(true_size=true_size, nsub=nsub, ppc=ppc, nalloc_pc=nalloc_pc, vth=vth, levels=levels)
+    ne = 5e10
+    ve = thermal_velocity_si(vth, 0.2, 0.1, ne)
+    vi = ve * math.sqrt(1.0 / 1836)
+    vd = thermal_velocity_si(drift, 0.2, 0.1, ne)
+    c["population"].update({
+        "nSpecies": "3", "charge": "-1,-1,1", "mass": "1,1,1836", "density": f"{ne!r},{ne!r},1e11",
+        "drift": f"{vd!r},{-vd!r},0", "perturbAmplitude": ",".join(["0"] * 9), "perturbMode": ",".join(["0"] * 9),
+        "thermalVelocity": f"{ve!r},{ve!r},{vi!r}"})
+    return c
+
+
 def config(name: str, **kw) -> dict:
     if name == "langmuir1d":
         return _langmuir_nd(1)
@@ -116,6 +142,8 @@ def config(name: str, **kw) -> dict:
         return _cold3d(**kw)
     if name == "warm":
         return _warm(**kw)
+    if name == "c4ts":
+        return _two_stream(**kw)
     if name == "c3":
         kw.setdefault("true_size", (128, 128, 128))
         kw.setdefault("ppc", 32)

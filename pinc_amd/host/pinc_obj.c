@@ -417,7 +417,19 @@ void pinc_obj_collect(PincObj *o, Population *pop, int discard) {
 	int K = o->nObj;
 	double *cnt = calloc(K + 1, sizeof(double));
 	int *hc = calloc(K + 1, sizeof(int));
+	if (dv->objInside && dv->objInside != o->dInside)
+		msg(ERROR, "objects: the population is attached to another object table");
 	const int fusedPath = dv->objInside && !discard;
+	if (!fusedPath) {
+		/* every live particle is tested below, also those a fused push has
+		 * already deposited into rhoS: drop that deposit, so that distr
+		 * deposits the survivors afresh (a particle inside would otherwise
+		 * count twice, in rhoS and in rhoObj) */
+		dv->depValid = dv->depExtracted = 0;
+		/* the reference's API (oAlloc + oCollectObjectCharge, main.c:222)
+		 * never attaches: from the next push on, the push tests the object */
+		if (dv->fused && !discard) pinc_obj_attach(o, pop);
+	}
 	if (fusedPath) {
 		int ns = pop->nSpecies;
 		int *pc = malloc((size_t)ns * K * sizeof(int));

@@ -369,7 +369,9 @@ static int push_all(Population *pop, Grid *E, double *const *xout) {
 			a.tstamp = ts;
 			a.diag = ts + (np / 1024 + 1) * 8;
 		}
+		const int kind = sortS[s] ? PINC_PROBE_PUSH_SORT : countNext ? PINC_PROBE_PUSH_COUNT : PINC_PROBE_PUSH_PLAIN;
 		int slot = E ? pinc_probe_begin(PINC_PROBE_PUSH) : -1;
+		int slotK = E ? pinc_probe_begin(kind) : -1;
 		pinc_check(pinc_hip_push(p, s, g, &a, &nb, g_pinc.stream), "push");
 		if (ts) {
 			push_phase_report(ts, a.diag, nb, s, sortS[s], countNext);
@@ -377,7 +379,11 @@ static int push_all(Population *pop, Grid *E, double *const *xout) {
 		}
 		/* pos R+W, vel R+W (32 B per dim per particle) + E R (8 B per value
 		 * per node) + rho flush (8 B per node) */
-		if (E) pinc_probe_end(PINC_PROBE_PUSH, slot, 32.0 * nd * np + 8.0 * (nd + 1) * (double)n);
+		if (E) {
+			const double bytes = 32.0 * nd * np + 8.0 * (nd + 1) * (double)n;
+			pinc_probe_end(kind, slotK, bytes);
+			pinc_probe_end(PINC_PROBE_PUSH, slot, bytes);
+		}
 		if (E) {
 			/* two-stage (block partials of the partials): deterministic and
 			 * fast for a million partials */

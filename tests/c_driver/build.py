@@ -1,5 +1,7 @@
-"""Compile tests/c_driver/pinc_main.c against the in-tree libpinc.so
-(test infrastructure; called by __graft_entry__.build() and the tests)."""
+"""Compile the C callers under tests/c_driver/ (pinc_main.c: regular()
+through select(); pinc_objmain.c: main.c's object loop through the
+reference's object API) against the in-tree libpinc.so (test
+infrastructure; called by __graft_entry__.build() and the tests)."""
 from __future__ import annotations
 
 import subprocess
@@ -10,17 +12,19 @@ ROOT = HERE.parent.parent
 EXE = HERE / "pinc_main"
 
 
-def build() -> Path:
-    src = HERE / "pinc_main.c"
+def build(name: str = "pinc_main") -> Path:
+    src = HERE / f"{name}.c"
+    exe = HERE / name
     lib = ROOT / "pinc_amd" / "lib" / "libpinc.so"
     hdr = [ROOT / "include" / "pinc.h", ROOT / "include" / "pinc_hip.h"]
-    if EXE.exists() and all(EXE.stat().st_mtime >= p.stat().st_mtime for p in [src, lib, *hdr]):
-        return EXE
-    subprocess.run(["gcc", "-std=c11", "-O2", "-Wall", f"-I{ROOT / 'include'}", str(src), "-o", str(EXE),
+    if exe.exists() and all(exe.stat().st_mtime >= p.stat().st_mtime for p in [src, lib, *hdr]):
+        return exe
+    subprocess.run(["gcc", "-std=c11", "-O2", "-Wall", f"-I{ROOT / 'include'}", str(src), "-o", str(exe),
                     f"-L{lib.parent}", "-lpinc", f"-Wl,-rpath,{lib.parent}", "-Wl,-rpath,$ORIGIN/../../pinc_amd/lib"],
                    check=True)
-    return EXE
+    return exe
 
 
 if __name__ == "__main__":
     print(build())
+    print(build("pinc_objmain"))

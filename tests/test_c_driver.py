@@ -117,3 +117,63 @@ def test_process_exits_cleanly_in_either_import_order(built, order):
                        text=True, timeout=300)
     assert r.returncode == 0, (r.returncode, r.stdout[-1500:], r.stderr[-3000:])
     assert r.stdout.startswith("ok")
+
+
+def _sphere_mask(T, c, r):
+    z, y, x = np.meshgrid(*[np.arange(t, dtype=float) for t in (T[2], T[1], T[0])], indexing="ij")
+    return (((x - c[0]) ** 2 + (y - c[1]) ** 2 + (z - c[2]) ** 2) <= r * r).astype(float)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fused,layout", [(1, "reference"), (0, "reference"), (1, "tiled")])
+def test_reference_object_api_matches_checker(built, fused, layout):
+    """main.c's object loop driven through the reference's own API
+    (tests/c_driver/pinc_objmain.c: oAlloc, oComputeCapacitanceMatrix,
+    oCollectObjectCharge into the caller's rhoObj, gAddTo, solve,
+    oApplyCapacitanceMatrix, solve), which never attaches the object to the
+    population up front.  With population:fused = 1 the first collection
+    must discard the push's deposit (it tested no object) and attach the
+    object for the pushes after it (particles inside were
+    counted twice, in rhoS and rhoObj).  Counts exact, energies to 1e-7
+    against the checker (tolerances of tests/test_gpu_objects.py)."""
+    import orc
+    from pinc_amd import configs
+    import build as cbuild
+    exe = cbuild.build("pinc_objmain")
+    T, sphere, steps = (16, 16, 16), (8.0, 8.0, 8.0, 2.5), 4
+    cfg = configs.config("cold3d", true_size=T, nsub=(1, 1, 1))
+    cfg["multigrid"]["mgLevels"] = "3"
+    cfg["population"]["fused"] = "0"
+    cfg["objects"] = {"sphere": ",".join(map(str, sphere))}
+    cfg["time"]["nTimeSteps"] = str(steps)
+    ini = configs.write_ini(cfg)
+    cfg["population"]["fused"] = str(fused)
+    if layout == "tiled":
+        cfg["population"]["layout"] = "tiled"
+        cfg["population"]["sortInterval"] = "2"
+    ini_dev = configs.write_ini(cfg)
+    try:
+        env = dict(os.environ)
+        env.pop("PINC_QUIET", None)
+        r = subprocess.run([str(exe), ini_dev], capture_output=True, text=True, timeout=300, env=env)
+        assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
+        ke, pe = _energies(r.stdout)
+        n = [int(m.group(1)) for m in re.finditer(r"^STATUS: N (\d+)$", r.stdout, flags=re.M)]
+        assert len(ke) == steps and len(n) == steps
+        w = orc.World(ini)
+        w.init()
+        ob = orc.Objects(w, _sphere_mask(T, sphere[:3], sphere[3]))
+        ob.capacitance()
+        ob.init_collect()
+        w.init_fields()
+        for k in range(steps):
+            ob.step()
+            ke_o, pe_o = w.energy()
+            assert n[k] == w.count(0) + w.count(1), (k, n[k])
+            assert abs(ke[k] - ke_o) <= 1e-7 * abs(ke_o), (k, ke[k], ke_o)
+            assert abs(pe[k] - pe_o) <= 1e-7 * abs(pe_o), (k, pe[k], pe_o)
+        assert ob.collected(0) != 0.0
+        w.close()
+    finally:
+        os.unlink(ini)
+        os.unlink(ini_dev)
