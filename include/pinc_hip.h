@@ -427,6 +427,11 @@ void pinc_hip_fft_slab_destroy(pinc_fft_slab_t *plan);
 int pinc_hip_comm_unique_id(unsigned char *id);
 int pinc_hip_comm_init(void **comm, const unsigned char *id, int nranks, int rank);
 int pinc_hip_comm_destroy(void *comm);
+/* label of the next RCCL call for the watchdog's message (pinc_hip_comm_init
+ * starts a watchdog thread: a call that has not completed after
+ * PINC_COMM_TIMEOUT seconds, default 300, aborts the communicator and ends
+ * the process with status 3) */
+int pinc_hip_comm_note(const char *what);
 int pinc_hip_comm_sendrecv(void *comm, const void *sendbuf, long sendBytes, int peerSend,
                            void *recvbuf, long recvBytes, int peerRecv, void *stream);
 /* grouped point-to-point exchange: op i sends sendBytes[i] to sendPeer[i]

@@ -6,7 +6,13 @@
 #include "common.h"
 #include <rccl/rccl.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
+#include <time.h>
+#include <unistd.h>
+#include <atomic>
+#include <mutex>
+#include <thread>
 
 namespace pinc {
 
@@ -195,6 +201,102 @@ extern "C" int pinc_hip_comm_unique_id(unsigned char *id) {
 	return 0;
 }
 
+// Watchdog of the RCCL calls.  A collective whose peers never post the
+// matching call (a rank that skipped or reordered one) does not fail in RCCL:
+// the stream just never drains and the job hangs.  Every enqueued RCCL call
+// records an event behind it; a host thread polls the newest one, and when
+// the calls enqueued since the stream was last seen drained have not
+// completed within PINC_COMM_TIMEOUT seconds (default 300, 0 = off), or
+// RCCL reports an asynchronous error, it names the call, aborts the
+// communicator (ncclCommAbort) and ends the process with exit status 3.
+namespace {
+struct CommWatch {
+	std::mutex m;
+	std::thread th;
+	std::atomic<bool> stop{false};
+	ncclComm_t comm = nullptr;
+	static constexpr int kRing = 64;
+	hipEvent_t ev[kRing];
+	int latest = -1;
+	bool armed = false;
+	double t0 = 0, timeout = 300;
+	long seq = 0, seqFirst = 0;
+	char what[96] = "", whatFirst[96] = "";
+	int rank = 0;
+};
+CommWatch *g_watch = nullptr;
+
+double mono_s() {
+	timespec ts;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+[[noreturn]] void watch_fail(CommWatch *w, const char *why) {
+	fprintf(stderr,
+	        "[pinc rank %d] RCCL watchdog: %s; oldest pending call #%ld (%s), newest #%ld (%s); aborting the "
+	        "communicator\n",
+	        w->rank, why, w->seqFirst, w->whatFirst, w->seq, w->what);
+	fflush(stderr);
+	ncclCommAbort(w->comm);
+	_exit(3);
+}
+
+void watch_loop(CommWatch *w) {
+	while (!w->stop.load()) {
+		usleep(100000);
+		std::lock_guard<std::mutex> g(w->m);
+		ncclResult_t ae = ncclSuccess;
+		if (ncclCommGetAsyncError(w->comm, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress) {
+			char b[160];
+			snprintf(b, sizeof(b), "asynchronous error %s", ncclGetErrorString(ae));
+			watch_fail(w, b);
+		}
+		if (!w->armed) continue;
+		hipError_t q = hipEventQuery(w->ev[w->latest]);
+		if (q == hipSuccess) {
+			w->armed = false;
+			continue;
+		}
+		if (q != hipErrorNotReady) watch_fail(w, hipGetErrorString(q));
+		if (w->timeout > 0 && mono_s() - w->t0 > w->timeout) {
+			char b[160];
+			snprintf(b, sizeof(b), "no completion for %.0f s (PINC_COMM_TIMEOUT)", w->timeout);
+			watch_fail(w, b);
+		}
+	}
+}
+
+thread_local char g_note[96] = "";
+
+// after an RCCL call was enqueued on `stream`
+int watch_mark(hipStream_t stream, const char *kind) {
+	char what[200];
+	snprintf(what, sizeof(what), "%s %s", kind, g_note);
+	CommWatch *w = g_watch;
+	if (!w) return 0;
+	std::lock_guard<std::mutex> g(w->m);
+	if (w->armed && hipEventQuery(w->ev[w->latest]) == hipSuccess) w->armed = false;
+	const int idx = (w->latest + 1) % CommWatch::kRing;
+	HIPCALL(hipEventRecord(w->ev[idx], stream), "watchdog event");
+	w->latest = idx;
+	w->seq++;
+	snprintf(w->what, sizeof(w->what), "%s", what);
+	if (!w->armed) {
+		w->armed = true;
+		w->t0 = mono_s();
+		w->seqFirst = w->seq;
+		snprintf(w->whatFirst, sizeof(w->whatFirst), "%s", what);
+	}
+	return 0;
+}
+}  // namespace
+
+extern "C" int pinc_hip_comm_note(const char *what) {
+	snprintf(g_note, sizeof(g_note), "%s", what ? what : "");
+	return 0;
+}
+
 extern "C" int pinc_hip_comm_init(void **comm, const unsigned char *id, int nranks, int rank) {
 	ncclUniqueId u;
 	memcpy(&u, id, sizeof(u));
@@ -202,11 +304,28 @@ extern "C" int pinc_hip_comm_init(void **comm, const unsigned char *id, int nran
 	ncclResult_t r = ncclCommInitRank(&c, nranks, u, rank);
 	if (r != ncclSuccess) return nccl_error(r, "ncclCommInitRank");
 	*comm = (void *)c;
+	if (!g_watch) {
+		CommWatch *w = new CommWatch;
+		w->comm = c;
+		w->rank = rank;
+		if (const char *t = getenv("PINC_COMM_TIMEOUT")) w->timeout = atof(t);
+		for (int i = 0; i < CommWatch::kRing; i++)
+			HIPCALL(hipEventCreateWithFlags(&w->ev[i], hipEventDisableTiming), "watchdog events");
+		w->th = std::thread(watch_loop, w);
+		g_watch = w;
+	}
 	return 0;
 }
 
 extern "C" int pinc_hip_comm_destroy(void *comm) {
 	if (!comm) return 0;
+	if (g_watch && g_watch->comm == (ncclComm_t)comm) {
+		g_watch->stop.store(true);
+		g_watch->th.join();
+		for (int i = 0; i < CommWatch::kRing; i++) hipEventDestroy(g_watch->ev[i]);
+		delete g_watch;
+		g_watch = nullptr;
+	}
 	ncclResult_t r = ncclCommDestroy((ncclComm_t)comm);
 	if (r != ncclSuccess) return nccl_error(r, "ncclCommDestroy");
 	return 0;
@@ -222,7 +341,7 @@ extern "C" int pinc_hip_comm_sendrecv(void *comm, const void *sendbuf, long send
 	ncclResult_t r2 = ncclGroupEnd();
 	if (r != ncclSuccess) return nccl_error(r, "sendrecv");
 	if (r2 != ncclSuccess) return nccl_error(r2, "sendrecv group");
-	return 0;
+	return watch_mark(st, "sendrecv");
 }
 
 extern "C" int pinc_hip_comm_exchange(void *comm, int nOps, const int *sendPeer, void *const *sendbuf,
@@ -239,14 +358,14 @@ extern "C" int pinc_hip_comm_exchange(void *comm, int nOps, const int *sendPeer,
 	ncclResult_t r2 = ncclGroupEnd();
 	if (r != ncclSuccess) return nccl_error(r, "exchange");
 	if (r2 != ncclSuccess) return nccl_error(r2, "exchange group");
-	return 0;
+	return watch_mark(st, "exchange");
 }
 
 extern "C" int pinc_hip_comm_allgather(void *comm, const double *send, double *recv, long count,
                                        void *stream) {
 	ncclResult_t r = ncclAllGather(send, recv, count, ncclDouble, (ncclComm_t)comm, (hipStream_t)stream);
 	if (r != ncclSuccess) return nccl_error(r, "allgather");
-	return 0;
+	return watch_mark((hipStream_t)stream, "allgather");
 }
 
 extern "C" int pinc_hip_comm_allreduce_sum(void *comm, const double *send, double *recv, long count,
@@ -254,5 +373,5 @@ extern "C" int pinc_hip_comm_allreduce_sum(void *comm, const double *send, doubl
 	ncclResult_t r = ncclAllReduce(send, recv, count, ncclDouble, ncclSum, (ncclComm_t)comm,
 	                               (hipStream_t)stream);
 	if (r != ncclSuccess) return nccl_error(r, "allreduce");
-	return 0;
+	return watch_mark((hipStream_t)stream, "allreduce");
 }

@@ -17,6 +17,32 @@
  */
 #include "pinc_internal.h"
 
+/* PINC_COMM_TRACE=<dir>: every collective this rank issues, in issue order,
+ * one line each in <dir>/comm_rank<r>.log (kind, sequence number, caller's
+ * label, peers and byte counts), flushed per line, whichever transport
+ * carries it.  RCCL pairs point-to-point calls per peer in issue order and
+ * needs every rank to issue the same collectives in the same order; gloo
+ * matches by tag and is more forgiving, so the host-transport rehearsal
+ * records the sequence and tools/comm_pairing.py checks it under RCCL's
+ * rules (tests/test_gpu_comm_pairing.py). */
+static FILE *g_trace = NULL;
+static int g_traceInit = 0;
+static long g_traceSeq = 0;
+
+static FILE *trace_file(void) {
+	if (!g_traceInit) {
+		g_traceInit = 1;
+		const char *d = getenv("PINC_COMM_TRACE");
+		if (d && *d) {
+			char path[4096];
+			snprintf(path, sizeof(path), "%s/comm_rank%d.log", d, g_pinc.rank);
+			g_trace = fopen(path, "w");
+			if (!g_trace) msg(ERROR, "PINC_COMM_TRACE: cannot write %s", path);
+		}
+	}
+	return g_trace;
+}
+
 static pinc_host_transport_t g_tr;
 static int g_trSet = 0;
 static unsigned char *g_stage = NULL;
@@ -47,7 +73,15 @@ static unsigned char *stage(long bytes) {
 
 void pinc_comm_exchange(int nOps, const int *sendPeer, void *const *sendbuf, const long *sendBytes,
                         const int *recvPeer, void *const *recvbuf, const long *recvBytes, const char *what) {
+	FILE *tf = trace_file();
+	if (tf) {
+		fprintf(tf, "X %ld %s|%d", g_traceSeq++, what, nOps);
+		for (int i = 0; i < nOps; i++) fprintf(tf, " s%d:%ld r%d:%ld", sendPeer[i], sendBytes[i], recvPeer[i], recvBytes[i]);
+		fputc('\n', tf);
+		fflush(tf);
+	}
 	if (!g_trSet) {
+		pinc_hip_comm_note(what);
 		pinc_check(pinc_hip_comm_exchange(g_pinc.comm, nOps, sendPeer, sendbuf, sendBytes, recvPeer, recvbuf,
 		                                  recvBytes, g_pinc.stream),
 		           what);
@@ -78,7 +112,13 @@ void pinc_comm_exchange(int nOps, const int *sendPeer, void *const *sendbuf, con
 }
 
 void pinc_comm_allgather(const double *send, double *recv, long count, const char *what) {
+	FILE *tf = trace_file();
+	if (tf) {
+		fprintf(tf, "G %ld %s|%ld\n", g_traceSeq++, what, count);
+		fflush(tf);
+	}
 	if (!g_trSet) {
+		pinc_hip_comm_note(what);
 		pinc_check(pinc_hip_comm_allgather(g_pinc.comm, send, recv, count, g_pinc.stream), what);
 		return;
 	}
@@ -91,7 +131,13 @@ void pinc_comm_allgather(const double *send, double *recv, long count, const cha
 }
 
 void pinc_comm_allreduce_sum(double *buf, long count, const char *what) {
+	FILE *tf = trace_file();
+	if (tf) {
+		fprintf(tf, "R %ld %s|%ld\n", g_traceSeq++, what, count);
+		fflush(tf);
+	}
 	if (!g_trSet) {
+		pinc_hip_comm_note(what);
 		pinc_check(pinc_hip_comm_allreduce_sum(g_pinc.comm, buf, buf, count, g_pinc.stream), what);
 		return;
 	}
