@@ -291,37 +291,15 @@ def main() -> int:
     nd = 2 if c2 else 3
     if S % world:
         raise SystemExit("grid size must divide by the GPU count")
-    if c2:
-        # input/langmuir2D.ini + SURVEY.md 8(d)'s C2 overrides, slabs along y
-        cfg = configs.config("c2")
-        cfg["grid"]["trueSize"] = f"{S},{S // world}"
-        cfg["grid"]["nSubdomains"] = f"1,{world}"
-        cfg["population"]["nParticles"] = f"{args.ppc} pc"
-        cfg["population"]["nAlloc"] = f"{args.ppc + 16} pc"
-    else:
-        cfg = configs.config("c3" if c3 else "c4ts" if ts else "warm", true_size=(S, S, S // world),
-                             nsub=(1, 1, world), ppc=args.ppc, nalloc_pc=args.ppc + 8)
+    if args.mg_graph is None:
+        args.mg_graph = 1 if c2 else 0
+    cfg = configs.bench_config(args.workload, S, args.ppc, world, mg=args.mg, mg_shard=args.mg_shard,
+                               mg_extrapolate=args.mg_extrapolate, mg_spectral_coarse=args.mg_spectral_coarse,
+                               mg_graph=args.mg_graph, obj_capacitance=args.obj_capacitance,
+                               obj_second_guess=args.obj_second_guess, c5_fused=args.c5_fused, layout=args.layout,
+                               sort_interval=args.sort_interval, sort_in_push=args.sort_in_push,
+                               sort_fraction=args.sort_fraction, sort_max=args.sort_max)
     nspecies = int(cfg["population"]["nSpecies"])
-    if args.mg == "native":
-        cfg["multigrid"]["native"] = "1"
-        cfg["multigrid"]["shard"] = args.mg_shard
-        cfg["multigrid"]["extrapolate"] = str(args.mg_extrapolate)
-        cfg["multigrid"]["spectralCoarse"] = str(args.mg_spectral_coarse)
-        if args.mg_graph is None:
-            args.mg_graph = 1 if c2 else 0
-        cfg["multigrid"]["graph"] = str(args.mg_graph)
-    if c5:
-        # a generated sphere (the reference's bepiColombo object file is not
-        # available): centre of the grid, radius S/32
-        cfg["objects"] = {"sphere": f"{S / 2},{S / 2},{S / 2},{S / 32}", "capacitance": args.obj_capacitance,
-                          "secondGuess": args.obj_second_guess}
-        cfg["population"]["fused"] = str(args.c5_fused)
-    if args.layout == "tiled":
-        cfg["population"]["layout"] = "tiled"
-        cfg["population"]["sortInterval"] = str(args.sort_interval)
-        cfg["population"]["sortInPush"] = str(args.sort_in_push)
-        cfg["population"]["sortFraction"] = str(args.sort_fraction)
-        cfg["population"]["sortMax"] = str(args.sort_max)
     ini = configs.write_ini(cfg)
 
     def barrier():

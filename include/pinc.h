@@ -298,6 +298,9 @@ int pinc_sim_mg_limit(PincSim *sim, long maxCycles, long histCap);
 int pinc_sim_mg_levels(PincSim *sim);  /* levels of the multigrid hierarchy in use */
 int pinc_sim_mg_shard(PincSim *sim);   /* mgShardHalo of the solver (0: replicated or spectral) */
 int pinc_sim_spectral_distributed(PincSim *sim); /* sSolveDistributed (0 for multigrid) */
+/* charge the immersed objects have collected since init (object.c:497
+ * chargeCounter, summed over objects and ranks; 0 without objects) */
+double pinc_sim_obj_collected(PincSim *sim);
 long pinc_sim_mg_history(PincSim *sim, double *out, long cap);
 int pinc_sim_nspecies(const PincSim *sim);
 int pinc_sim_ndims(const PincSim *sim);

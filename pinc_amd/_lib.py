@@ -74,6 +74,7 @@ _sigs = {
     "pinc_sim_mg_levels": (C.c_int, [C.c_void_p]),
     "pinc_sim_mg_shard": (C.c_int, [C.c_void_p]),
     "pinc_sim_spectral_distributed": (C.c_int, [C.c_void_p]),
+    "pinc_sim_obj_collected": (C.c_double, [C.c_void_p]),
     "pinc_sim_nspecies": (C.c_int, [C.c_void_p]),
     "pinc_sim_ndims": (C.c_int, [C.c_void_p]),
     "pinc_sim_pop_count": (C.c_long, [C.c_void_p, C.c_int]),

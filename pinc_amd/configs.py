@@ -154,6 +154,53 @@ def config(name: str, **kw) -> dict:
     raise KeyError(name)
 
 
+def bench_config(workload: str = "c4", size: int | None = None, ppc: int | None = None, world: int = 1, *,
+                 mg: str = "native", mg_shard: str = "auto", mg_extrapolate: int = 1, mg_spectral_coarse: int = 1,
+                 mg_graph: int | None = None, obj_capacitance: str = "solve", obj_second_guess: str = "spectral",
+                 c5_fused: int = 1, layout: str = "tiled", sort_interval: int = 8, sort_in_push: int = 1,
+                 sort_fraction: float = 0.8, sort_max: int = 32) -> dict:
+    """bench.py's configuration of one rank's ini (its defaults are the
+    bench's): workload c4 / c4ts / c5 / c3 / c2 at size^nd cells split into
+    `world` slabs along the last dimension, ppc particles per cell per
+    species.  The parity tests at the bench's scale build their runs here,
+    so they run exactly the bench's flags."""
+    c2, c3, c5, ts = workload == "c2", workload == "c3", workload == "c5", workload == "c4ts"
+    if size is None:
+        size = 128 if (c3 or c2) else 256
+    if ppc is None:
+        ppc = 32 if (c3 or c2) else 43 if ts else 64
+    S = size
+    if c2:
+        # input/langmuir2D.ini + SURVEY.md 8(d)'s C2 overrides, slabs along y
+        cfg = config("c2")
+        cfg["grid"]["trueSize"] = f"{S},{S // world}"
+        cfg["grid"]["nSubdomains"] = f"1,{world}"
+        cfg["population"]["nParticles"] = f"{ppc} pc"
+        cfg["population"]["nAlloc"] = f"{ppc + 16} pc"
+    else:
+        cfg = config("c3" if c3 else "c4ts" if ts else "warm", true_size=(S, S, S // world),
+                     nsub=(1, 1, world), ppc=ppc, nalloc_pc=ppc + 8)
+    if mg == "native":
+        cfg["multigrid"]["native"] = "1"
+        cfg["multigrid"]["shard"] = mg_shard
+        cfg["multigrid"]["extrapolate"] = str(mg_extrapolate)
+        cfg["multigrid"]["spectralCoarse"] = str(mg_spectral_coarse)
+        cfg["multigrid"]["graph"] = str(mg_graph if mg_graph is not None else int(c2))
+    if c5:
+        # a generated sphere (the reference's bepiColombo object file is not
+        # available): centre of the grid, radius S/32
+        cfg["objects"] = {"sphere": f"{S / 2},{S / 2},{S / 2},{S / 32}", "capacitance": obj_capacitance,
+                          "secondGuess": obj_second_guess}
+        cfg["population"]["fused"] = str(c5_fused)
+    if layout == "tiled":
+        cfg["population"]["layout"] = "tiled"
+        cfg["population"]["sortInterval"] = str(sort_interval)
+        cfg["population"]["sortInPush"] = str(sort_in_push)
+        cfg["population"]["sortFraction"] = str(sort_fraction)
+        cfg["population"]["sortMax"] = str(sort_max)
+    return cfg
+
+
 def to_ini(cfg: Mapping[str, Mapping[str, str]]) -> str:
     out = []
     for sec, kv in cfg.items():

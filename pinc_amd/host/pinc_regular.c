@@ -353,6 +353,7 @@ int pinc_sim_mg_limit(PincSim *S, long maxCycles, long histCap) {
 int pinc_sim_mg_levels(PincSim *S) { return S->spectral ? 0 : mgLevels(S->solver); }
 int pinc_sim_mg_shard(PincSim *S) { return S->spectral ? 0 : mgShardHalo(S->solver); }
 int pinc_sim_spectral_distributed(PincSim *S) { return S->spectral ? sSolveDistributed(S->solver) : 0; }
+double pinc_sim_obj_collected(PincSim *S) { return pinc_obj_collected(S->obj); }
 
 long pinc_sim_mg_history(PincSim *S, double *out, long cap) {
 	if (S->spectral) return -1;

@@ -117,6 +117,11 @@ class Sim:
         """The spectral solve is slab-distributed (no gather of rho)."""
         return bool(HOST.pinc_sim_spectral_distributed(self._h))
 
+    @property
+    def obj_collected(self) -> float:
+        """Charge the immersed objects collected since init (0 without objects)."""
+        return HOST.pinc_sim_obj_collected(self._h)
+
     def mg_history(self) -> np.ndarray:
         """RMS residual after each V-cycle of the last solve (mgHistory)."""
         n = HOST.pinc_sim_mg_history(self._h, None, 0)

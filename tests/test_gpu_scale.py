@@ -1,0 +1,175 @@
+"""Parity and invariants at the scale the bench runs.
+
+* C4's per-GPU load -- 128^3 cells x 64 ppc x 2 species = 268 M particles,
+  the particles one of 8 GPUs holds at 256^3 -- with the bench's exact
+  flags (configs.bench_config: tiled layout with the in-push tile sort on
+  the adaptive schedule, fused push, native multigrid with the extrapolated
+  guess and the exact level-1 solve, device-side initial state) against
+  the oracle running the same algorithm on the same initial state:
+  particle counts exact, KE and PE to 1e-8 every step, V-cycles per solve
+  +-1, over enough steps for the electrons' in-push sort to run on decayed
+  order (the LDS brick box overflow, the global-slot ranking and the sort
+  schedule only trigger there).
+* The two-stream variant C4ts at 32^3 against the oracle (three species).
+* The full 256^3 C4 and C5 on one GPU (2.15 G particles), where the oracle
+  cannot follow in test time: the invariants of the loop main.c:197-274 --
+  particles conserved (with an object: remaining plus collected charge),
+  total charge of rho zero to round-off, the true-node RMS residual of
+  every solve <= 1e-10, and bounded drift of KE + PE.
+"""
+import os
+import sys
+import time
+
+import numpy as np
+import pytest
+
+from pinc_amd import configs
+
+pytestmark = pytest.mark.gpu
+SEED = 20260101
+
+
+def _probe_launches(kind: str) -> int:
+    from pinc_amd import _lib
+    return _lib.probe_read(kind)["launches"]
+
+
+def _energy_series_match(s, w, steps, ns, rtol=1e-8, log=None):
+    """Step the device and the oracle side by side."""
+    cyc = []
+    for n in range(steps):
+        cs, co = s.cycles, w.cycles
+        t0 = time.perf_counter()
+        s.step()
+        t1 = time.perf_counter()
+        w.step()
+        t2 = time.perf_counter()
+        dg, do = s.cycles - cs, w.cycles - co
+        cyc.append((dg, do))
+        ke, pe, _ = s.energy()
+        ke_o, pe_o = w.energy()
+        if log is not None:
+            log.append((n, ke, ke_o, pe, pe_o, dg, do, t1 - t0, t2 - t1))
+        for sp in range(ns):
+            assert s.count(sp) == w.count(sp), (n, sp, s.count(sp), w.count(sp))
+        assert abs(dg - do) <= 1, (n, dg, do)
+        assert abs(ke - ke_o) <= rtol * abs(ke_o), (n, ke, ke_o)
+        assert abs(pe - pe_o) <= rtol * abs(pe_o), (n, pe, pe_o)
+    return cyc
+
+
+def test_c4_per_gpu_load_matches_oracle(built):
+    """268 M particles, the bench's flags, 18 steps: the electrons' adaptive
+    sort (80 % of them displaced since the last sort, ~7 steps) runs twice,
+    the second time in the push on decayed order."""
+    import orc
+    from pinc_amd import Sim, _lib
+    cfg = configs.bench_config("c4", size=128, ppc=64)
+    ini = configs.write_ini(cfg)
+    steps = 18
+    try:
+        w = orc.World(ini)
+        w.init(perturb=False, maxwell=True, seed=SEED)
+        w.init_fields()
+        with Sim(ini, maxwell=True, perturb=False, device_init=True, seed=SEED) as s:
+            s.init()
+            for sp in range(2):
+                assert s.count(sp) == w.count(sp)
+            _lib.probe_start("all", 64)
+            log = []
+            cyc = _energy_series_match(s, w, steps, 2, log=log)
+            sorts, plain = _probe_launches("push_sort"), _probe_launches("push_plain")
+        w.close()
+    finally:
+        os.unlink(ini)
+    for row in log:
+        print("step %d KE %.12g/%.12g PE %.12g/%.12g cycles %d/%d  gpu %.2fs cpu %.2fs" % row)
+    assert sorts >= 2 and plain > sorts, (sorts, plain)
+    assert sum(g for g, _ in cyc) <= 3 * steps + 2   # the extrapolated guess: ~3 cycles per solve
+
+
+def test_c4ts_matches_oracle(built):
+    """C4's two-stream variant (bench --workload c4ts) at 32^3: two electron
+    beams drifting +-0.1 cells/step per component and ions, all on the same
+    lattice sites; the bench's flags; counts per species exact, energies to
+    1e-8 for 12 steps (the beams cross cells every ~8 steps per component,
+    so the sort schedule runs)."""
+    import orc
+    from pinc_amd import Sim
+    cfg = configs.bench_config("c4ts", size=32, ppc=8)
+    ini = configs.write_ini(cfg)
+    try:
+        w = orc.World(ini)
+        w.init(perturb=False, maxwell=True, seed=SEED)
+        w.init_fields()
+        with Sim(ini, maxwell=True, perturb=False, device_init=True, seed=SEED) as s:
+            s.init()
+            assert s.nspecies == 3
+            _energy_series_match(s, w, 12, 3)
+            v0 = s.particles(0)[1].mean(axis=0)
+            v1 = s.particles(1)[1].mean(axis=0)
+        w.close()
+    finally:
+        os.unlink(ini)
+    assert np.all(np.abs(v0 - 0.1) < 0.01) and np.all(np.abs(v1 + 0.1) < 0.01), (v0, v1)
+
+
+def _full_size_run(workload: str, steps: int, extra=None):
+    from pinc_amd import Sim
+    cfg = configs.bench_config(workload, size=256)
+    if extra:
+        for sec, kv in extra.items():
+            cfg.setdefault(sec, {}).update(kv)
+    ini = configs.write_ini(cfg)
+    out = {"n": [], "ke": [], "pe": [], "rho_sum": [], "rho_abs": [], "res": [], "collected": []}
+    try:
+        with Sim(ini, maxwell=True, perturb=False, device_init=True, seed=SEED) as s:
+            s.init()
+            q, _ = s.species()
+            out["q"] = q
+            s.mg_limit(0, 64)
+
+            def record():
+                out["n"].append([s.count(sp) for sp in range(s.nspecies)])
+                rho = s.grid(0)[1:-1, 1:-1, 1:-1]
+                out["rho_sum"].append(float(rho.sum()))
+                out["rho_abs"].append(float(np.abs(rho).sum()))
+                out["collected"].append(s.obj_collected)
+            record()
+            for _ in range(steps):
+                s.step()
+                ke, pe, _ = s.energy()
+                out["ke"].append(ke)
+                out["pe"].append(pe)
+                out["res"].append(s.mg_history()[-1])
+                record()
+    finally:
+        os.unlink(ini)
+    return out
+
+
+def test_c4_full_size_invariants(built):
+    """256^3, 64 ppc, 2.15 G particles, the bench's configuration, 4 steps."""
+    r = _full_size_run("c4", 4)
+    n = np.array(r["n"])
+    assert np.all(n == n[0]) and n[0].sum() == 2 * 64 * 256 ** 3
+    # equal numbers of +1 and -1 charges: rho sums to zero up to round-off
+    assert max(abs(a) for a in r["rho_sum"]) <= 1e-12 * max(r["rho_abs"])
+    assert max(r["res"]) <= 1e-10
+    e = np.array(r["ke"]) + np.array(r["pe"])
+    assert np.max(np.abs(e - e[0])) <= 1e-3 * abs(e[0])
+
+
+def test_c5_full_size_invariants(built):
+    """256^3 with the sphere of radius 8 cells (bench --workload c5, the
+    capacitance matrix by translation to keep the set-up short: the same
+    run to solver tolerance, tests/test_gpu_objects.py), 4 steps: charge
+    that left the plasma is on the object."""
+    r = _full_size_run("c5", 4, {"objects": {"capacitance": "green"}})
+    n, q = np.array(r["n"], dtype=float), np.asarray(r["q"])
+    plasma = n @ q[: n.shape[1]]
+    total = plasma + np.array(r["collected"]) - r["collected"][0]
+    assert np.max(np.abs(total - total[0])) <= 1e-9 * np.abs(q[0]) * n[0].sum()
+    assert np.any(np.diff(n[:, 0]) < 0)              # electrons were collected
+    assert max(r["res"]) <= 1e-10

@@ -125,6 +125,46 @@ __global__ __launch_bounds__(kT) void cp_pair32(Six s, long n) {
 	}
 }
 
+// the push's streaming shape in other patterns: one particle per lane with
+// 8-B accesses, two consecutive particles per lane with 16-B accesses, and
+// pair32 with the velocities updated in place (the plain push writes its
+// positions to the other buffer and its velocities in place)
+__global__ __launch_bounds__(kT) void cp_b64(Six s, long n) {
+	for (long i = blockIdx.x * (long)kT + threadIdx.x; i < n; i += (long)gridDim.x * kT) {
+		double v[6];
+#pragma unroll
+		for (int c = 0; c < 6; c++) v[c] = s.x[c][i];
+#pragma unroll
+		for (int c = 0; c < 6; c++) s.y[c][i] = v[c] + 1.0;
+	}
+}
+__global__ __launch_bounds__(kT) void cp_b128(Six s, long n) {
+	for (long i = 2 * (blockIdx.x * (long)kT + threadIdx.x); i + 1 < n; i += 2 * (long)gridDim.x * kT) {
+		dvec2 v[6];
+#pragma unroll
+		for (int c = 0; c < 6; c++) v[c] = *reinterpret_cast<const dvec2 *>(s.x[c] + i);
+#pragma unroll
+		for (int c = 0; c < 6; c++) *reinterpret_cast<dvec2 *>(s.y[c] + i) = v[c] + 1.0;
+	}
+}
+__global__ __launch_bounds__(kT) void cp_push(Six s, long n) {
+	// s.y[0..2] positions out, velocities in place in s.x[3..5]
+	for (long i = 4 * (blockIdx.x * (long)kT + threadIdx.x); i + 3 < n; i += 4 * (long)gridDim.x * kT) {
+		dvec2 v[6][2];
+#pragma unroll
+		for (int c = 0; c < 6; c++) {
+			v[c][0] = *reinterpret_cast<const dvec2 *>(s.x[c] + i);
+			v[c][1] = *reinterpret_cast<const dvec2 *>(s.x[c] + i + 2);
+		}
+#pragma unroll
+		for (int c = 0; c < 6; c++) {
+			double *o = c < 3 ? s.y[c] : const_cast<double *>(s.x[c]);
+			*reinterpret_cast<dvec2 *>(o + i) = v[c][0] + 1.0;
+			*reinterpret_cast<dvec2 *>(o + i + 2) = v[c][1] + 1.0;
+		}
+	}
+}
+
 int main(int argc, char **argv) {
 	const long bytes = argc > 1 ? atol(argv[1]) << 20 : 2048L << 20;  // MiB
 	const int reps = argc > 2 ? atoi(argv[2]) : 3;
@@ -174,6 +214,11 @@ int main(int argc, char **argv) {
 	timed("wr_b8x4", bytes / 8, [&] { wr_b8x4<<<grid, kT>>>((unsigned char *)b, bytes / 8); });
 	timed("at_f64", bytes / 4, [&] { at_f64<<<grid, kT>>>((double *)b, bytes / 4 / 8); });
 	timed("cp_pair32", 2.0 * 6 * n6 * 8, [&] { cp_pair32<<<grid, kT>>>(six, n6); });
+	timed("cp_b64", 2.0 * 6 * n6 * 8, [&] { cp_b64<<<grid, kT>>>(six, n6); });
+	timed("cp_b128", 2.0 * 6 * n6 * 8, [&] { cp_b128<<<grid, kT>>>(six, n6); });
+	timed("cp_push", 2.0 * 6 * n6 * 8, [&] { cp_push<<<grid, kT>>>(six, n6); });
+	// the same with a grid of one block per 1024 particles (the push's launch)
+	timed("cp_pair32_chunks", 2.0 * 6 * n6 * 8, [&] { cp_pair32<<<(unsigned)(n6 / 1024), kT>>>(six, n6); });
 	CHECK(hipDeviceSynchronize());
 	CHECK(hipFree(a));
 	CHECK(hipFree(b));

@@ -55,8 +55,14 @@ def short(name: str) -> str:
     return "".join(out).strip()
 
 
+def _db(d: Path) -> Path:
+    """rocprofv3's rocpd database of a run (<output name>_results.db)."""
+    dbs = sorted(d.glob("*_results.db"))
+    return dbs[0] if dbs else d / "bench_results.db"
+
+
 def stats(d: Path) -> list:
-    db = d / "bench_results.db"
+    db = _db(d)
     rows = []
     if db.exists():
         c = sqlite3.connect(db)
@@ -78,7 +84,7 @@ def stats(d: Path) -> list:
 
 def counters(d: Path, name: str) -> dict:
     per = defaultdict(list)
-    db = d / "bench_results.db"
+    db = _db(d)
     if db.exists():
         c = sqlite3.connect(db)
         q = "select kernel_name, grid_size, value from counters_collection where counter_name=? order by dispatch_id"
@@ -114,7 +120,7 @@ def fetch_factor(name: str, cal) -> tuple:
         for prefix, pat in FETCH_PATTERN:
             if name.startswith(prefix) and pat in cal:
                 return 1.0 / cal[pat], pat
-        if "rd_b128" in cal:
+        if "rd_b128" in cal and "rd_b128" in cal:
             return 1.0 / cal["rd_b128"], "rd_b128"
     return 2.0, "guide x2"
 
