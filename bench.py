@@ -486,6 +486,7 @@ def main() -> int:
         "cpu_baseline": None,
     }
     result["config"]["traffic_key"] = traffic_key
+    result["config"]["runtime_stack"] = _lib.runtime_stack()
     tr = _pmc_traffic(dk["rocprof_name"].rstrip("*").rstrip(" ,").split("*")[0], traffic_key)
     if tr is not None:
         result["roofline"]["traffic"] = tr["bytes_per_launch"]

@@ -414,6 +414,9 @@ int pinc_hip_fft_set_symbol(pinc_fft_t *plan, int discrete);
 typedef struct pinc_fft_slab_s pinc_fft_slab_t;
 int pinc_hip_fft_slab_create(pinc_fft_slab_t **plan, const int *T, int nloc, int nranks, int rank, void *stream);
 int pinc_hip_fft_slab_buffers(pinc_fft_slab_t *plan, void **S, void **B, long *blockBytes);
+/* the slab plan's symbol, as pinc_hip_fft_set_symbol (1: the multigrid's
+ * 7-point Laplacian; the sharded multigrid's spectral second guess) */
+int pinc_hip_fft_slab_set_symbol(pinc_fft_slab_t *plan, int discrete);
 int pinc_hip_fft_slab_forward(pinc_fft_slab_t *plan, const double *rhoSlab, void *stream);
 int pinc_hip_fft_slab_kspace(pinc_fft_slab_t *plan, void *stream);
 int pinc_hip_fft_slab_backward(pinc_fft_slab_t *plan, double *phiSlab, void *stream);

@@ -49,16 +49,38 @@ def _load() -> tuple[C.CDLL, C.CDLL]:
     # module the caller imported first; a process without torch (the C
     # driver, tests/c_driver) runs on /opt/rocm.  RTLD_LOCAL keeps our
     # symbols out of the global scope; libpinc finds libpinc_hip by rpath.
-    try:
-        import torch  # noqa: F401  (see above: binds our libraries to torch's ROCm stack)
-    except ImportError:
-        pass
+    # PINC_TORCH_STACK=0 skips the pre-import (a torch-free Python process
+    # then runs on /opt/rocm like the C driver; it must not import torch
+    # afterwards).  runtime_stack() reports which copies a process mapped.
+    if os.environ.get("PINC_TORCH_STACK", "1") != "0":
+        try:
+            import torch  # noqa: F401  (see above: binds our libraries to torch's ROCm stack)
+        except ImportError:
+            pass
     hip = C.CDLL(str(hip_path), mode=C.RTLD_LOCAL)
     host = C.CDLL(str(host_path), mode=C.RTLD_LOCAL)
     return hip, host
 
 
 HIP, HOST = _load()
+
+
+def runtime_stack() -> dict:
+    """The HIP runtime, rocFFT and RCCL files this process has mapped: torch's
+    bundled copies for Python entry points (torch imported first, see _load),
+    /opt/rocm for the C driver and PINC_TORCH_STACK=0.  The libraries are
+    built against /opt/rocm's headers (ROCm 7.2); torch's bundled runtime is
+    its own release (torch.version.hip), used through the stable HIP C ABI."""
+    out = {}
+    try:
+        for line in Path("/proc/self/maps").read_text().splitlines():
+            f = line.split()[-1] if line.count("/") else ""
+            for key in ("libamdhip64", "librocfft", "librccl"):
+                if key in f and key not in out:
+                    out[key] = f
+    except OSError:
+        pass
+    return out
 
 _sigs = {
     "pinc_last_error": (C.c_char_p, []),

@@ -57,7 +57,7 @@ __global__ __launch_bounds__(kObjThreads) void k_obj_flag(const double *__restri
 __global__ void k_obj_gather(const double *__restrict__ grid, const long *__restrict__ idx, long n,
                              double *__restrict__ out) {
 	const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-	if (i < n) out[i] = grid[idx[i]];
+	if (i < n) out[i] = idx[i] >= 0 ? grid[idx[i]] : 0.0;  // -1: another rank's node
 }
 
 __global__ void k_obj_correct(const double *__restrict__ M, const double *__restrict__ phiS, long n, double phiC,

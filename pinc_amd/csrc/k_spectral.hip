@@ -197,6 +197,7 @@ extern "C" void pinc_hip_fft_destroy(pinc_fft_t *f) {
 // results agree to FFT round-off, not bit for bit.
 struct pinc_fft_slab_s {
 	int T[3], nloc, P, rank, Tyl, Mx;
+	int discrete;     // the 7-point symbol (pinc_hip_fft_slab_set_symbol)
 	long nBlock;      // complex values per (rank pair) block: nloc * Tyl * Mx
 	rocfft_plan fwd2, inv2, zfwd, zinv;
 	rocfft_execution_info info;
@@ -238,8 +239,9 @@ __global__ void k_slab_unpack(const double2 *__restrict__ S, double2 *__restrict
 }
 
 // B [z][yl][kx] *= factor at (kx, ky = y0 + yl, kz = z): k_spectral_scale's 3-D
-// branch
-__global__ void k_slab_scale(double2 *__restrict__ B, int Tx, int Ty, int Tz, int Tyl, int y0, double Ntot) {
+// branches (continuous or discrete symbol)
+__global__ void k_slab_scale(double2 *__restrict__ B, int Tx, int Ty, int Tz, int Tyl, int y0, double Ntot,
+                             int discrete) {
 	const int Mx = Tx / 2 + 1;
 	const long n = (long)Tz * Tyl * Mx;
 	for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
@@ -253,9 +255,15 @@ __global__ void k_slab_scale(double2 *__restrict__ B, int Tx, int Ty, int Tz, in
 		} else {
 			const int ny = iy <= Ty / 2 ? iy : iy - Ty;
 			const int nz = iz <= Tz / 2 ? iz : iz - Tz;
-			const double kx = 2 * M_PI * ix / Tx, ky = 2 * M_PI * ny / Ty, kz = 2 * M_PI * nz / Tz;
-			f = 1.0 / (kx * kx + ky * ky + kz * kz);
-			f /= Ntot;
+			if (discrete) {
+				const double s = (2.0 - 2.0 * cos(2 * M_PI * ix / Tx)) + (2.0 - 2.0 * cos(2 * M_PI * ny / Ty)) +
+				                 (2.0 - 2.0 * cos(2 * M_PI * nz / Tz));
+				f = 1.0 / s / Ntot;
+			} else {
+				const double kx = 2 * M_PI * ix / Tx, ky = 2 * M_PI * ny / Ty, kz = 2 * M_PI * nz / Tz;
+				f = 1.0 / (kx * kx + ky * ky + kz * kz);
+				f /= Ntot;
+			}
 		}
 		double2 v = B[i];
 		v.x *= f;
@@ -361,6 +369,12 @@ extern "C" int pinc_hip_fft_slab_create(pinc_fft_slab_t **out, const int *T, int
 	return 0;
 }
 
+extern "C" int pinc_hip_fft_slab_set_symbol(pinc_fft_slab_t *f, int discrete) {
+	if (!f) return set_error(hipErrorInvalidValue, "fft_slab_set_symbol: no plan");
+	f->discrete = discrete != 0;
+	return 0;
+}
+
 extern "C" int pinc_hip_fft_slab_buffers(pinc_fft_slab_t *f, void **S, void **B, long *blockBytes) {
 	*S = f->S;
 	*B = f->B;
@@ -389,7 +403,7 @@ extern "C" int pinc_hip_fft_slab_kspace(pinc_fft_slab_t *f, void *stream) {
 	if (s == rocfft_status_success) s = rocfft_execute(f->zfwd, io, nullptr, f->info);
 	if (s != rocfft_status_success) return fft_error(s, "fft_slab_kspace: z forward");
 	hipLaunchKernelGGL(k_slab_scale, dim3(slab_blocks(f->nBlock * f->P)), dim3(256), 0, st, f->B, f->T[0], f->T[1],
-	                   f->T[2], f->Tyl, f->rank * f->Tyl, (double)f->T[0] * f->T[1] * f->T[2]);
+	                   f->T[2], f->Tyl, f->rank * f->Tyl, (double)f->T[0] * f->T[1] * f->T[2], f->discrete);
 	if (int rc = check_launch("fft_slab_kspace: scale")) return rc;
 	s = rocfft_execute(f->zinv, io, nullptr, f->info);
 	if (s != rocfft_status_success) return fft_error(s, "fft_slab_kspace: z inverse");

@@ -148,6 +148,8 @@ void pinc_obj_add_rho(PincObj *o, Grid *rho);
 void pinc_obj_attach(PincObj *o, Population *pop);
 double pinc_obj_apply(PincObj *o, Grid *rho, const Grid *phi);
 long pinc_obj_nsurface(const PincObj *o);
+/* slab-distributed Poisson solve with a slab plan (pinc_spectral.c) */
+void pinc_slab_poisson(pinc_fft_slab_t *plan, const double *rhoSlab, double *phiSlab, const char *what);
 double pinc_obj_collected(const PincObj *o);
 /* Boris selected through methods:acc: its initial half step (pinc_regular.c) */
 void pinc_boris_half_step(int on);
@@ -185,6 +187,7 @@ struct MultigridSolver {
 	int secondSpectral;
 	double *rhoSave, *dphi;
 	pinc_fft_t *fft;
+	pinc_fft_slab_t *fftSlab; /* secondSpectral == 2: the sharded level 0's transform */
 	/* multigrid:spectralCoarse (native mode): level 1's correction solved
 	 * exactly (rocFFT, the 7-point symbol) instead of by the levels below */
 	pinc_fft_t *fftCoarse;

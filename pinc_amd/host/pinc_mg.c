@@ -65,15 +65,15 @@ static void shard_setup(MultigridSolver *S, const dictionary *ini, const Grid *r
 		free(v);
 	}
 	S->shard = 0;
-	int objects = iniHas(ini, "objects:sphere") || iniHas(ini, "objects:file");
 	int nl = g.nloc;
 	int m = S->nPre > S->nPost ? S->nPre : S->nPost;
 	if (m > (nl - 2) / 2) m = (nl - 2) / 2;
-	int ok = S->native && g.nd == 3 && !objects && S->nLevels >= 2 && nl % 2 == 0 && m >= 1;
+	/* (objects shard too: pinc_obj.c reads the surface potentials from the
+	 * slabs and sums them over the ranks, object.c:163-364's MPI pattern) */
+	int ok = S->native && g.nd == 3 && S->nLevels >= 2 && nl % 2 == 0 && m >= 1;
 	if (!mode || !ok) {
 		if (mode == 1 && !ok)
-			msg(WARNING, "multigrid:shard=1 needs native mode, 3-D, no objects and slabs of >= 4 planes: "
-			             "replicated solve");
+			msg(WARNING, "multigrid:shard=1 needs native mode, 3-D and slabs of >= 4 planes: replicated solve");
 		return;
 	}
 	int h = 2 * m + 2;
@@ -208,11 +208,14 @@ MultigridSolver *mgAllocSolver(const dictionary *ini, Grid *rho, Grid *phi) {
 		pinc_check(pinc_hip_malloc((void **)&S->phiPrev, S->N[0] * sizeof(double)), "mg extrapolation");
 	if (S->extrap && S->objects && iniHas(ini, "objects:secondGuess")) {
 		char *v = iniGetStr(ini, "objects:secondGuess");
-		/* (objects: the solve is replicated, rho[0] and phi[0] global on
-		 * every rank, rho[0] gathered before guess_begin) */
+		/* replicated solve: rho[0] and phi[0] global on every rank (rho[0]
+		 * gathered before guess_begin), one transform of the global grid;
+		 * sharded level 0: the owned planes, a slab-distributed transform */
 		if (!strcmp(v, "spectral")) {
 			if (!S->shard) S->secondSpectral = 1;
-			else msg(WARNING, "objects:secondGuess = spectral needs the replicated solve: the last correction response instead");
+			else if (g.T[1] % g_pinc.nranks == 0 && g.T[2] == g.nloc * g_pinc.nranks) S->secondSpectral = 2;
+			else msg(WARNING, "objects:secondGuess = spectral on the sharded solve needs grid:trueSize y divisible by "
+			                  "the rank count: the last correction response instead");
 		} else if (strcmp(v, "response")) msg(ERROR, "objects:secondGuess = %s (spectral | response)", v);
 		free(v);
 	}
@@ -221,11 +224,18 @@ MultigridSolver *mgAllocSolver(const dictionary *ini, Grid *rho, Grid *phi) {
 		pinc_check(pinc_hip_fft_create(&S->fftCoarse, S->L[1].nd, S->L[1].T, g_pinc.stream), "mg spectral coarse");
 		pinc_check(pinc_hip_fft_set_symbol(S->fftCoarse, 1), "mg spectral coarse");
 	}
-	if (S->secondSpectral) {
+	if (S->secondSpectral == 1) {
 		pinc_check(pinc_hip_malloc((void **)&S->rhoSave, S->N[0] * sizeof(double)), "mg second guess");
 		pinc_check(pinc_hip_malloc((void **)&S->dphi, S->N[0] * sizeof(double)), "mg second guess");
 		pinc_check(pinc_hip_fft_create(&S->fft, S->L[0].nd, S->L[0].T, g_pinc.stream), "mg second guess");
 		pinc_check(pinc_hip_fft_set_symbol(S->fft, 1), "mg second guess");
+	} else if (S->secondSpectral == 2) {
+		long n = S->ps0 * S->nloc0;
+		pinc_check(pinc_hip_malloc((void **)&S->rhoSave, n * sizeof(double)), "mg second guess");
+		pinc_check(pinc_hip_malloc((void **)&S->dphi, n * sizeof(double)), "mg second guess");
+		pinc_check(pinc_hip_fft_slab_create(&S->fftSlab, g.T, g.nloc, g_pinc.nranks, g_pinc.rank, g_pinc.stream),
+		           "mg second guess");
+		pinc_check(pinc_hip_fft_slab_set_symbol(S->fftSlab, 1), "mg second guess");
 	}
 	if (S->extrap && S->objects) {
 		pinc_check(pinc_hip_malloc((void **)&S->phiA, S->N[0] * sizeof(double)), "mg extrapolation");
@@ -247,6 +257,7 @@ void mgFreeSolver(MultigridSolver *S) {
 	pinc_hip_free(S->rhoSave);
 	pinc_hip_free(S->dphi);
 	pinc_hip_fft_destroy(S->fft);
+	pinc_hip_fft_slab_destroy(S->fftSlab);
 	pinc_hip_fft_destroy(S->fftCoarse);
 	free(S->hist);
 	for (int q = 0; q < S->nLevels; q++) {
@@ -283,12 +294,21 @@ static void guess_begin(MultigridSolver *S, int role) {
 	} else if (role == PINC_MG_GUESS_FIRST && S->havePrev >= 2) {
 		/* from the first solutions of the last two steps */
 		pinc_check(pinc_hip_lincomb(phi, S->phiA, 2.0, S->phiB, -1.0, n, g_pinc.stream), "mg extrapolation");
-	} else if (role == PINC_MG_GUESS_SECOND && S->secondSpectral && S->havePrev >= 1) {
+	} else if (role == PINC_MG_GUESS_SECOND && S->secondSpectral == 1 && S->havePrev >= 1) {
 		/* this step's first solution + the exact discrete response to the
 		 * correction charge (rho now minus rho of the first solve) */
 		pinc_check(pinc_hip_lincomb(S->rhoSave, S->rho[0], 1.0, S->rhoSave, -1.0, n, g_pinc.stream), "mg second guess");
 		pinc_check(pinc_hip_fft_poisson(S->fft, S->rhoSave, S->dphi, g_pinc.stream), "mg second guess");
 		pinc_check(pinc_hip_lincomb(phi, phi, 1.0, S->dphi, 1.0, n, g_pinc.stream), "mg second guess");
+	} else if (role == PINC_MG_GUESS_SECOND && S->secondSpectral == 2 && S->havePrev >= 1) {
+		/* the same on the sharded level 0: the owned planes of the correction
+		 * charge through the slab-distributed transform; the halo planes of
+		 * the guess are refreshed before the first smoothing chunk */
+		long no = S->ps0 * S->nloc0, o = (long)S->hz * S->ps0;
+		pinc_check(pinc_hip_lincomb(S->rhoSave, S->rho[0] + o, 1.0, S->rhoSave, -1.0, no, g_pinc.stream),
+		           "mg second guess");
+		pinc_slab_poisson(S->fftSlab, S->rhoSave, S->dphi, "mg second guess");
+		pinc_check(pinc_hip_lincomb(phi + o, phi + o, 1.0, S->dphi, 1.0, no, g_pinc.stream), "mg second guess");
 	} else if (role == PINC_MG_GUESS_SECOND && S->haveCorr) {
 		/* this step's first solution + the last step's correction response */
 		pinc_check(pinc_hip_lincomb(phi, phi, 1.0, S->dCorr, 1.0, n, g_pinc.stream), "mg extrapolation");
@@ -302,8 +322,12 @@ static void guess_end(MultigridSolver *S, int role) {
 		S->phiB = S->phiA;
 		S->phiA = t;
 		pinc_check(pinc_hip_d2d(S->phiA, S->phi[0], n * sizeof(double), g_pinc.stream), "mg extrapolation");
-		if (S->secondSpectral)
+		if (S->secondSpectral == 1)
 			pinc_check(pinc_hip_d2d(S->rhoSave, S->rho[0], n * sizeof(double), g_pinc.stream), "mg second guess");
+		else if (S->secondSpectral == 2)
+			pinc_check(pinc_hip_d2d(S->rhoSave, S->rho[0] + (long)S->hz * S->ps0, S->ps0 * S->nloc0 * sizeof(double),
+			                        g_pinc.stream),
+			           "mg second guess");
 		if (S->havePrev < 2) S->havePrev++;
 	} else if (role == PINC_MG_GUESS_SECOND && S->havePrev >= 1) {
 		pinc_check(pinc_hip_lincomb(S->dCorr, S->phi[0], 1.0, S->phiA, -1.0, n, g_pinc.stream), "mg extrapolation");

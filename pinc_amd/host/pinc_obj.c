@@ -1,10 +1,12 @@
 /*
  * pinc_obj.c -- immersed objects (object.c, config C5) on the device path,
- * any number of z-slabs (the solve is replicated, so phi is read from its
- * global view and the charge corrections go to the owning slab), fused or
- * unfused operators, either particle layout (with the tiled one the
- * back-filled slots are deposited individually until the next sort, as
- * after a migration).
+ * any number of z-slabs, fused or unfused operators, either particle layout
+ * (with the tiled one the back-filled slots are deposited individually until
+ * the next sort, as after a migration).  With a replicated solve phi is read
+ * from its global view; with the sharded multigrid (pinc_mg.c, native mode)
+ * each rank reads the surface nodes of its own slab and the surface
+ * potentials are summed over the ranks (n doubles, as object.c:163-364 does
+ * with MPI_Allreduce/Allgather).  Charge corrections go to the owning slab.
  *
  *   pinc_obj_create       oFillLookupTables (object.c:111-160) and
  *                         oFindObjectSurfaceNodes (object.c:368-458) on the
@@ -283,6 +285,19 @@ double pinc_obj_collected(const PincObj *o) {
 	return t;
 }
 
+/* phi at surface entries [s0, s0 + n) into dst (device): from the solve's
+ * global view, or -- sharded solve, no global phi -- from this rank's slab
+ * (the solve leaves the owned planes there) with the other ranks' nodes read
+ * as zero, summed over the ranks */
+static void surface_phi(PincObj *o, const Grid *phi, long s0, long n, double *dst) {
+	if (phi->dev->global) {
+		pinc_check(pinc_hip_obj_gather(phi->dev->global, o->dSurfG + s0, n, dst, g_pinc.stream), "object gather");
+		return;
+	}
+	pinc_check(pinc_hip_obj_gather(phi->dev->d, o->dSurf + s0, n, dst, g_pinc.stream), "object gather");
+	if (g_pinc.nranks > 1) pinc_comm_allreduce_sum(dst, n, "surface phi");
+}
+
 /* object.c:163-298: column i = phi at the surface nodes for a unit charge
  * at surface node i (solver warm-started column to column, as the
  * reference's); rho and phi are restored afterwards */
@@ -295,13 +310,20 @@ void pinc_obj_capacitance(PincObj *o, Grid *rho, Grid *phi, void *solver,
 	pinc_check(pinc_hip_d2d(saveR, rho->dev->d, N * sizeof(double), g_pinc.stream), "cap save");
 	pinc_check(pinc_hip_d2d(saveP, phi->dev->d, N * sizeof(double), g_pinc.stream), "cap save");
 	pinc_check(pinc_hip_memset(phi->dev->d, 0, N * sizeof(double), g_pinc.stream), "cap");
-	/* several ranks: the solver's global phi is a buffer of its own */
-	double *saveG = NULL;
+	/* several ranks: the solver's global phi is a buffer of its own; the
+	 * sharded solve keeps its level 0 in the extended slab */
+	double *saveG = NULL, *saveE = NULL;
 	long NG = (long)phi->dev->geom.T[0] * phi->dev->geom.T[1] * phi->dev->geom.T[2];
+	long NE = phi->dev->ext && phi->dev->ext != phi->dev->d ? (long)phi->dev->extPlanes * phi->dev->planeSize : 0;
 	if (phi->dev->ownsGlobal) {
 		pinc_check(pinc_hip_malloc((void **)&saveG, NG * sizeof(double)), "cap save");
 		pinc_check(pinc_hip_d2d(saveG, phi->dev->global, NG * sizeof(double), g_pinc.stream), "cap save");
 		pinc_check(pinc_hip_memset(phi->dev->global, 0, NG * sizeof(double), g_pinc.stream), "cap");
+	}
+	if (NE) {
+		pinc_check(pinc_hip_malloc((void **)&saveE, NE * sizeof(double)), "cap save");
+		pinc_check(pinc_hip_d2d(saveE, phi->dev->ext, NE * sizeof(double), g_pinc.stream), "cap save");
+		pinc_check(pinc_hip_memset(phi->dev->ext, 0, NE * sizeof(double), g_pinc.stream), "cap");
 	}
 	double *col = malloc(n * sizeof(double));
 	for (int a = 0; a < o->nObj; a++) {
@@ -331,7 +353,18 @@ void pinc_obj_capacitance(PincObj *o, Grid *rho, Grid *phi, void *solver,
 			pinc_check(pinc_hip_h2d(rho->dev->d + i0, &one, sizeof(double), g_pinc.stream), "cap unit charge");
 		}
 		solve(solver, rho, phi, mpi);
-		pinc_check(pinc_hip_d2h(G, phi->dev->global, NG * sizeof(double), g_pinc.stream), "cap green");
+		if (phi->dev->global) {
+			pinc_check(pinc_hip_d2h(G, phi->dev->global, NG * sizeof(double), g_pinc.stream), "cap green");
+		} else {
+			/* sharded solve: the response's slabs gathered once (set-up only) */
+			long ps = phi->dev->planeSize, nl = phi->dev->geom.nloc;
+			double *dG = NULL;
+			pinc_check(pinc_hip_malloc((void **)&dG, NG * sizeof(double)), "cap green");
+			if (g_pinc.nranks > 1) pinc_comm_allgather(phi->dev->d + ps, dG, ps * nl, "cap green gather");
+			else pinc_check(pinc_hip_d2d(dG, phi->dev->d + ps, NG * sizeof(double), g_pinc.stream), "cap green");
+			pinc_check(pinc_hip_d2h(G, dG, NG * sizeof(double), g_pinc.stream), "cap green");
+			pinc_hip_free(dG);
+		}
 	}
 	for (int a = 0; a < o->nObj; a++) {
 		long s0 = o->surfOff[a], na = o->surfOff[a + 1] - s0;
@@ -350,8 +383,7 @@ void pinc_obj_capacitance(PincObj *o, Grid *rho, Grid *phi, void *solver,
 			pinc_check(pinc_hip_memset(rho->dev->d, 0, N * sizeof(double), g_pinc.stream), "cap");
 			pinc_check(pinc_hip_obj_add(rho->dev->d, o->dSurf + s0 + i, 1, 1.0, g_pinc.stream), "cap unit charge");
 			solve(solver, rho, phi, mpi);
-			pinc_check(pinc_hip_obj_gather(phi->dev->global, o->dSurfG + s0, na, o->dPhiS, g_pinc.stream),
-			           "cap gather");
+			surface_phi(o, phi, s0, na, o->dPhiS);
 			pinc_check(pinc_hip_d2h(col, o->dPhiS, na * sizeof(double), g_pinc.stream), "cap gather");
 			for (long k = 0; k < na; k++) P[k * na + i] = col[k];
 		}
@@ -371,10 +403,12 @@ void pinc_obj_capacitance(PincObj *o, Grid *rho, Grid *phi, void *solver,
 	pinc_check(pinc_hip_d2d(rho->dev->d, saveR, N * sizeof(double), g_pinc.stream), "cap restore");
 	pinc_check(pinc_hip_d2d(phi->dev->d, saveP, N * sizeof(double), g_pinc.stream), "cap restore");
 	if (saveG) pinc_check(pinc_hip_d2d(phi->dev->global, saveG, NG * sizeof(double), g_pinc.stream), "cap restore");
+	if (saveE) pinc_check(pinc_hip_d2d(phi->dev->ext, saveE, NE * sizeof(double), g_pinc.stream), "cap restore");
 	pinc_check(pinc_hip_stream_sync(g_pinc.stream), "cap");
 	pinc_hip_free(saveR);
 	pinc_hip_free(saveP);
 	pinc_hip_free(saveG);
+	pinc_hip_free(saveE);
 	free(col);
 	free(G);
 	rho->dev->ghostsValid = phi->dev->ghostsValid = 0;
@@ -505,7 +539,7 @@ double pinc_obj_apply(PincObj *o, Grid *rho, const Grid *phi) {
 	long n = o->nSurf;
 	/* phi at every object's surface first: the corrections do not change
 	 * phi until the next solve (object.c:313-363 loops the objects) */
-	pinc_check(pinc_hip_obj_gather(phi->dev->global, o->dSurfG, n, o->dPhiS, g_pinc.stream), "object gather");
+	surface_phi(o, phi, 0, n, o->dPhiS);
 	double *ph = malloc(n * sizeof(double));
 	pinc_check(pinc_hip_d2h(ph, o->dPhiS, n * sizeof(double), g_pinc.stream), "object gather");
 	double pc = 0;

@@ -24,6 +24,8 @@
 #define _GNU_SOURCE
 #include "pinc_internal.h"
 
+static void all_to_all(char *src, char *dst, long blockBytes, const char *what);
+
 struct SpectralSolver {
 	pinc_fft_t *fft;
 	pinc_fft_slab_t *slab;  /* slab-distributed plan (several ranks, 3-D) */
@@ -79,6 +81,19 @@ SpectralSolver *sAlloc(const dictionary *ini, Grid *rho, Grid *phi) {
 	return S;
 }
 
+/* phi slab = the plan's Poisson operator on the rho slab (nloc planes each,
+ * no ghosts), slab-distributed over the ranks */
+void pinc_slab_poisson(pinc_fft_slab_t *plan, const double *rhoSlab, double *phiSlab, const char *what) {
+	void *sBuf = NULL, *bBuf = NULL;
+	long blk = 0;
+	pinc_check(pinc_hip_fft_slab_buffers(plan, &sBuf, &bBuf, &blk), what);
+	pinc_check(pinc_hip_fft_slab_forward(plan, rhoSlab, g_pinc.stream), what);
+	all_to_all(sBuf, bBuf, blk, what);
+	pinc_check(pinc_hip_fft_slab_kspace(plan, g_pinc.stream), what);
+	all_to_all(bBuf, sBuf, blk, what);
+	pinc_check(pinc_hip_fft_slab_backward(plan, phiSlab, g_pinc.stream), what);
+}
+
 void sFree(SpectralSolver *S) {
 	if (!S) return;
 	pinc_hip_fft_destroy(S->fft);
@@ -101,7 +116,7 @@ static void all_to_all(char *src, char *dst, long blockBytes, const char *what) 
 		nb[i - 1] = blockBytes;
 	}
 	pinc_check(pinc_hip_d2d(dst + (long)r * blockBytes, src + (long)r * blockBytes, blockBytes, g_pinc.stream), what);
-	pinc_comm_exchange(n, sp, sb, nb, rp, rb, nb, what);
+	if (n > 0) pinc_comm_exchange(n, sp, sb, nb, rp, rb, nb, what);
 	free(sp);
 	free(rp);
 	free(sb);
@@ -114,15 +129,8 @@ void sSolve(SpectralSolver *S, Grid *rho, Grid *phi, const MpiInfo *mpiInfo) {
 	pinc_phase_begin(4);
 	if (S->slab) {
 		long ps = rho->dev->planeSize;
-		void *sBuf = NULL, *bBuf = NULL;
-		long blk = 0;
-		pinc_check(pinc_hip_fft_slab_buffers(S->slab, &sBuf, &bBuf, &blk), "spectral slab");
 		int slot = pinc_probe_begin(PINC_PROBE_SPECTRAL);
-		pinc_check(pinc_hip_fft_slab_forward(S->slab, rho->dev->d + ps, g_pinc.stream), "spectral slab forward");
-		all_to_all(sBuf, bBuf, blk, "spectral transpose");
-		pinc_check(pinc_hip_fft_slab_kspace(S->slab, g_pinc.stream), "spectral slab k-space");
-		all_to_all(bBuf, sBuf, blk, "spectral transpose back");
-		pinc_check(pinc_hip_fft_slab_backward(S->slab, phi->dev->d + ps, g_pinc.stream), "spectral slab backward");
+		pinc_slab_poisson(S->slab, rho->dev->d + ps, phi->dev->d + ps, "spectral transpose");
 		pinc_probe_end(PINC_PROBE_SPECTRAL, slot, 48.0 * S->N / g_pinc.nranks);
 		S->solves++;
 		phi->dev->ghostsValid = 0;

@@ -33,6 +33,7 @@ def main() -> int:
             c = torch.tensor([s.count(0), s.count(1)], dtype=torch.int64)
             dist.all_reduce(c)
             res["counts"].append(c.tolist())
+        res["mg_shard"] = s.mg_shard
     if rank == 0:
         Path(args.out).write_text(json.dumps(res))
     dist.barrier()

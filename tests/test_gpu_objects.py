@@ -115,19 +115,29 @@ def test_object_mask_file_equals_sphere(built, tmp_path):
         assert abs(a - b) <= 1e-10 * abs(a)
 
 
-@pytest.mark.parametrize("capacitance,fused,guess", [("solve", 0, None), ("green", 0, None), ("solve", 1, None),
-                                                     ("solve", 1, "spectral")])
-def test_object_two_slabs_match_one(built, tmp_path, capacitance, fused, guess):
-    """Two z-slabs (host transport, one GPU): the object's lookups are
-    global, phi is read from the replicated solve's global view, charge
-    corrections land in the owning slab and the collected charge is summed
-    over the ranks; counts and energies match a one-rank run.  green: the
-    unit charge of the translated response sits on the rank holding global
-    node (0,0,0) and the response is read from the replicated potential.
-    fused: the push collects the particles that stay, the flag pass the
-    immigrants (the sphere straddles the slab boundary).  spectral: native
-    multigrid with the extrapolated guesses and the spectral second guess
-    (every rank transforms the gathered global rho)."""
+@pytest.mark.parametrize("capacitance,fused,guess,world,shard", [
+    ("solve", 0, None, 2, None), ("green", 0, None, 2, None), ("solve", 1, None, 2, None),
+    ("solve", 1, "spectral", 2, None),
+    # the sharded level 0 with an object: surface
+    # potentials read from the owning slabs and summed over the ranks, the
+    # spectral second guess slab-distributed
+    ("solve", 1, "spectral", 2, "1"), ("solve", 1, "response", 2, "1"), ("green", 1, "spectral", 4, "1")])
+def test_object_two_slabs_match_one(built, tmp_path, capacitance, fused, guess, world, shard):
+    """Two (or four) z-slabs (host transport, one GPU): the object's lookups
+    are global, charge corrections land in the owning slab and the collected
+    charge is summed over the ranks; counts and energies match a one-rank
+    run.  Replicated solve: phi is read from its global view.  shard = 1:
+    the native multigrid's level 0 stays distributed,
+    each rank reads the surface nodes of its slab and the potentials are
+    summed over the ranks; the one-rank run it is compared with solves
+    replicated.  green: the unit charge of the translated response sits on
+    the rank holding global node (0,0,0) and the response is read from the
+    potential (all-gathered once when sharded).  fused: the push collects the
+    particles that stay, the flag pass the immigrants (the sphere straddles
+    a slab boundary).  spectral: native multigrid with the extrapolated
+    guesses and the spectral second guess (replicated: every rank transforms
+    the gathered global rho; sharded: the slab-distributed transform of the
+    owned planes)."""
     import json
     import os
     import socket
@@ -136,10 +146,11 @@ def test_object_two_slabs_match_one(built, tmp_path, capacitance, fused, guess):
     from pathlib import Path
     from pinc_amd import Sim
     root = Path(__file__).resolve().parent.parent
-    sphere = "8.2,7.7,8.4,3.3"   # straddles the slab boundary at z = 8
+    zb = 8 * world // 2
+    sphere = f"8.2,7.7,{zb + 0.4},3.3"   # straddles the slab boundary at z = zb
     steps = 4 if guess else 3
 
-    def cfg(nsub, T):
+    def cfg(nsub, T, shard_mode):
         c = configs.config("cold3d", true_size=T, nsub=nsub)
         c["multigrid"]["mgLevels"] = "3"
         c["population"]["fused"] = str(fused)
@@ -148,10 +159,12 @@ def test_object_two_slabs_match_one(built, tmp_path, capacitance, fused, guess):
             c["multigrid"]["native"] = "1"
             c["multigrid"]["extrapolate"] = "1"
             c["objects"]["secondGuess"] = guess
+        if shard_mode is not None:
+            c["multigrid"]["shard"] = shard_mode
         return configs.write_ini(c)
 
     one = {"energy": [], "counts": []}
-    with Sim(cfg((1, 1, 1), (16, 16, 16))) as s:
+    with Sim(cfg((1, 1, 1), (16, 16, 8 * world), None)) as s:
         s.init()
         for _ in range(steps):
             s.step()
@@ -163,12 +176,14 @@ def test_object_two_slabs_match_one(built, tmp_path, capacitance, fused, guess):
         port = so.getsockname()[1]
     out = tmp_path / "two.json"
     env = dict(os.environ, PYTHONPATH=str(root))
-    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
                         "--master-addr=127.0.0.1", f"--master-port={port}", str(root / "tests" / "obj_worker.py"),
-                        "--ini", cfg((1, 1, 2), (16, 16, 8)), "--out", str(out), "--steps", str(steps)],
+                        "--ini", cfg((1, 1, world), (16, 16, 8), shard), "--out", str(out), "--steps", str(steps)],
                        env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     two = json.loads(out.read_text())
+    if shard:
+        assert two["mg_shard"] > 0
     assert two["counts"] == one["counts"]
     for a, b in zip(one["energy"], two["energy"]):
         assert abs(a[0] - b[0]) <= 1e-7 * abs(a[0]) and abs(a[1] - b[1]) <= 1e-7 * abs(a[1]), (a, b)

@@ -170,18 +170,29 @@ def test_native_mg_same_solution(sim_cls, name, kw):
     assert cyc_native <= 12, (cyc_native, cyc_ref)
 
 
-def test_native_mg_graph_replay(sim_cls):
+@pytest.mark.parametrize("case,coarse", [("3d", 0), ("3d", 1), ("c2", 1)])
+def test_native_mg_graph_replay(sim_cls, case, coarse):
     """multigrid:graph=1 (the V-cycle captured once into a HIP graph and
     replayed) gives the solution and cycle count of direct launches over
-    several steps (the graph is reused across solves).  The kernels are the
-    same; the deposit's atomics make rho differ by rounding between any two
-    runs, so phi is compared to 1e-9 of its scale and the cycle count to 1."""
-    cfg = configs.config("warm", true_size=(32, 32, 64), ppc=8, nalloc_pc=16, levels=4)
-    cfg["multigrid"]["native"] = "1"
+    several steps (the graph is reused across solves).  coarse = 1: with the
+    exact level-1 solve (multigrid:spectralCoarse), whose rocFFT execution
+    and copies are captured into the graph too; "c2" is the
+    bench's C2 line (2-D 128^2, graph and spectral coarse solve on).  The
+    kernels are the same; the deposit's atomics make rho differ by rounding
+    between any two runs, so phi is compared to 1e-9 of its scale and the
+    cycle count to 1."""
+    if case == "c2":
+        cfg = configs.bench_config("c2", 128)
+        kw = dict(perturb=True)
+    else:
+        cfg = configs.config("warm", true_size=(32, 32, 64), ppc=8, nalloc_pc=16, levels=4)
+        cfg["multigrid"]["native"] = "1"
+        cfg["multigrid"]["spectralCoarse"] = str(coarse)
+        kw = dict(maxwell=True, perturb=False, seed=3)
     out = {}
     for graph in ("0", "1"):
         cfg["multigrid"]["graph"] = graph
-        with sim_cls(configs.write_ini(cfg), maxwell=True, perturb=False, seed=3) as s:
+        with sim_cls(configs.write_ini(cfg), **kw) as s:
             s.init()
             for _ in range(3):
                 s.step()
