@@ -219,6 +219,7 @@ int main(int argc, char **argv) {
 	timed("cp_push", 2.0 * 6 * n6 * 8, [&] { cp_push<<<grid, kT>>>(six, n6); });
 	// the same with a grid of one block per 1024 particles (the push's launch)
 	timed("cp_pair32_chunks", 2.0 * 6 * n6 * 8, [&] { cp_pair32<<<(unsigned)(n6 / 1024), kT>>>(six, n6); });
+	timed("cp_push_chunks", 2.0 * 6 * n6 * 8, [&] { cp_push<<<(unsigned)(n6 / 1024), kT>>>(six, n6); });
 	CHECK(hipDeviceSynchronize());
 	CHECK(hipFree(a));
 	CHECK(hipFree(b));
