@@ -1299,7 +1299,6 @@ constexpr int kPushGroups = PINC_PUSH_GROUPS;
 #ifndef PINC_PUSH_THREADS
 #define PINC_PUSH_THREADS 256
 #endif
-
 constexpr int kPushThreads = PINC_PUSH_THREADS;
 constexpr int kPushItems = PINC_PUSH_ITEMS;  // particles per thread, in lane-contiguous pairs
 constexpr int kPushChunk = kPushThreads * kPushItems;  // particles per block (PINC_CHUNK / 2 by default)
@@ -1609,25 +1608,6 @@ __device__ __forceinline__ int brick_key(const TileGeo &tg, const BrickBox &bb, 
 }
 
 typedef double dvec2 __attribute__((ext_vector_type(2)));
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-
-// Particle streams through buffer instructions: the resource (base address
-// of the block's first particle, scalar registers) plus one 32-bit byte
-// offset per lane shared by all six arrays, instead of a 64-bit address per
-// array and lane (PINC_PUSH_BUF; 0: global loads and stores)
-#ifndef PINC_PUSH_BUF
-#define PINC_PUSH_BUF 1
-#endif
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const double *p) {
-	// stride 0, 2^31 - 1 bytes in range, dword 3 of the gfx9 family
-	return __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(p), (short)0, 0x7fffffff, 0x00020000);
-}
-__device__ __forceinline__ dvec2 buf_load2(const double *p, int byteOff) {
-	return __builtin_bit_cast(dvec2, __builtin_amdgcn_raw_buffer_load_b128(buf_rsrc(p), byteOff, 0, 0));
-}
-__device__ __forceinline__ void buf_store2(dvec2 v, double *p, int byteOff) {
-	__builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), buf_rsrc(p), byteOff, 0, 0);
-}
 
 // OBJ: the object test of the fused collection (separate instances, so the
 // plain push carries none of its code)
@@ -1678,14 +1658,10 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	// array and thread: a wave instruction covers every other 16 B of 2 KB,
 	// the next one the rest, through L2), so a thread's particles mostly share
 	// a cell and their charge is summed in the thread before the LDS adds
-	auto item = [&](int k) -> int { return kPushItems * (int)threadIdx.x + k; };
+	auto item = [&](int k) -> long { return base + (long)(kPushItems * threadIdx.x + k); };
 #else
-	auto item = [&](int k) -> int { return (k >> 1) * (2 * kPushThreads) + 2 * (int)threadIdx.x + (k & 1); };
+	auto item = [&](int k) -> long { return base + (long)((k >> 1) * (2 * kPushThreads) + 2 * threadIdx.x + (k & 1)); };
 #endif
-	// item indices are 32-bit offsets from the block's first particle: the
-	// 64-bit base is block-uniform (scalar registers), so no per-lane 64-bit
-	// index stays live through the kernel
-	const int nloc = (int)min((long)kPushChunk, a.n - base);
 	// pairs are 16-B aligned when every species array is (the species
 	// offset iStart is even); otherwise one 8-B access per particle
 	bool al = true;
@@ -1702,34 +1678,29 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	static_assert(kPushItems % 2 == 0, "items come in pairs");
 #pragma unroll
 	for (int k = 0; k < kPushItems; k += 2) {
-		const int i = item(k);
-		const bool ok0 = i < nloc, ok1 = i + 1 < nloc;
+		const long i = item(k);
+		const bool ok0 = i < a.n, ok1 = i + 1 < a.n;
 		valid |= ((unsigned)ok0 | (unsigned)ok1 << 1) << k;
 #pragma unroll
 		for (int d = 0; d < ND; d++) {
 			if (ok1 && al) {
 				// streamed once per step (far beyond L2/MALL): non-temporal
 #if PINC_PUSH_CONSEC
-#if PINC_PUSH_BUF
-				const dvec2 x = buf_load2(a.xi[d] + base, 8 * i);
-				const dvec2 v = buf_load2(a.vi[d] + base, 8 * i);
+				const dvec2 x = *reinterpret_cast<const dvec2 *>(a.xi[d] + i);
+				const dvec2 v = *reinterpret_cast<const dvec2 *>(a.vi[d] + i);
 #else
-				const dvec2 x = *reinterpret_cast<const dvec2 *>(a.xi[d] + base + i);
-				const dvec2 v = *reinterpret_cast<const dvec2 *>(a.vi[d] + base + i);
-#endif
-#else
-				const dvec2 x = __builtin_nontemporal_load(reinterpret_cast<const dvec2 *>(a.xi[d] + base + i));
-				const dvec2 v = __builtin_nontemporal_load(reinterpret_cast<const dvec2 *>(a.vi[d] + base + i));
+				const dvec2 x = __builtin_nontemporal_load(reinterpret_cast<const dvec2 *>(a.xi[d] + i));
+				const dvec2 v = __builtin_nontemporal_load(reinterpret_cast<const dvec2 *>(a.vi[d] + i));
 #endif
 				p[k][d] = x.x;
 				p[k + 1][d] = x.y;
 				vv[k][d] = v.x;
 				vv[k + 1][d] = v.y;
 			} else {
-				p[k][d] = ok0 ? a.xi[d][base + i] : 1.0;
-				vv[k][d] = ok0 ? a.vi[d][base + i] : 0.0;
-				p[k + 1][d] = ok1 ? a.xi[d][base + i + 1] : 1.0;
-				vv[k + 1][d] = ok1 ? a.vi[d][base + i + 1] : 0.0;
+				p[k][d] = ok0 ? a.xi[d][i] : 1.0;
+				vv[k][d] = ok0 ? a.vi[d][i] : 0.0;
+				p[k + 1][d] = ok1 ? a.xi[d][i + 1] : 1.0;
+				vv[k + 1][d] = ok1 ? a.vi[d][i + 1] : 0.0;
 			}
 #pragma unroll
 			for (int h = 0; h < 2; h++) {
@@ -1911,28 +1882,33 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 		eoffs[c] = o * ND;
 	}
 	double ke = 0.0;
-	int bad = 0;
+	int cnt = 0, bad = 0;
 	unsigned dep = 0;
-	// kick of item k (puAcc3D1KE / puAccND1KE, pusher.c:178-265): E of the
-	// cell's 2^ND corners from the staged box (lds) or from global memory
-	auto kick = [&](int k, bool lds) {
-		double dec[3], comp[3];
-		int j[3] = {0, 0, 0};
 #pragma unroll
-		for (int d = 0; d < ND; d++) {
-			j[d] = (int)p[k][d];
-			dec[d] = p[k][d] - j[d];
-			comp[d] = 1 - dec[d];
-		}
-		double dv[ND];
-		{
+	for (int k = 0; k < kPushItems; k++) {
+		if (!((valid >> k) & 1u)) continue;
+		const long i = item(k);
+		if (KICK) {
+			double dec[3], comp[3];
+			int j[3] = {0, 0, 0};
+#pragma unroll
+			for (int d = 0; d < ND; d++) {
+				j[d] = (int)p[k][d];
+				dec[d] = p[k][d] - j[d];
+				comp[d] = 1 - dec[d];
+			}
+			// all 2^ND corners in the staged box: one unsigned compare per
+			// dimension, evaluated without short-circuit branches
+			bool inE = eB.vol > 0;
+#pragma unroll
+			for (int d = 0; d < ND; d++) inE &= (unsigned)(j[d] - eB.lo[d]) < (unsigned)(eB.n[d] - 1);
 			double e[NC][ND];
 			if (PINC_PUSH_SKIP & 2) {
 #pragma unroll
 				for (int c = 0; c < NC; c++)
 #pragma unroll
 					for (int q = 0; q < ND; q++) e[c][q] = 0.0;
-			} else if (lds) {
+			} else if (inE) {
 				const double *eb = eL + mul24(eB.index(j, ND), ND);
 #pragma unroll
 				for (int c = 0; c < NC; c++)
@@ -1952,6 +1928,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 					for (int q = 0; q < ND; q++) e[c][q] = ep[q];
 				}
 			}
+			double dv[ND];
 			if (V3D) {
 				// puInterp3D1 (pusher.c:1116-1120), corner c = x + 2y + 4z
 				double x = dec[0], y = dec[1], z = dec[2];
@@ -1981,40 +1958,14 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 					}
 				}
 			}
+			double vsq = 0;
+#pragma unroll
+			for (int d = 0; d < ND; d++) {
+				vsq += vv[k][d] * (vv[k][d] + dv[d]);
+				vv[k][d] = vv[k][d] + dv[d];
+			}
+			ke += vsq;
 		}
-		double vsq = 0;
-#pragma unroll
-		for (int d = 0; d < ND; d++) {
-			vsq += vv[k][d] * (vv[k][d] + dv[d]);
-			vv[k][d] = vv[k][d] + dv[d];
-		}
-		ke += vsq;
-	};
-	if (KICK) {
-		// items whose 2^ND corners all lie in the staged box first (one
-		// unsigned compare per dimension, no short-circuit branches); the
-		// others (far movers, wrapped particles, an untrimmable box) after
-		// them, in a loop a wave skips unless one of its lanes needs it
-		unsigned slow = 0;
-#pragma unroll
-		for (int k = 0; k < kPushItems; k++) {
-			if (!((valid >> k) & 1u)) continue;
-			bool inE = eB.vol > 0;
-#pragma unroll
-			for (int d = 0; d < ND; d++) inE &= (unsigned)((int)p[k][d] - eB.lo[d]) < (unsigned)(eB.n[d] - 1);
-			if (inE) kick(k, true);
-			else slow |= 1u << k;
-		}
-		if (__ballot(slow != 0)) {
-#pragma unroll
-			for (int k = 0; k < kPushItems; k++)
-				if ((slow >> k) & 1u) kick(k, false);
-		}
-	}
-#pragma unroll
-	for (int k = 0; k < kPushItems; k++) {
-		if (!((valid >> k) & 1u)) continue;
-		const int i = item(k);
 		// drift + pVelAssertMax (population.c:342-365)
 		int chg = 0;
 #pragma unroll
@@ -2066,37 +2017,36 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 			                     : kPushChunk + k * kPushThreads + (int)threadIdx.x;
 			stageF[t] = (unsigned char)ne;
 		}
-		if (!SORT) a.flags[base + i] = (unsigned char)ne;
-		if (ne == a.center) dep |= (1u | (unsigned)chg << 16) << k;  // bits 16+: changed cell
+		if (!SORT) a.flags[i] = (unsigned char)ne;
+		if (ne != a.center) {
+			if (!SORT) cnt++;
+		} else {
+			dep |= (1u | (unsigned)chg << 16) << k;  // bits 16+: changed cell
+		}
 	}
 	if (!SORT) {
 		// positions (and velocities if kicked or moved) in pairs
 		const bool wv = KICK || a.vo[0] != a.vi[0];
 #pragma unroll
 		for (int k = 0; k < kPushItems; k += 2) {
-			const int i = item(k);
+			const long i = item(k);
 			const bool ok0 = (valid >> k) & 1u, ok1 = (valid >> (k + 1)) & 1u;
 #pragma unroll
 			for (int d = 0; d < ND; d++) {
 				if (ok1 && al) {
 #if PINC_PUSH_CONSEC
-#if PINC_PUSH_BUF
-					buf_store2(dvec2{p[k][d], p[k + 1][d]}, a.xo[d] + base, 8 * i);
-					if (wv) buf_store2(dvec2{vv[k][d], vv[k + 1][d]}, a.vo[d] + base, 8 * i);
+					*reinterpret_cast<dvec2 *>(a.xo[d] + i) = dvec2{p[k][d], p[k + 1][d]};
+					if (wv) *reinterpret_cast<dvec2 *>(a.vo[d] + i) = dvec2{vv[k][d], vv[k + 1][d]};
 #else
-					*reinterpret_cast<dvec2 *>(a.xo[d] + base + i) = dvec2{p[k][d], p[k + 1][d]};
-					if (wv) *reinterpret_cast<dvec2 *>(a.vo[d] + base + i) = dvec2{vv[k][d], vv[k + 1][d]};
-#endif
-#else
-					__builtin_nontemporal_store(dvec2{p[k][d], p[k + 1][d]}, reinterpret_cast<dvec2 *>(a.xo[d] + base + i));
+					__builtin_nontemporal_store(dvec2{p[k][d], p[k + 1][d]}, reinterpret_cast<dvec2 *>(a.xo[d] + i));
 					if (wv)
-						__builtin_nontemporal_store(dvec2{vv[k][d], vv[k + 1][d]}, reinterpret_cast<dvec2 *>(a.vo[d] + base + i));
+						__builtin_nontemporal_store(dvec2{vv[k][d], vv[k + 1][d]}, reinterpret_cast<dvec2 *>(a.vo[d] + i));
 #endif
 				} else {
-					if (ok0) a.xo[d][base + i] = p[k][d];
-					if (ok0 && wv) a.vo[d][base + i] = vv[k][d];
-					if (ok1) a.xo[d][base + i + 1] = p[k + 1][d];
-					if (ok1 && wv) a.vo[d][base + i + 1] = vv[k + 1][d];
+					if (ok0) a.xo[d][i] = p[k][d];
+					if (ok0 && wv) a.vo[d][i] = vv[k][d];
+					if (ok1) a.xo[d][i + 1] = p[k + 1][d];
+					if (ok1 && wv) a.vo[d][i + 1] = vv[k + 1][d];
 				}
 			}
 		}
@@ -2112,7 +2062,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 			for (int k = 0; k < kPushItems; k++) {
 				slot[k] = -1;
 				if (!((valid >> k) & 1u)) continue;
-				const int i = item(k);
+				const long i = item(k);
 				const int r = rlL[k * kPushThreads + threadIdx.x];
 				if (r >= 0) {
 					const int l = r & 255, rank = r >> 9;
@@ -2120,7 +2070,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 					slot[k] = (br ? bCnt[l] : locStart[l]) + rank;
 					const int o = (br ? bBase[l] : cntIn[l]) + rank;
 					gdst[slot[k]] = o;
-					a.perm[base + i] = o;
+					a.perm[i] = o;
 				} else {
 					const long o = ~r;
 #pragma unroll
@@ -2130,7 +2080,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 					}
 					const int f = stageF[kPushChunk + k * kPushThreads + threadIdx.x];
 					a.flags[o] = (unsigned char)f;
-					a.perm[base + i] = (int)o;
+					a.perm[i] = (int)o;
 					if (f != a.center) atomicAdd(&a.chunkCount[o / PINC_CHUNK], 1);
 				}
 			}
@@ -2178,8 +2128,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	}
 	if (bad) atomicOr(a.err, bad);
 	if (!SORT) {
-		// items that leave (ne != center): the valid ones not kept in dep
-		int wc = wave_sum(__popc(valid) - __popc(dep & 0xffffu));
+		int wc = wave_sum(cnt);
 		if (lane == 0) wcnt[wv] = wc;
 	}
 	if (a.moved) {

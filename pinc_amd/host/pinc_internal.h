@@ -80,8 +80,6 @@ struct PincDevPop {
 	 * adds the immigrants and combines */
 	int fused;
 	int pending;                        /* altX holds the positions after the next move */
-	int vout;                           /* a kicking push writes its velocities to altV (population:velocityOut) */
-	int pendingV;                       /* ... and the pending push did: the kicked velocities are in altV */
 	int depValid;                       /* rhoS holds the last move's deposits */
 	int depExtracted;                   /* ... and extract ran since (depEnd valid) */
 	long depEnd[PINC_MAX_SPECIES];      /* particles [iStart, depEnd) are in rhoS */

@@ -111,14 +111,6 @@ Population *pAlloc(const dictionary *ini) {
 			for (int s = 0; s < PINC_MAX_SPECIES; s++) dv->sortNext[s] = 1;
 		}
 	}
-	/* population:velocityOut (fused push): the kicked velocities go to the
-	 * second buffer like the moved positions, instead of back in place
-	 * (tools/pmc_calibrate.hip: the push's streams run at 5.1 TB/s with
-	 * every output in a buffer of its own, 4.4 TB/s with the velocities
-	 * rewritten in place) */
-	dv->vout = (dv->tiled || dv->fused) && dv->fused &&
-	           (iniHas(ini, "population:velocityOut") ? iniGetInt(ini, "population:velocityOut")
-	                                                 : (getenv("PINC_PUSH_VOUT") ? atoi(getenv("PINC_PUSH_VOUT")) : 0));
 	if (dv->tiled || dv->fused) {
 		for (int d = 0; d < nd; d++) {
 			pinc_check(pinc_hip_malloc((void **)&dv->altX[d], cap * sizeof(double)), "pAlloc pos (tiled)");
@@ -360,12 +352,10 @@ void pSyncToHost(Population *p) {
 		 * slot order; read them back in the current order through perm */
 		if (dv->pending && dv->pendingSorted)
 			pinc_check(pinc_hip_malloc((void **)&dtmp, n * sizeof(double)), "pSyncToHost tmp");
-		/* an unsorted one with population:velocityOut: in altV, same order */
-		const int inAlt = dv->pending && dv->pendingV && !dv->pendingSorted;
 		for (int d = 0; d < nd; d++) {
 			pinc_check(pinc_hip_d2h(tmp, dv->p.x[d] + a, n * sizeof(double), g_pinc.stream), "pSyncToHost");
 			for (long i = 0; i < n; i++) p->pos[(a + i) * nd + d] = tmp[i];
-			const double *vsrc = (inAlt ? dv->altV[d] : dv->p.v[d]) + a;
+			const double *vsrc = dv->p.v[d] + a;
 			if (dtmp) {
 				pinc_check(pinc_hip_gather_perm(dv->altV[d] + a, dv->perm + a, n, dtmp, g_pinc.stream), "pSyncToHost");
 				vsrc = dtmp;
@@ -383,7 +373,7 @@ void pSyncToDevice(Population *p) {
 	int nd = p->nDims;
 	PincDevPop *dv = p->dev;
 	/* new particles: a pending fused move and its deposits no longer apply */
-	dv->pending = dv->pendingSorted = dv->pendingV = dv->depValid = dv->depExtracted = 0;
+	dv->pending = dv->pendingSorted = dv->depValid = dv->depExtracted = 0;
 	dv->everSorted = 0;
 	for (int s = 0; s < PINC_MAX_SPECIES; s++) {
 		dv->cntValid[s] = 0;

@@ -255,8 +255,7 @@ static void push_phase_report(const unsigned long long *dts, const unsigned long
  * xout, velocities in place.  Tiled layout: every sortInterval-th push writes
  * its output in cell order instead (to altX/altV, counting sort on the cell
  * counts of its input), and the push before it counts those cells.  Returns
- * 1 if this push sorted, | 2 if its velocities went to altV (sorted, or
- * population:velocityOut). */
+ * 1 if this push sorted. */
 static int push_all(Population *pop, Grid *E, double *const *xout) {
 	PincDevPop *dv = pop->dev;
 	pinc_geom_t g = dv->geom;
@@ -296,9 +295,6 @@ static int push_all(Population *pop, Grid *E, double *const *xout) {
 		dv->everSorted = 1;
 	}
 	int nd = pop->nDims;
-	/* population:velocityOut: a kicking push that does not sort writes its
-	 * velocities to altV as well (all species: the buffers swap together) */
-	const int voutNow = E && dv->vout && !sortNow;
 	if (adaptive)
 		pinc_check(pinc_hip_memset(dv->movedCnt, 0, PINC_MAX_SPECIES * sizeof(unsigned long long), g_pinc.stream),
 		           "moved counts");
@@ -320,7 +316,7 @@ static int push_all(Population *pop, Grid *E, double *const *xout) {
 		long chunks = dv->chunkBase[s + 1] - dv->chunkBase[s];
 		for (int d = 0; d < 3; d++) {
 			a.xout[d] = sortNow ? dv->altX[d] : xout[d];
-			a.vout[d] = (sortNow || voutNow) ? dv->altV[d] : dv->p.v[d];
+			a.vout[d] = sortNow ? dv->altV[d] : dv->p.v[d];
 		}
 		a.rhoS = dv->rhoS[s];
 		a.thr = g_pinc.thr;
@@ -420,7 +416,7 @@ static int push_all(Population *pop, Grid *E, double *const *xout) {
 	}
 	dv->depValid = 1;
 	dv->depExtracted = 0;
-	return sortNow | (sortNow || voutNow) << 1;
+	return sortNow;
 }
 
 static void swap_pos(PincDevPop *dv, int nd, int vel) {
@@ -443,13 +439,6 @@ static void classify(Population *pop, int doMove) {
 	if (!doMove && dv->pending) {
 		/* flags recomputed for the current positions: drop the pending move
 		 * (a sorted one first puts the kicked velocities back in order) */
-		if (dv->pendingV && !dv->pendingSorted)
-			/* population:velocityOut: the kicked velocities, in order, in altV */
-			for (int d = 0; d < nd; d++) {
-				double *t = dv->p.v[d];
-				dv->p.v[d] = dv->altV[d];
-				dv->altV[d] = t;
-			}
 		if (dv->pendingSorted)
 			for (int s = 0; s < pop->nSpecies; s++)
 				for (int d = 0; d < nd; d++)
@@ -457,7 +446,7 @@ static void classify(Population *pop, int doMove) {
 					                                pop->iStop[s] - pop->iStart[s], dv->p.v[d] + pop->iStart[s],
 					                                g_pinc.stream),
 					           "unsort velocities");
-		dv->pending = dv->pendingSorted = dv->pendingV = 0;
+		dv->pending = dv->pendingSorted = 0;
 		/* its object counts go with it */
 		if (dv->objCount)
 			pinc_check(pinc_hip_memset(dv->objCount, 0, (long)PINC_MAX_SPECIES * dv->objK * sizeof(int), g_pinc.stream),
@@ -465,8 +454,8 @@ static void classify(Population *pop, int doMove) {
 	}
 	if (doMove && dv->pending) {
 		/* the fused puAcc already moved, classified and deposited */
-		swap_pos(dv, nd, dv->pendingV);
-		dv->pending = dv->pendingSorted = dv->pendingV = 0;
+		swap_pos(dv, nd, dv->pendingSorted);
+		dv->pending = dv->pendingSorted = 0;
 		dv->flagsValid = 1;
 		dv->depValid = 1;
 		dv->depExtracted = 0;
@@ -474,7 +463,7 @@ static void classify(Population *pop, int doMove) {
 	}
 	if (doMove && !dv->sorted) maybe_sort(pop);
 	if (doMove && dv->fused) {
-		if (push_all(pop, NULL, dv->p.x) & 1) swap_pos(dv, nd, 1);
+		if (push_all(pop, NULL, dv->p.x)) swap_pos(dv, nd, 1);
 		dv->flagsValid = 1;
 		return;
 	}
@@ -743,9 +732,7 @@ static void acc(Population *pop, Grid *E, int ke) {
 		 * deposit ride along (positions to altX, swapped in by puMove) */
 		if (!dv->sorted) maybe_sort(pop);
 		dv->pending = 0;
-		const int r = push_all(pop, E, dv->altX);
-		dv->pendingSorted = r & 1;
-		dv->pendingV = (r >> 1) & 1;
+		dv->pendingSorted = push_all(pop, E, dv->altX);
 		dv->pending = 1;
 		dv->flagsValid = 0;
 		if (ke) {

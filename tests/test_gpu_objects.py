@@ -271,6 +271,9 @@ def test_reference_masks_match_checker(built, name):
     T = tuple(reversed(mask.shape))
     cfg = configs.config("cold3d", true_size=T, nsub=(1, 1, 1))
     cfg["multigrid"]["mgLevels"] = "3"
+    # native multigrid on both sides (oracle/orc_native.c): the same object
+    # operators with ~4 instead of ~20 V-cycles per capacitance column
+    cfg["multigrid"]["native"] = "1"
     cfg["population"]["fused"] = "0"
     cfg["population"]["nParticles"] = "8 pc"
     cfg["population"]["nAlloc"] = "12 pc"
@@ -316,6 +319,7 @@ def test_reference_masks_64_green_equals_solve(built, name):
     for mode in ("solve", "green"):
         cfg = configs.config("cold3d", true_size=T, nsub=(1, 1, 1))
         cfg["multigrid"]["mgLevels"] = "4"
+        cfg["multigrid"]["native"] = "1"   # ~4 V-cycles per capacitance column
         cfg["population"]["fused"] = "0"
         cfg["population"]["nParticles"] = "4 pc"
         cfg["population"]["nAlloc"] = "6 pc"
