@@ -967,6 +967,27 @@ __global__ __launch_bounds__(kThreads) void k_sort_count(const double *__restric
 	}
 }
 
+// the sorting push's key counts: per brick, at the brick's first key (the
+// push reserves per brick; immigrants joining the counts, or counts made
+// without a counting push)
+template <int ND>
+__global__ __launch_bounds__(kThreads) void k_count_bricks(const double *__restrict__ x0,
+                                                           const double *__restrict__ x1,
+                                                           const double *__restrict__ x2, long n,
+                                                           TileGeo tg, int *__restrict__ counts) {
+	const double *xs[3] = {x0, x1, x2};
+	for (long base = (long)blockIdx.x * blockDim.x; base < n; base += (long)gridDim.x * blockDim.x) {
+		long i = base + threadIdx.x;
+		bool act = i < n;
+		int c[3] = {0, 0, 0};
+		if (act) {
+#pragma unroll
+			for (int d = 0; d < ND; d++) c[d] = (int)xs[d][i];
+		}
+		agg_add(counts, act ? brick_first_key<ND>(tg, c) : 0, act);
+	}
+}
+
 template <int ND>
 __global__ __launch_bounds__(kThreads) void k_sort_scatter(pinc_pop_t in, pinc_pop_t out, long b0, long n,
                                                            TileGeo tg, int *__restrict__ cursor) {
@@ -1753,6 +1774,10 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	const Box rB = !empty ? make_box(clo, chi, cmid, 1, 2, ND, kRhoBoxCap) : Box{{0, 0, 0}, {1, 1, 1}, 0};
 	const Box iB = (SORT && !empty) ? make_box(clo, chi, cmid, 0, 0, ND, kInCellCap) : Box{{0, 0, 0}, {1, 1, 1}, 0};
 	const Box oB = (a.cntNext && !empty) ? make_box(clo, chi, cmid, 1, 1, ND, kOutCellCap) : Box{{0, 0, 0}, {1, 1, 1}, 0};
+	// the sorting push reserves per brick from the cursor of the brick's
+	// first cell, so the counting push counts per brick (at its first key):
+	// a block's output falls into a few bricks, where it spans tens of cells
+	const BrickBox obb = (a.cntNext && !empty) ? make_brick_box<ND>(a.tg, oB) : BrickBox{{0, 0, 0}, {1, 1, 1}, 0};
 	// sorting push: the items of the cell box iB are ranked by cell, the
 	// others inside the wide brick box ib by brick (one run of each brick per
 	// block, the brick's own items first); only items outside both take a
@@ -2114,16 +2139,16 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	}
 	PUSH_TS(5);
 	if (a.cntNext) {
-		// count the output cells of the particles that stay (next push's sort)
+		// count the output bricks of the particles that stay (next push's sort)
 #pragma unroll
 		for (int k = 0; k < kPushItems; k++) {
 			const bool mine = (dep >> k) & 1u;
 			int c[3] = {0, 0, 0};
 #pragma unroll
 			for (int d = 0; d < ND; d++) c[d] = (int)p[k][d];
-			const bool inB = mine && oB.inside(c, ND);
-			lds_agg_add<false>(cntOut, inB ? oB.index(c, ND) : 0, inB);
-			if (mine && !inB) atomicAdd(&a.cntNext[tile_key_cells<ND>(a.tg, c)], 1);
+			const int lb = mine ? brick_inside<ND>(a.tg, obb, c) : -1;
+			lds_agg_add<false>(cntOut, lb < 0 ? 0 : lb, lb >= 0);
+			if (mine && lb < 0) atomicAdd(&a.cntNext[brick_first_key<ND>(a.tg, c)], 1);
 		}
 	}
 	if (bad) atomicOr(a.err, bad);
@@ -2329,12 +2354,9 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 		unsafeAtomicAdd(&a.rho[(unsigned)off], v);
 	}
 	if (a.cntNext) {
-		for (int t = threadIdx.x; t < oB.vol; t += kPushThreads) {
+		for (int t = threadIdx.x; t < obb.vol; t += kPushThreads) {
 			int m = cntOut[t];
-			if (!m) continue;
-			int c[3] = {0, 0, 0};
-			oB.coords(t, c, ND);
-			atomicAdd(&a.cntNext[tile_key_cells<ND>(a.tg, c)], m);
+			if (m) atomicAdd(&a.cntNext[brick_key<ND>(a.tg, obb, t)], m);
 		}
 	}
 	PUSH_TS(7);
@@ -2784,9 +2806,9 @@ extern "C" int pinc_hip_count_keys(pinc_pop_t pop, int s, long first, pinc_geom_
 	int nd = g.nd;
 	const double *x0 = pop.x[0] + b0, *x1 = nd > 1 ? pop.x[1] + b0 : nullptr, *x2 = nd > 2 ? pop.x[2] + b0 : nullptr;
 	hipStream_t st = (hipStream_t)stream;
-	if (nd == 3) hipLaunchKernelGGL(k_sort_count<3>, dim3(nb), dim3(kThreads), 0, st, x0, x1, x2, n, tg, counts);
-	else if (nd == 2) hipLaunchKernelGGL(k_sort_count<2>, dim3(nb), dim3(kThreads), 0, st, x0, x1, x2, n, tg, counts);
-	else hipLaunchKernelGGL(k_sort_count<1>, dim3(nb), dim3(kThreads), 0, st, x0, x1, x2, n, tg, counts);
+	if (nd == 3) hipLaunchKernelGGL(k_count_bricks<3>, dim3(nb), dim3(kThreads), 0, st, x0, x1, x2, n, tg, counts);
+	else if (nd == 2) hipLaunchKernelGGL(k_count_bricks<2>, dim3(nb), dim3(kThreads), 0, st, x0, x1, x2, n, tg, counts);
+	else hipLaunchKernelGGL(k_count_bricks<1>, dim3(nb), dim3(kThreads), 0, st, x0, x1, x2, n, tg, counts);
 	return check_launch("count_keys");
 }
 
