@@ -1639,7 +1639,9 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	// the sorting push keeps its LDS at 40 KB (4 blocks per CU): fewer copies
 	constexpr int RL = SORT ? 1024 : kRhoLds;
 	__shared__ double rhoL[RL];
-	__shared__ double eL[KICK ? kEBoxCap * ND : 1];
+	// staged E box: 3-D (E_x, E_y) pairs at eL[2t] (one ds_read_b128 per
+	// corner) and E_z at eL[2 cap + t], else value-major
+	__shared__ __attribute__((aligned(16))) double eL[KICK ? kEBoxCap * ND : 1];
 	__shared__ int cntIn[SORT ? kInCellCap : 1];
 	__shared__ int cntOut[kOutCellCap];
 	__shared__ int red[3 * 3 * NW];
@@ -1723,6 +1725,12 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 				p[k + 1][d] = ok1 ? a.xi[d][i + 1] : 1.0;
 				vv[k + 1][d] = ok1 ? a.vi[d][i + 1] : 0.0;
 			}
+		}
+	}
+#pragma unroll
+	for (int k = 0; k < kPushItems; k += 2) {
+#pragma unroll
+		for (int d = 0; d < ND; d++) {
 #pragma unroll
 			for (int h = 0; h < 2; h++) {
 				if ((valid >> (k + h)) & 1u) {
@@ -1813,8 +1821,14 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 				off += o0;
 			}
 			const double *ep = a.Es + (unsigned)(off * ND);
+			if constexpr (ND == 3) {
+				eL[2 * t] = ep[0];
+				eL[2 * t + 1] = ep[1];
+				eL[2 * kEBoxCap + t] = ep[2];
+			} else {
 #pragma unroll
-			for (int q = 0; q < ND; q++) eL[t * ND + q] = ep[q];
+				for (int q = 0; q < ND; q++) eL[t * ND + q] = ep[q];
+			}
 		}
 	}
 	__syncthreads();
@@ -1904,7 +1918,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 			o += ((c >> d) & 1) ? st : 0;
 			st *= eB.n[d];
 		}
-		eoffs[c] = o * ND;
+		eoffs[c] = ND == 3 ? o : o * ND;
 	}
 	double ke = 0.0;
 	int cnt = 0, bad = 0;
@@ -1927,42 +1941,82 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 			bool inE = eB.vol > 0;
 #pragma unroll
 			for (int d = 0; d < ND; d++) inE &= (unsigned)(j[d] - eB.lo[d]) < (unsigned)(eB.n[d] - 1);
-			double e[NC][ND];
-			if (PINC_PUSH_SKIP & 2) {
-#pragma unroll
-				for (int c = 0; c < NC; c++)
-#pragma unroll
-					for (int q = 0; q < ND; q++) e[c][q] = 0.0;
-			} else if (inE) {
-				const double *eb = eL + mul24(eB.index(j, ND), ND);
-#pragma unroll
-				for (int c = 0; c < NC; c++)
-#pragma unroll
-					for (int q = 0; q < ND; q++) e[c][q] = eb[eoffs[c] + q];
-			} else {
-				int o[3][2];
-#pragma unroll
-				for (int d = 0; d < ND; d++) node_pair(G, d, j[d], o[d][0], o[d][1]);
-#pragma unroll
-				for (int c = 0; c < NC; c++) {
-					int off = 0;
-#pragma unroll
-					for (int d = 0; d < ND; d++) off += o[d][(c >> d) & 1];
-					const double *ep = a.Es + (unsigned)(off * ND);
-#pragma unroll
-					for (int q = 0; q < ND; q++) e[c][q] = ep[q];
-				}
-			}
 			double dv[ND];
-			if (V3D) {
-				// puInterp3D1 (pusher.c:1116-1120), corner c = x + 2y + 4z
-				double x = dec[0], y = dec[1], z = dec[2];
-				double xc = comp[0], yc = comp[1], zc = comp[2];
+			if constexpr (V3D) {
+				// puInterp3D1 (pusher.c:1116-1120), corner c = x + 2y + 4z, one
+				// component at a time (E_x and E_y from one 16-B LDS read per
+				// corner, then E_z): 16 corner values live instead of 24
+				const double x = dec[0], y = dec[1], z = dec[2];
+				const double xc = comp[0], yc = comp[1], zc = comp[2];
+				auto interp = [&](const double *f) -> double {
+					return zc * (yc * (xc * f[0] + x * f[1]) + y * (xc * f[2] + x * f[3])) +
+					       z * (yc * (xc * f[4] + x * f[5]) + y * (xc * f[6] + x * f[7]));
+				};
+				if (PINC_PUSH_SKIP & 2) {
+					dv[0] = dv[1] = dv[2] = 0.0;
+				} else if (inE) {
+					const int ei = eB.index(j, ND);
+					double fx[NC], fy[NC];
 #pragma unroll
-				for (int q = 0; q < ND; q++)
-					dv[q] = zc * (yc * (xc * e[0][q] + x * e[1][q]) + y * (xc * e[2][q] + x * e[3][q])) +
-					        z * (yc * (xc * e[4][q] + x * e[5][q]) + y * (xc * e[6][q] + x * e[7][q]));
+					for (int c = 0; c < NC; c++) {
+						const dvec2 xy = *reinterpret_cast<const dvec2 *>(eL + 2 * (ei + eoffs[c]));
+						fx[c] = xy.x;
+						fy[c] = xy.y;
+					}
+					dv[0] = interp(fx);
+					dv[1] = interp(fy);
+					__builtin_amdgcn_sched_barrier(0);
+					double fz[NC];
+#pragma unroll
+					for (int c = 0; c < NC; c++) fz[c] = eL[2 * kEBoxCap + ei + eoffs[c]];
+					dv[2] = interp(fz);
+				} else {
+					int o[3][2];
+#pragma unroll
+					for (int d = 0; d < ND; d++) node_pair(G, d, j[d], o[d][0], o[d][1]);
+					unsigned off[NC];
+#pragma unroll
+					for (int c = 0; c < NC; c++) {
+						int t = 0;
+#pragma unroll
+						for (int d = 0; d < ND; d++) t += o[d][(c >> d) & 1];
+						off[c] = (unsigned)(t * ND);
+					}
+#pragma unroll
+					for (int q = 0; q < ND; q++) {
+						double f[NC];
+#pragma unroll
+						for (int c = 0; c < NC; c++) f[c] = a.Es[off[c] + q];
+						dv[q] = interp(f);
+					}
+				}
 			} else {
+				double e[NC][ND];
+				if (PINC_PUSH_SKIP & 2) {
+#pragma unroll
+					for (int c = 0; c < NC; c++)
+#pragma unroll
+						for (int q = 0; q < ND; q++) e[c][q] = 0.0;
+				} else if (inE) {
+					const double *eb = eL + mul24(eB.index(j, ND), ND);
+#pragma unroll
+					for (int c = 0; c < NC; c++)
+#pragma unroll
+						for (int q = 0; q < ND; q++) e[c][q] = eb[eoffs[c] + q];
+				} else {
+					int o[3][2];
+#pragma unroll
+					for (int d = 0; d < ND; d++) node_pair(G, d, j[d], o[d][0], o[d][1]);
+#pragma unroll
+					for (int c = 0; c < NC; c++) {
+						int off = 0;
+#pragma unroll
+						for (int d = 0; d < ND; d++) off += o[d][(c >> d) & 1];
+						const double *ep = a.Es + (unsigned)(off * ND);
+#pragma unroll
+						for (int q = 0; q < ND; q++) e[c][q] = ep[q];
+					}
+				}
 				// puInterpND1Inner: corner by corner in the recursion order
 #pragma unroll
 				for (int q = 0; q < ND; q++) dv[q] = 0;
