@@ -1420,8 +1420,20 @@ __device__ __forceinline__ void node_pair(const Geo32 &G, int d, int j, int &o0,
 
 // LDS capacities of the push: E nodes (pre-move cells + 1), charge nodes
 // (post-move cells + 1), input cells and output cells of the sort counters
-constexpr int kEBoxCap = 384;
+// (the sorting push, whose LDS also holds the rank and staging arrays, keeps
+// the smaller boxes).  The unsorted push's boxes take a chunk that straddles
+// two tiles (8 x 4 x 4 cells) after a step of motion ((10 x 6 x 6 cells):
+// 539 E nodes, 1053 charge nodes); with 384 and 1024 such chunks -- a
+// quarter of them -- gathered E and added charge through global memory.
 constexpr int kRhoBoxCap = 1024;
+#ifndef PINC_PUSH_EBOX
+#define PINC_PUSH_EBOX 768
+#endif
+constexpr int kEBoxCapPlain = PINC_PUSH_EBOX;
+#ifndef PINC_PUSH_SORT_EBOX
+#define PINC_PUSH_SORT_EBOX 704
+#endif
+constexpr int kEBoxCapSort = PINC_PUSH_SORT_EBOX;
 constexpr int kInCellCap = 256;
 constexpr int kOutCellCap = 512;
 
@@ -1453,7 +1465,10 @@ struct Box {
 // entries: each dimension first to kBoxReach cells either side of the mean
 // cell mid, then the widest one cell at a time from its side farther from mid
 // (block-uniform; vol 0 if even a single cell does not fit).
-constexpr int kBoxReach = 4;
+#ifndef PINC_PUSH_REACH
+#define PINC_PUSH_REACH 8
+#endif
+constexpr int kBoxReach = PINC_PUSH_REACH;
 __device__ __forceinline__ Box make_box(const int *clo, const int *chi, const int *mid, int grow_lo, int grow_hi,
                                         int nd, int cap) {
 	int lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
@@ -1641,7 +1656,14 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	__shared__ double rhoL[RL];
 	// staged E box: 3-D (E_x, E_y) pairs at eL[2t] (one ds_read_b128 per
 	// corner) and E_z at eL[2 cap + t], else value-major
-	__shared__ __attribute__((aligned(16))) double eL[KICK ? kEBoxCap * ND : 1];
+	constexpr int EC = SORT ? kEBoxCapSort : kEBoxCapPlain;  // E box capacity (nodes)
+	constexpr int RC = SORT ? kRhoBoxCap : RL;              // charge box capacity (nodes)
+	// the sorting push stages its sorted output in the same LDS once the
+	// kick has read E (a barrier separates the last E read from the first
+	// staged write)
+	constexpr int kEL = KICK ? EC * ND : 1, kST = SORT ? kPushChunk : 1;
+	__shared__ __attribute__((aligned(16))) double eLs[kEL > kST ? kEL : kST];
+	double *const eL = eLs;
 	__shared__ int cntIn[SORT ? kInCellCap : 1];
 	__shared__ int cntOut[kOutCellCap];
 	__shared__ int red[3 * 3 * NW];
@@ -1654,7 +1676,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	__shared__ int locStart[SORT ? kInCellCap : 1];
 	__shared__ int rlL[SORT ? kPushChunk : 1];
 	__shared__ int gdst[SORT ? kPushChunk : 1];
-	__shared__ double stage[SORT ? kPushChunk : 1];
+	double *const stage = eLs;
 	__shared__ unsigned char stageF[SORT ? 2 * kPushChunk : 1];
 	const Geo32 G = make_geo32(a.g);
 	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -1778,8 +1800,8 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	// most one cell (|v| <= maxVel <= 1).  Each box is trimmed around the
 	// block's mean cell to its LDS capacity; the items outside it (far movers,
 	// wrapped particles) take the global path.
-	const Box eB = (KICK && !empty) ? make_box(clo, chi, cmid, 0, 1, ND, kEBoxCap) : Box{{0, 0, 0}, {1, 1, 1}, 0};
-	const Box rB = !empty ? make_box(clo, chi, cmid, 1, 2, ND, kRhoBoxCap) : Box{{0, 0, 0}, {1, 1, 1}, 0};
+	const Box eB = (KICK && !empty) ? make_box(clo, chi, cmid, 0, 1, ND, EC) : Box{{0, 0, 0}, {1, 1, 1}, 0};
+	const Box rB = !empty ? make_box(clo, chi, cmid, 1, 2, ND, RC) : Box{{0, 0, 0}, {1, 1, 1}, 0};
 	const Box iB = (SORT && !empty) ? make_box(clo, chi, cmid, 0, 0, ND, kInCellCap) : Box{{0, 0, 0}, {1, 1, 1}, 0};
 	const Box oB = (a.cntNext && !empty) ? make_box(clo, chi, cmid, 1, 1, ND, kOutCellCap) : Box{{0, 0, 0}, {1, 1, 1}, 0};
 	// the sorting push reserves per brick from the cursor of the brick's
@@ -1824,7 +1846,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 			if constexpr (ND == 3) {
 				eL[2 * t] = ep[0];
 				eL[2 * t + 1] = ep[1];
-				eL[2 * kEBoxCap + t] = ep[2];
+				eL[2 * EC + t] = ep[2];
 			} else {
 #pragma unroll
 				for (int q = 0; q < ND; q++) eL[t * ND + q] = ep[q];
@@ -1941,6 +1963,10 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 			bool inE = eB.vol > 0;
 #pragma unroll
 			for (int d = 0; d < ND; d++) inE &= (unsigned)(j[d] - eB.lo[d]) < (unsigned)(eB.n[d] - 1);
+			if (a.diag) {  // (trace: [1] += particles that gather E from memory)
+				const int ng = __popcll(__ballot(!inE));
+				if (lane == 0 && ng) atomicAdd(&a.diag[1], (unsigned long long)ng);
+			}
 			double dv[ND];
 			if constexpr (V3D) {
 				// puInterp3D1 (pusher.c:1116-1120), corner c = x + 2y + 4z, one
@@ -1968,7 +1994,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 					__builtin_amdgcn_sched_barrier(0);
 					double fz[NC];
 #pragma unroll
-					for (int c = 0; c < NC; c++) fz[c] = eL[2 * kEBoxCap + ei + eoffs[c]];
+					for (int c = 0; c < NC; c++) fz[c] = eL[2 * EC + ei + eoffs[c]];
 					dv[2] = interp(fz);
 				} else {
 					int o[3][2];
@@ -2256,6 +2282,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 #pragma unroll
 			for (int c = 0; c < NC; c++) atomicAdd(&rhoL[l0 + coff[c]], w[c]);
 		} else {
+			if (a.diag) atomicAdd(&a.diag[2], 1ull);  // (trace: [2] += runs added to memory)
 #pragma unroll
 			for (int c = 0; c < NC; c++) add_corner_global(j, c, w[c]);
 		}
@@ -2412,6 +2439,12 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 			int m = cntOut[t];
 			if (m) atomicAdd(&a.cntNext[brick_key<ND>(a.tg, obb, t)], m);
 		}
+	}
+	// (trace: the last phase includes every wave's drain of its stores and
+	// atomics)
+	if (a.tstamp) {
+		__builtin_amdgcn_s_waitcnt(0);
+		__syncthreads();
 	}
 	PUSH_TS(7);
 }

@@ -227,12 +227,17 @@ static void ensure_keys(Population *pop) {
 	dv->nKeys = nk;
 }
 
+static int cmp_double(const void *x, const void *y) {
+	const double a = *(const double *)x, b = *(const double *)y;
+	return (a > b) - (a < b);
+}
+
 /* PINC_TRACE_SORT=2: mean per-block time of each push phase (s_memrealtime,
  * 100 MHz) and the kernel's span */
 static void push_phase_report(const unsigned long long *dts, const unsigned long long *ddiag, int nb, int s, int sort,
                               int count) {
 	unsigned long long *t = malloc((size_t)nb * 8 * sizeof(*t));
-	unsigned long long dg[1];
+	unsigned long long dg[3];
 	pinc_check(pinc_hip_d2h(t, dts, (size_t)nb * 8 * sizeof(*t), g_pinc.stream), "push timestamps");
 	pinc_check(pinc_hip_d2h(dg, ddiag, sizeof(dg), g_pinc.stream), "push diagnostics");
 	double ph[7] = {0};
@@ -243,10 +248,55 @@ static void push_phase_report(const unsigned long long *dts, const unsigned long
 		if (t[b * 8 + 7] > t1) t1 = t[b * 8 + 7];
 	}
 	fprintf(stderr, "[pinc] push species %d%s%s: span %.2f ms, per block us: load+box %.2f, lds %.2f, rank %.2f, "
-	        "kick/drift %.2f, sorted stores %.2f, count %.2f, deposit %.2f; global slots %.3g per block\n", s,
+	        "kick/drift %.2f, sorted stores %.2f, count %.2f, deposit %.2f; global slots %.3g, E gathers %.3g, "
+	        "charge runs %.3g per block\n", s,
 	        sort ? " sort" : "",
 	        count ? " count" : "", (t1 - t0) * 1e-5, ph[0] / nb * 1e-2, ph[1] / nb * 1e-2, ph[2] / nb * 1e-2,
-	        ph[3] / nb * 1e-2, ph[4] / nb * 1e-2, ph[5] / nb * 1e-2, ph[6] / nb * 1e-2, (double)dg[0] / nb);
+	        ph[3] / nb * 1e-2, ph[4] / nb * 1e-2, ph[5] / nb * 1e-2, ph[6] / nb * 1e-2, (double)dg[0] / nb,
+	        (double)dg[1] / nb, (double)dg[2] / nb);
+	/* per XCD (the push deals chunks [x q + min(x, r), ...) to XCD x): span
+	 * from its first block's start to its last block's end, and the mean
+	 * number of its blocks between their first and last timestamp */
+	if (g_pinc.traceSort > 2) {
+		const int q = nb / 8, r = nb % 8;
+		fprintf(stderr, "[pinc]   xcd span ms / blocks in flight:");
+		for (int x = 0; x < 8; x++) {
+			const int c0 = x * q + (x < r ? x : r), c1 = c0 + q + (x < r);
+			unsigned long long a0 = ~0ull, a1 = 0;
+			double life = 0;
+			for (int b = c0; b < c1; b++) {
+				if (t[b * 8] < a0) a0 = t[b * 8];
+				if (t[b * 8 + 7] > a1) a1 = t[b * 8 + 7];
+				life += (double)(t[b * 8 + 7] - t[b * 8]);
+			}
+			fprintf(stderr, " %.2f/%.0f", (a1 - a0) * 1e-5, a1 > a0 ? life / (double)(a1 - a0) : 0.0);
+		}
+		fprintf(stderr, "\n");
+		/* block lifetime percentiles (first to last timestamp) */
+		double *lv = malloc((size_t)nb * sizeof(*lv));
+		for (int b = 0; b < nb; b++) lv[b] = (double)(t[b * 8 + 7] - t[b * 8]) * 1e-2;
+		qsort(lv, nb, sizeof(*lv), cmp_double);
+		fprintf(stderr, "[pinc]   block us p10 %.1f p50 %.1f p90 %.1f p99 %.1f max %.1f\n", lv[nb / 10], lv[nb / 2],
+		        lv[nb * 9 / 10], lv[nb * 99 / 100], lv[nb - 1]);
+		/* phases of the blocks above p90 and below p50 */
+		const double p90 = lv[nb * 9 / 10], p50 = lv[nb / 2];
+		double hs[7] = {0}, ls[7] = {0};
+		int nh = 0, nl = 0;
+		for (int b = 0; b < nb; b++) {
+			const double l = (double)(t[b * 8 + 7] - t[b * 8]) * 1e-2;
+			double *acc = l >= p90 ? hs : (l <= p50 ? ls : NULL);
+			if (!acc) continue;
+			for (int k = 0; k < 7; k++) acc[k] += (double)(t[b * 8 + k + 1] - t[b * 8 + k]) * 1e-2;
+			if (l >= p90) nh++;
+			else nl++;
+		}
+		fprintf(stderr, "[pinc]   phases us, slowest 10%%:");
+		for (int k = 0; k < 7; k++) fprintf(stderr, " %.2f", nh ? hs[k] / nh : 0.0);
+		fprintf(stderr, "; fastest 50%%:");
+		for (int k = 0; k < 7; k++) fprintf(stderr, " %.2f", nl ? ls[k] / nl : 0.0);
+		fprintf(stderr, "\n");
+		free(lv);
+	}
 	free(t);
 }
 
@@ -364,8 +414,8 @@ static int push_all(Population *pop, Grid *E, double *const *xout) {
 		int nb = 0;
 		unsigned long long *ts = NULL;
 		if (g_pinc.traceSort > 1) {
-			pinc_check(pinc_hip_malloc((void **)&ts, ((np / 1024 + 1) * 8 + 2) * sizeof(*ts)), "push timestamps");
-			pinc_check(pinc_hip_memset(ts + (np / 1024 + 1) * 8, 0, sizeof(*ts), g_pinc.stream), "push diagnostics");
+			pinc_check(pinc_hip_malloc((void **)&ts, ((np / 1024 + 1) * 8 + 4) * sizeof(*ts)), "push timestamps");
+			pinc_check(pinc_hip_memset(ts + (np / 1024 + 1) * 8, 0, 3 * sizeof(*ts), g_pinc.stream), "push diagnostics");
 			a.tstamp = ts;
 			a.diag = ts + (np / 1024 + 1) * 8;
 		}
