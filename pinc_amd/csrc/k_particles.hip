@@ -1803,11 +1803,14 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	const Box eB = (KICK && !empty) ? make_box(clo, chi, cmid, 0, 1, ND, EC) : Box{{0, 0, 0}, {1, 1, 1}, 0};
 	const Box rB = !empty ? make_box(clo, chi, cmid, 1, 2, ND, RC) : Box{{0, 0, 0}, {1, 1, 1}, 0};
 	const Box iB = (SORT && !empty) ? make_box(clo, chi, cmid, 0, 0, ND, kInCellCap) : Box{{0, 0, 0}, {1, 1, 1}, 0};
-	const Box oB = (a.cntNext && !empty) ? make_box(clo, chi, cmid, 1, 1, ND, kOutCellCap) : Box{{0, 0, 0}, {1, 1, 1}, 0};
 	// the sorting push reserves per brick from the cursor of the brick's
 	// first cell, so the counting push counts per brick (at its first key):
-	// a block's output falls into a few bricks, where it spans tens of cells
-	const BrickBox obb = (a.cntNext && !empty) ? make_brick_box<ND>(a.tg, oB) : BrickBox{{0, 0, 0}, {1, 1, 1}, 0};
+	// a block's output falls into a few bricks.  Only the brick counters live
+	// in LDS, so the cell box they cover may be 16 times their number; a
+	// brick box beyond the counters (far movers) counts in memory.
+	const Box oB = (a.cntNext && !empty) ? make_box(clo, chi, cmid, 1, 1, ND, 16 * kOutCellCap) : Box{{0, 0, 0}, {1, 1, 1}, 0};
+	BrickBox obb = (a.cntNext && !empty) ? make_brick_box<ND>(a.tg, oB) : BrickBox{{0, 0, 0}, {1, 1, 1}, 0};
+	if (obb.vol > kOutCellCap) obb.vol = 0;
 	// sorting push: the items of the cell box iB are ranked by cell, the
 	// others inside the wide brick box ib by brick (one run of each brick per
 	// block, the brick's own items first); only items outside both take a
@@ -1830,7 +1833,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	for (int t = threadIdx.x; t < (PINC_PUSH_COPIES ? nCopy * rStride : rB.vol); t += kPushThreads) rhoL[t] = 0.0;
 	if (SORT)
 		for (int t = threadIdx.x; t < iB.vol; t += kPushThreads) cntIn[t] = 0;
-	for (int t = threadIdx.x; t < (SORT ? kInCellCap : oB.vol); t += kPushThreads) cntOut[t] = 0;
+	for (int t = threadIdx.x; t < (SORT ? kInCellCap : obb.vol); t += kPushThreads) cntOut[t] = 0;
 	if (KICK && !(PINC_PUSH_SKIP & 2)) {
 		for (int t = threadIdx.x; t < eB.vol; t += kPushThreads) {
 			int c[3] = {0, 0, 0};
