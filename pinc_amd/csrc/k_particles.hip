@@ -903,7 +903,6 @@ inline long ceil_div(long a, long b) { return (a + b - 1) / b; }
 struct TileGeo {
 	int tw;         // cells per tile side
 	int nt[3];      // tiles per dimension (cell index (int)p is in [0, T+1])
-	long ts[3];     // tile index stride per dimension
 	int cmax[3];    // largest admissible cell index
 	// bricks of the push's sort: tw^(nd-1) consecutive cell keys of a tile
 	// (tw x tw x 1 in 3-D), bs[d] = log2 of the brick's extent along d (all
@@ -911,22 +910,88 @@ struct TileGeo {
 	int bs[3];
 };
 
-// sort key: tile index (tiles in x-fastest order) then the cell inside the
-// tile (x fastest), so particles of one cell end up contiguous and cells of
-// one tile adjacent
+// Sort key: tile index, then the cell inside the tile.  Tiles run along a
+// serpentine (x rows alternate direction, y columns alternate per z plane),
+// and a tile's layers along the slab dimension run in reverse in odd tiles,
+// so consecutive keys of different tiles are neighbouring cells: a block of
+// particles that straddles two tiles after a sort spans two adjacent bricks
+// (8 x 4 x 1 cells), not a jump of a whole tile row or of the tile's depth.
+// Inside a layer the cells are x fastest, so a brick (one layer of a tile,
+// TileGeo::bs) is a run of consecutive keys.
 template <int ND>
-__device__ __forceinline__ int tile_key(const TileGeo &tg, const double *p) {
-	long tile = 0;
+__device__ __forceinline__ long tile_serp(const TileGeo &tg, const int *t) {
+	if (ND == 1) return t[0];
+	if (ND == 2) return (long)t[1] * tg.nt[0] + ((t[1] & 1) ? tg.nt[0] - 1 - t[0] : t[0]);
+	const int ty = (t[2] & 1) ? tg.nt[1] - 1 - t[1] : t[1];
+	const long r = (long)t[2] * tg.nt[1] + ty;
+	return r * tg.nt[0] + ((r & 1) ? tg.nt[0] - 1 - t[0] : t[0]);
+}
+// inverse of tile_serp
+template <int ND>
+__device__ __forceinline__ void tile_unserp(const TileGeo &tg, long tile, int *t) {
+	t[1] = t[2] = 0;
+	if (ND == 1) {
+		t[0] = (int)tile;
+		return;
+	}
+	const long r = tile / tg.nt[0];
+	const int tx = (int)(tile - r * tg.nt[0]);
+	t[0] = (r & 1) ? tg.nt[0] - 1 - tx : tx;
+	if (ND == 2) {
+		t[1] = (int)r;
+		return;
+	}
+	t[2] = (int)(r / tg.nt[1]);
+	const int ty = (int)(r - (long)t[2] * tg.nt[1]);
+	t[1] = (t[2] & 1) ? tg.nt[1] - 1 - ty : ty;
+}
+// key of clamped cell coordinates c (each in [0, cmax])
+template <int ND>
+__device__ __forceinline__ int tile_key_of(const TileGeo &tg, const int *c) {
+	int t[3] = {0, 0, 0}, in[3] = {0, 0, 0};
+#pragma unroll
+	for (int d = 0; d < ND; d++) {
+		t[d] = c[d] / tg.tw;
+		in[d] = c[d] - t[d] * tg.tw;
+	}
+	const long tile = tile_serp<ND>(tg, t);
+	if (ND > 1 && (tile & 1)) in[ND - 1] = tg.tw - 1 - in[ND - 1];
 	int cell = 0, cs = 1;
 #pragma unroll
 	for (int d = 0; d < ND; d++) {
-		int c = (int)p[d];
-		c = c < 0 ? 0 : (c > tg.cmax[d] ? tg.cmax[d] : c);
-		tile += (long)(c / tg.tw) * tg.ts[d];
-		cell += (c % tg.tw) * cs;
+		cell += in[d] * cs;
 		cs *= tg.tw;
 	}
 	return (int)(tile * cs + cell);
+}
+// cell coordinates of a key (inverse of tile_key_of)
+template <int ND>
+__device__ __forceinline__ void tile_key_cell(const TileGeo &tg, long key, int *c) {
+	int cpt = 1;
+#pragma unroll
+	for (int d = 0; d < ND; d++) cpt *= tg.tw;
+	const long tile = key / cpt;
+	int in = (int)(key - tile * cpt);
+	int t[3];
+	tile_unserp<ND>(tg, tile, t);
+	c[1] = c[2] = 0;
+#pragma unroll
+	for (int d = 0; d < ND; d++) {
+		int q = in % tg.tw;
+		in /= tg.tw;
+		if (ND > 1 && d == ND - 1 && (tile & 1)) q = tg.tw - 1 - q;
+		c[d] = t[d] * tg.tw + q;
+	}
+}
+template <int ND>
+__device__ __forceinline__ int tile_key(const TileGeo &tg, const double *p) {
+	int c[3] = {0, 0, 0};
+#pragma unroll
+	for (int d = 0; d < ND; d++) {
+		const int x = (int)p[d];
+		c[d] = x < 0 ? 0 : (x > tg.cmax[d] ? tg.cmax[d] : x);
+	}
+	return tile_key_of<ND>(tg, c);
 }
 
 // wave-aggregated atomicAdd of 1 per active lane on ctr[key]; returns the
@@ -1100,18 +1165,20 @@ __global__ __launch_bounds__(kThreads) void k_deposit_cells(const double *__rest
 	for (int d = 0; d < ND; d++) cpt *= tg.tw;
 	const long k0 = (long)blockIdx.x * kThreads;
 	const long k1 = min(k0 + kThreads, nKeys) - 1;
-	// node box of the block's tiles plus a one-cell margin
-	long t0 = k0 / cpt, t1 = k1 / cpt;
-	int tlo[3], thi[3];
-	bool boxOk = true;
+	// node box of the block's tiles plus a one-cell margin (the tiles of a
+	// key range are a path of neighbouring tiles, tile_serp)
+	const long t0 = k0 / cpt, t1 = k1 / cpt;
+	int tlo[3] = {INT32_MAX, INT32_MAX, INT32_MAX}, thi[3] = {INT32_MIN, INT32_MIN, INT32_MIN};
+	for (long t = t0; t <= t1; t++) {
+		int tc[3];
+		tile_unserp<ND>(tg, t, tc);
 #pragma unroll
-	for (int d = ND - 1; d >= 0; d--) {
-		tlo[d] = (int)(t0 / tg.ts[d]);
-		thi[d] = (int)(t1 / tg.ts[d]);
-		t0 -= (long)tlo[d] * tg.ts[d];
-		t1 -= (long)thi[d] * tg.ts[d];
-		if (d > 0 && tlo[d] != thi[d]) boxOk = false;
+		for (int d = 0; d < ND; d++) {
+			tlo[d] = min(tlo[d], tc[d]);
+			thi[d] = max(thi[d], tc[d]);
+		}
 	}
+	const bool boxOk = t1 - t0 < 16;
 	int blo[3] = {0, 0, 0}, bn[3] = {1, 1, 1}, st[3] = {0, 0, 0};
 	int vol = 1;
 #pragma unroll
@@ -1150,20 +1217,8 @@ __global__ __launch_bounds__(kThreads) void k_deposit_cells(const double *__rest
 	const long key = k0 + threadIdx.x;
 	if (key < nKeys) {
 		// this thread's cell
-		long tile = key / cpt;
-		int cin = (int)(key - tile * cpt);
 		int cell[3] = {0, 0, 0};
-#pragma unroll
-		for (int d = ND - 1; d >= 0; d--) {
-			int tc = (int)(tile / tg.ts[d]);
-			tile -= (long)tc * tg.ts[d];
-			cell[d] = tc * tg.tw;
-		}
-#pragma unroll
-		for (int d = 0; d < ND; d++) {
-			cell[d] += cin % tg.tw;
-			cin /= tg.tw;
-		}
+		tile_key_cell<ND>(tg, key, cell);
 		long a = key > 0 ? (long)offs[key - 1] : 0, b = min((long)offs[key], nCell);
 		double sum[NC];
 #pragma unroll
@@ -1531,17 +1586,10 @@ __device__ __forceinline__ int lds_agg_add(int *ctr, int idx, bool active) {
 // sort key of integer cell coordinates (tile_key's order)
 template <int ND>
 __device__ __forceinline__ int tile_key_cells(const TileGeo &tg, const int *cin) {
-	long tile = 0;
-	int cell = 0, cs = 1;
+	int c[3] = {0, 0, 0};
 #pragma unroll
-	for (int d = 0; d < ND; d++) {
-		int c = cin[d];
-		c = c < 0 ? 0 : (c > tg.cmax[d] ? tg.cmax[d] : c);
-		tile += (long)(c / tg.tw) * tg.ts[d];
-		cell += (c % tg.tw) * cs;
-		cs *= tg.tw;
-	}
-	return (int)(tile * cs + cell);
+	for (int d = 0; d < ND; d++) c[d] = cin[d] < 0 ? 0 : (cin[d] > tg.cmax[d] ? tg.cmax[d] : cin[d]);
+	return tile_key_of<ND>(tg, c);
 }
 
 // Bricks (TileGeo::bs) of a cell box: brick coordinates = clamped cell >> bs.
@@ -2723,7 +2771,6 @@ static TileGeo make_tile_geo(pinc_geom_t g, int tileWidth, long *nKeys) {
 		int T = d < g.nd ? (d == g.nd - 1 ? g.nloc : g.T[d]) : 1;
 		tg.cmax[d] = T + 1;
 		tg.nt[d] = d < g.nd ? (T + 1) / tileWidth + 1 : 1;
-		tg.ts[d] = nt;
 		tg.bs[d] = brick && d < g.nd - 1 ? lw : 0;
 		nt *= tg.nt[d];
 		if (d < g.nd) cpt *= tileWidth;
