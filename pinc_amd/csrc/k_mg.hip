@@ -28,6 +28,32 @@ constexpr int kMaxBlocks = 2048;
 
 inline long ceil_div(long a, long b) { return (a + b - 1) / b; }
 
+// Grid-stride walk of the point stencils (residual, norm, restriction,
+// prolongation).  PINC_MG_XCD: the 8 XCDs (block b on XCD b % 8) take
+// contiguous eighths of [0, n) and each XCD's blocks sweep theirs in order,
+// so the rows and planes a point's stencil reads around it are read by the
+// same XCD close in time (one L2), instead of by the XCDs of the blocks of
+// the neighbouring rows.  Placement only: the same points, the same
+// arithmetic.  Otherwise the plain grid stride.
+#ifndef PINC_MG_XCD_WALK
+#define PINC_MG_XCD_WALK 1
+#endif
+struct Walk {
+	long g0, g1, step;
+};
+__device__ __forceinline__ Walk point_walk(long n) {
+	const long nt = blockDim.x;
+#if PINC_MG_XCD_WALK
+	if ((gridDim.x & 7u) == 0) {
+		const unsigned x = blockIdx.x & 7u, j = blockIdx.x >> 3, perXcd = gridDim.x >> 3;
+		const long span = ((n + 8 * nt - 1) / (8 * nt)) * nt;  // an eighth, whole blocks
+		const long b0 = (long)x * span;
+		return {b0 + (long)j * nt + threadIdx.x, min(n, b0 + span), (long)perXcd * nt};
+	}
+#endif
+	return {(long)blockIdx.x * nt + threadIdx.x, n, (long)gridDim.x * nt};
+}
+
 struct Lv {
 	int T[3];
 	long s[3];
@@ -137,7 +163,8 @@ __global__ void k_residual(double *__restrict__ res, const double *__restrict__ 
                            const double *__restrict__ rho, pinc_lvl_t Lp) {
 	Lv L = make_lv(Lp);
 	long n = (long)L.T[0] * L.T[1] * L.T[2];
-	for (long g = (long)blockIdx.x * blockDim.x + threadIdx.x; g < n; g += (long)gridDim.x * blockDim.x) {
+	const Walk w = point_walk(n);
+	for (long g = w.g0; g < w.g1; g += w.step) {
 		int c[3];
 		{  // 32-bit index arithmetic (levels hold < 2^31 points, checked on the host)
 			const unsigned u = (unsigned)g, t0 = (unsigned)L.T[0], t1 = (unsigned)L.T[1];
@@ -159,7 +186,8 @@ __global__ __launch_bounds__(kThreads) void k_residual_sumsq(const double *__res
 	Lv L = make_lv(Lp);
 	long n = (long)L.T[0] * L.T[1] * L.T[2];
 	double acc = 0.;
-	for (long g = (long)blockIdx.x * blockDim.x + threadIdx.x; g < n; g += (long)gridDim.x * blockDim.x) {
+	const Walk w = point_walk(n);
+	for (long g = w.g0; g < w.g1; g += w.step) {
 		int c[3];
 		{  // 32-bit index arithmetic (levels hold < 2^31 points, checked on the host)
 			const unsigned u = (unsigned)g, t0 = (unsigned)L.T[0], t1 = (unsigned)L.T[1];
@@ -182,7 +210,8 @@ __global__ void k_restrict(const double *__restrict__ fine, double *__restrict__
 	for (int d = 0; d < ND; d++) Lfp.T[d] = 2 * Lc.T[d];
 	Lv F = make_lv(Lfp);
 	long n = (long)C.T[0] * C.T[1] * C.T[2];
-	for (long gc = (long)blockIdx.x * blockDim.x + threadIdx.x; gc < n; gc += (long)gridDim.x * blockDim.x) {
+	const Walk w = point_walk(n);
+	for (long gc = w.g0; gc < w.g1; gc += w.step) {
 		int cc[3], cf[3] = {0, 0, 0};
 		{  // 32-bit index arithmetic (levels hold < 2^31 points, checked on the host)
 			const unsigned u = (unsigned)gc, t0 = (unsigned)C.T[0], t1 = (unsigned)C.T[1];
@@ -240,7 +269,8 @@ __global__ void k_prolong_add(double *__restrict__ phiF, const double *__restric
 	Lv C = make_lv(Lcp);
 	Lv F = make_lv(Lf);
 	long n = (long)F.T[0] * F.T[1] * F.T[2];
-	for (long g = (long)blockIdx.x * blockDim.x + threadIdx.x; g < n; g += (long)gridDim.x * blockDim.x) {
+	const Walk w = point_walk(n);
+	for (long g = w.g0; g < w.g1; g += w.step) {
 		int cf[3];
 		{  // 32-bit index arithmetic (levels hold < 2^31 points, checked on the host)
 			const unsigned u = (unsigned)g, t0 = (unsigned)F.T[0], t1 = (unsigned)F.T[1];
