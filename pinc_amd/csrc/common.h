@@ -26,6 +26,32 @@ __device__ __forceinline__ int wrap(int i, int T) {
 	return (i < 0) ? i + T : ((i >= T) ? i - T : i);
 }
 
+// Grid-stride walk of the point stencils (residual, norm, restriction,
+// prolongation, E = -grad phi).  PINC_MG_XCD: the 8 XCDs (block b on XCD b % 8) take
+// contiguous eighths of [0, n) and each XCD's blocks sweep theirs in order,
+// so the rows and planes a point's stencil reads around it are read by the
+// same XCD close in time (one L2), instead of by the XCDs of the blocks of
+// the neighbouring rows.  Placement only: the same points, the same
+// arithmetic.  Otherwise the plain grid stride.
+#ifndef PINC_MG_XCD_WALK
+#define PINC_MG_XCD_WALK 1
+#endif
+struct Walk {
+	long g0, g1, step;
+};
+__device__ __forceinline__ Walk point_walk(long n) {
+	const long nt = blockDim.x;
+#if PINC_MG_XCD_WALK
+	if ((gridDim.x & 7u) == 0) {
+		const unsigned x = blockIdx.x & 7u, j = blockIdx.x >> 3, perXcd = gridDim.x >> 3;
+		const long span = ((n + 8 * nt - 1) / (8 * nt)) * nt;  // an eighth, whole blocks
+		const long b0 = (long)x * span;
+		return {b0 + (long)j * nt + threadIdx.x, min(n, b0 + span), (long)perXcd * nt};
+	}
+#endif
+	return {(long)blockIdx.x * nt + threadIdx.x, n, (long)gridDim.x * nt};
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll

@@ -28,31 +28,6 @@ constexpr int kMaxBlocks = 2048;
 
 inline long ceil_div(long a, long b) { return (a + b - 1) / b; }
 
-// Grid-stride walk of the point stencils (residual, norm, restriction,
-// prolongation).  PINC_MG_XCD: the 8 XCDs (block b on XCD b % 8) take
-// contiguous eighths of [0, n) and each XCD's blocks sweep theirs in order,
-// so the rows and planes a point's stencil reads around it are read by the
-// same XCD close in time (one L2), instead of by the XCDs of the blocks of
-// the neighbouring rows.  Placement only: the same points, the same
-// arithmetic.  Otherwise the plain grid stride.
-#ifndef PINC_MG_XCD_WALK
-#define PINC_MG_XCD_WALK 1
-#endif
-struct Walk {
-	long g0, g1, step;
-};
-__device__ __forceinline__ Walk point_walk(long n) {
-	const long nt = blockDim.x;
-#if PINC_MG_XCD_WALK
-	if ((gridDim.x & 7u) == 0) {
-		const unsigned x = blockIdx.x & 7u, j = blockIdx.x >> 3, perXcd = gridDim.x >> 3;
-		const long span = ((n + 8 * nt - 1) / (8 * nt)) * nt;  // an eighth, whole blocks
-		const long b0 = (long)x * span;
-		return {b0 + (long)j * nt + threadIdx.x, min(n, b0 + span), (long)perXcd * nt};
-	}
-#endif
-	return {(long)blockIdx.x * nt + threadIdx.x, n, (long)gridDim.x * nt};
-}
 
 struct Lv {
 	int T[3];
@@ -1163,7 +1138,8 @@ __global__ __launch_bounds__(kThreads) void k_residual_slab(double *__restrict__
 	const long ps = L.s[2];
 	const long n = ps * (zhi - zlo);
 	double acc = 0.;
-	for (long q = (long)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (long)gridDim.x * blockDim.x) {
+	const Walk w = point_walk(n);
+	for (long q = w.g0; q < w.g1; q += w.step) {
 		const long g = (long)zlo * ps + q;
 		int c[3];
 		{  // 32-bit index arithmetic (levels hold < 2^31 points, checked on the host)
@@ -1194,7 +1170,8 @@ __global__ void k_restrict_slab(const double *__restrict__ fine, pinc_lvl_t Lfp,
 	Lv F = make_lv(Lfp), C = make_lv(Lcp);
 	const long ps = F.s[2];
 	const long n = (long)C.T[0] * C.T[1] * C.T[2];
-	for (long gc = (long)blockIdx.x * blockDim.x + threadIdx.x; gc < n; gc += (long)gridDim.x * blockDim.x) {
+	const Walk w = point_walk(n);
+	for (long gc = w.g0; gc < w.g1; gc += w.step) {
 		int cc[3];
 		{  // 32-bit index arithmetic (levels hold < 2^31 points, checked on the host)
 			const unsigned u = (unsigned)gc, t0 = (unsigned)C.T[0], t1 = (unsigned)C.T[1];
@@ -1226,7 +1203,8 @@ __global__ void k_prolong_add_slab(double *__restrict__ phiX, pinc_lvl_t Lxp, in
                                    const double *__restrict__ phiC, pinc_lvl_t Lcp) {
 	Lv X = make_lv(Lxp), C = make_lv(Lcp);
 	const long n = (long)X.T[0] * X.T[1] * X.T[2];
-	for (long g = (long)blockIdx.x * blockDim.x + threadIdx.x; g < n; g += (long)gridDim.x * blockDim.x) {
+	const Walk w = point_walk(n);
+	for (long g = w.g0; g < w.g1; g += w.step) {
 		int cf[3];
 		cf[0] = (int)(g % X.T[0]);
 		long r = g / X.T[0];

@@ -141,8 +141,16 @@ def test_cell_sort(hip, n, T, start):
     V0 = np.stack([v.cpu().numpy()[start:start + n] for v in vel], 1)
     c = P.astype(int)
     nt = [(t + 1) // 4 + 1 for t in T]
-    tile = (c[:, 0] // 4) + nt[0] * ((c[:, 1] // 4) + nt[1] * (c[:, 2] // 4))
-    key = tile * 64 + (c[:, 0] % 4) + 4 * ((c[:, 1] % 4) + 4 * (c[:, 2] % 4))
+    # tile_key_of (k_particles.hip): tiles along a serpentine (x rows
+    # alternate direction, y columns alternate per z plane), the z layers of
+    # odd tiles reversed, cells x fastest inside a layer
+    t = c // 4
+    ty = np.where(t[:, 2] % 2 == 1, nt[1] - 1 - t[:, 1], t[:, 1])
+    r = t[:, 2] * nt[1] + ty
+    tx = np.where(r % 2 == 1, nt[0] - 1 - t[:, 0], t[:, 0])
+    tile = r * nt[0] + tx
+    inz = np.where(tile % 2 == 1, 3 - c[:, 2] % 4, c[:, 2] % 4)
+    key = tile * 64 + (c[:, 0] % 4) + 4 * ((c[:, 1] % 4) + 4 * inz)
     assert np.all(np.diff(key) >= 0)
     a = np.concatenate([P, V], 1)
     b = np.concatenate([P0, V0], 1)
