@@ -1472,6 +1472,38 @@ __device__ __forceinline__ void node_pair(const Geo32 &G, int d, int j, int &o0,
 		o1 = d ? mul24(s1, G.stride[d]) : s1;
 	}
 }
+// periodic images of the cells nearest to the block's reference cell r (the
+// cell of its first item).  The half cells 0 and T (thresholds at 0.5 and
+// T + 0.5) are one cell of the torus: a particle that crosses T + 0.5 lands
+// in cell 0 while its neighbours stay in cell T, and the block's boxes,
+// centred on the mean cell, would sit between the two.  E at image nodes is
+// the same data (wrapped storage; the slab's ghost planes when the slab
+// dimension wraps, whose images stay within cells 0..T).  Block-uniform
+// bounds: cells <= lo move up by T, cells >= hi down by T.
+struct Images {
+	int lo[3], hi[3], T[3];
+	__device__ __forceinline__ int operator()(int d, int c) const {
+		return c + (c <= lo[d] ? T[d] : 0) - (c >= hi[d] ? T[d] : 0);
+	}
+};
+__device__ __forceinline__ Images make_images(const Geo32 &G, int wrapMask, const int *r, int nd) {
+	Images m;
+	for (int d = 0; d < 3; d++) {
+		const int T = G.T[d], h = T / 2;
+		m.T[d] = T;
+		m.lo[d] = INT32_MIN;
+		m.hi[d] = INT32_MAX;
+		if (d >= nd) continue;
+		if (d != G.slab) {
+			m.lo[d] = r[d] - h - 1;
+			m.hi[d] = r[d] + h + 1;
+		} else if ((wrapMask >> d) & 1) {
+			m.lo[d] = min(r[d] - h - 1, 0);
+			m.hi[d] = max(r[d] + h + 1, T);
+		}
+	}
+	return m;
+}
 
 // LDS capacities of the push: E nodes (pre-move cells + 1), charge nodes
 // (post-move cells + 1), input cells and output cells of the sort counters
@@ -1764,7 +1796,15 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 		              reinterpret_cast<unsigned long>(a.xo[d]) | reinterpret_cast<unsigned long>(a.vo[d])) & 15);
 
 	PUSH_TS(0);
-	// ---- phase A: load every item, cell box of the input positions
+	// ---- phase A: load every item, cell box of the input positions (periodic
+	// images nearest to the cell of the block's first item)
+	// (loaded first, converted after the item loads are issued: the oldest
+	// load in flight, so its wait does not hold back the items')
+	double xref[3] = {1.0, 1.0, 1.0};
+	if (base < a.n) {
+#pragma unroll
+		for (int d = 0; d < ND; d++) xref[d] = a.xi[d][base];
+	}
 	double p[kPushItems][ND], vv[kPushItems][ND];
 	unsigned valid = 0;
 	int lo[3] = {INT32_MAX, INT32_MAX, INT32_MAX}, hi[3] = {INT32_MIN, INT32_MIN, INT32_MIN}, sm[3] = {0, 0, 0};
@@ -1797,6 +1837,10 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 			}
 		}
 	}
+	int cref[3] = {0, 0, 0};
+#pragma unroll
+	for (int d = 0; d < ND; d++) cref[d] = __builtin_amdgcn_readfirstlane((int)xref[d]);
+	const Images img = make_images(G, a.wrapMask, cref, ND);
 #pragma unroll
 	for (int k = 0; k < kPushItems; k += 2) {
 #pragma unroll
@@ -1804,7 +1848,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 #pragma unroll
 			for (int h = 0; h < 2; h++) {
 				if ((valid >> (k + h)) & 1u) {
-					int c = (int)p[k + h][d];
+					const int c = img(d, (int)p[k + h][d]);
 					lo[d] = min(lo[d], c);
 					hi[d] = max(hi[d], c);
 					sm[d] += c;
@@ -2002,10 +2046,11 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 		const long i = item(k);
 		if (KICK) {
 			double dec[3], comp[3];
-			int j[3] = {0, 0, 0};
+			int j[3] = {0, 0, 0}, jc[3] = {0, 0, 0};
 #pragma unroll
 			for (int d = 0; d < ND; d++) {
 				j[d] = (int)p[k][d];
+				jc[d] = img(d, j[d]);
 				dec[d] = p[k][d] - j[d];
 				comp[d] = 1 - dec[d];
 			}
@@ -2013,10 +2058,16 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 			// dimension, evaluated without short-circuit branches
 			bool inE = eB.vol > 0;
 #pragma unroll
-			for (int d = 0; d < ND; d++) inE &= (unsigned)(j[d] - eB.lo[d]) < (unsigned)(eB.n[d] - 1);
-			if (a.diag) {  // (trace: [1] += particles that gather E from memory)
+			for (int d = 0; d < ND; d++) inE &= (unsigned)(jc[d] - eB.lo[d]) < (unsigned)(eB.n[d] - 1);
+			if (a.diag) {  // (trace: [1] += particles that gather E from memory, [3] += those of them
+				           // more than a quarter of the grid from the box: periodic wraps)
 				const int ng = __popcll(__ballot(!inE));
+				bool far = false;
+#pragma unroll
+				for (int d = 0; d < ND; d++) far |= abs(jc[d] - (eB.lo[d] + eB.n[d] / 2)) > G.T[d] / 4;
+				const int nf = __popcll(__ballot(!inE && far));
 				if (lane == 0 && ng) atomicAdd(&a.diag[1], (unsigned long long)ng);
+				if (lane == 0 && nf) atomicAdd(&a.diag[3], (unsigned long long)nf);
 			}
 			double dv[ND];
 			if constexpr (V3D) {
@@ -2032,7 +2083,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 				if (PINC_PUSH_SKIP & 2) {
 					dv[0] = dv[1] = dv[2] = 0.0;
 				} else if (inE) {
-					const int ei = eB.index(j, ND);
+					const int ei = eB.index(jc, ND);
 					double fx[NC], fy[NC];
 #pragma unroll
 					for (int c = 0; c < NC; c++) {
@@ -2075,7 +2126,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 #pragma unroll
 						for (int q = 0; q < ND; q++) e[c][q] = 0.0;
 				} else if (inE) {
-					const double *eb = eL + mul24(eB.index(j, ND), ND);
+					const double *eb = eL + mul24(eB.index(jc, ND), ND);
 #pragma unroll
 					for (int c = 0; c < NC; c++)
 #pragma unroll

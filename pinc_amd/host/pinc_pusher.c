@@ -237,7 +237,7 @@ static int cmp_double(const void *x, const void *y) {
 static void push_phase_report(const unsigned long long *dts, const unsigned long long *ddiag, int nb, int s, int sort,
                               int count) {
 	unsigned long long *t = malloc((size_t)nb * 8 * sizeof(*t));
-	unsigned long long dg[3];
+	unsigned long long dg[4];
 	pinc_check(pinc_hip_d2h(t, dts, (size_t)nb * 8 * sizeof(*t), g_pinc.stream), "push timestamps");
 	pinc_check(pinc_hip_d2h(dg, ddiag, sizeof(dg), g_pinc.stream), "push diagnostics");
 	double ph[7] = {0};
@@ -248,12 +248,12 @@ static void push_phase_report(const unsigned long long *dts, const unsigned long
 		if (t[b * 8 + 7] > t1) t1 = t[b * 8 + 7];
 	}
 	fprintf(stderr, "[pinc] push species %d%s%s: span %.2f ms, per block us: load+box %.2f, lds %.2f, rank %.2f, "
-	        "kick/drift %.2f, sorted stores %.2f, count %.2f, deposit %.2f; global slots %.3g, E gathers %.3g, "
-	        "charge runs %.3g per block\n", s,
+	        "kick/drift %.2f, sorted stores %.2f, count %.2f, deposit %.2f; global slots %.3g, E gathers %.3g "
+	        "(wrapped %.3g), charge runs %.3g per block\n", s,
 	        sort ? " sort" : "",
 	        count ? " count" : "", (t1 - t0) * 1e-5, ph[0] / nb * 1e-2, ph[1] / nb * 1e-2, ph[2] / nb * 1e-2,
 	        ph[3] / nb * 1e-2, ph[4] / nb * 1e-2, ph[5] / nb * 1e-2, ph[6] / nb * 1e-2, (double)dg[0] / nb,
-	        (double)dg[1] / nb, (double)dg[2] / nb);
+	        (double)dg[1] / nb, (double)dg[3] / nb, (double)dg[2] / nb);
 	/* per XCD (the push deals chunks [x q + min(x, r), ...) to XCD x): span
 	 * from its first block's start to its last block's end, and the mean
 	 * number of its blocks between their first and last timestamp */
@@ -415,7 +415,7 @@ static int push_all(Population *pop, Grid *E, double *const *xout) {
 		unsigned long long *ts = NULL;
 		if (g_pinc.traceSort > 1) {
 			pinc_check(pinc_hip_malloc((void **)&ts, ((np / 1024 + 1) * 8 + 4) * sizeof(*ts)), "push timestamps");
-			pinc_check(pinc_hip_memset(ts + (np / 1024 + 1) * 8, 0, 3 * sizeof(*ts), g_pinc.stream), "push diagnostics");
+			pinc_check(pinc_hip_memset(ts + (np / 1024 + 1) * 8, 0, 4 * sizeof(*ts), g_pinc.stream), "push diagnostics");
 			a.tstamp = ts;
 			a.diag = ts + (np / 1024 + 1) * 8;
 		}
