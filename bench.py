@@ -25,6 +25,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import re
 import sys
 import time
 from pathlib import Path
@@ -54,7 +55,11 @@ def _pmc_traffic(prefix: str, key: dict):
     run's configuration `key` (workload, grid, ppc, GPU count, layout),
     launch-weighted over the kernel's variants; None if no profile of this
     configuration covers it."""
-    files = sorted((ROOT / "profiles").glob("*_hbm_traffic.json"))
+    def order(f):  # round, then tag: r03w < r03ao < r04a (tags grow a letter once z is used)
+        m = re.match(r"r(\d+)([a-z]*)_", f.name)
+        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, f.name)
+
+    files = sorted((ROOT / "profiles").glob("*_hbm_traffic.json"), key=order)
     for f in reversed(files):
         try:
             d = json.loads(f.read_text())
