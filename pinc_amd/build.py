@@ -27,8 +27,14 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("PINC_ARCH", "gfx950")
 # -ffp-contract=off: the kernels reproduce the reference's fp64 association
 # order; a fused multiply-add would change the rounding.
+# (a variant library records its defines in build_flags.txt, so that a
+# rebuild without PINC_HIP_DEFINES in the environment keeps them)
+STAMP = LIB / "build_flags.txt"
+DEFINES = os.environ.get("PINC_HIP_DEFINES")
+if DEFINES is None:
+    DEFINES = STAMP.read_text().strip() if STAMP.exists() else ""
 HIP_FLAGS = ["-std=c++17", "-O3", f"--offload-arch={ARCH}", "-ffp-contract=off", "-fPIC",
-             "-munsafe-fp-atomics", f"-I{INC}", f"-I{CSRC}", *os.environ.get("PINC_HIP_DEFINES", "").split()]
+             "-munsafe-fp-atomics", f"-I{INC}", f"-I{CSRC}", *DEFINES.split()]
 C_FLAGS = ["-std=c11", "-O2", "-fPIC", "-Wall", "-ffp-contract=off", f"-I{INC}", f"-I{HOST}"]
 
 HIP_SRC = ["runtime.hip", "k_particles.hip", "k_grid.hip", "k_mg.hip", "k_spectral.hip", "k_objects.hip"]
@@ -48,15 +54,37 @@ def _newer(src: Path, dst: Path, deps: list[Path]) -> bool:
     return src.stat().st_mtime > t or any(d.stat().st_mtime > t for d in deps)
 
 
+def _up_to_date(libs: list[Path], inputs: list[Path]) -> bool:
+    """The libraries exist, are newer than every source and header, and were
+    built with these defines.  (The object directory is not consulted: it
+    does not travel to the GPU box, where the libraries are used as built.)"""
+    if not all(p.exists() for p in libs):
+        return False
+    stamp = STAMP.read_text().strip() if STAMP.exists() else ""
+    if stamp != DEFINES.strip():
+        return False
+    t = min(p.stat().st_mtime for p in libs)
+    return all(p.stat().st_mtime <= t for p in inputs)
+
+
 def build(verbose: bool = False, jobs: int = 8) -> dict:
-    LIB.mkdir(parents=True, exist_ok=True)
-    OBJ.mkdir(parents=True, exist_ok=True)
     hip_deps = [INC / "pinc_hip.h", CSRC / "common.h"]
     c_deps = [INC / "pinc.h", INC / "pinc_hip.h", HOST / "pinc_internal.h"]
+    libhip = LIB / "libpinc_hip.so"
+    libhost = LIB / "libpinc.so"
+    out = {"libpinc_hip": str(libhip), "libpinc": str(libhost)}
+    inputs = [CSRC / f for f in HIP_SRC] + [HOST / f for f in C_SRC] + hip_deps + c_deps
+    if _up_to_date([libhip, libhost], inputs):
+        if verbose:
+            print(out)
+        return out
+    LIB.mkdir(parents=True, exist_ok=True)
+    OBJ.mkdir(parents=True, exist_ok=True)
+    flags_changed = (STAMP.read_text().strip() if STAMP.exists() else "") != DEFINES.strip()
     jobs_list = []
     for f in HIP_SRC:
         src, obj = CSRC / f, OBJ / (f + ".o")
-        if _newer(src, obj, hip_deps):
+        if flags_changed or _newer(src, obj, hip_deps):
             jobs_list.append([HIPCC, *HIP_FLAGS, "-c", str(src), "-o", str(obj)])
     for f in C_SRC:
         src, obj = HOST / f, OBJ / (f + ".o")
@@ -66,14 +94,11 @@ def build(verbose: bool = False, jobs: int = 8) -> dict:
         list(ex.map(_run, jobs_list))
     hip_objs = [str(OBJ / (f + ".o")) for f in HIP_SRC]
     c_objs = [str(OBJ / (f + ".o")) for f in C_SRC]
-    libhip = LIB / "libpinc_hip.so"
-    libhost = LIB / "libpinc.so"
-    if jobs_list or not libhip.exists() or not libhost.exists():
-        _run([HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", str(libhip), *hip_objs,
-              "-L/opt/rocm/lib", "-lrccl", "-lrocfft", "-Wl,-rpath,/opt/rocm/lib"])
-        _run(["gcc", "-shared", "-o", str(libhost), *c_objs, f"-L{LIB}", "-lpinc_hip", "-lm", "-ldl",
-              "-Wl,-rpath,$ORIGIN"])
-    out = {"libpinc_hip": str(libhip), "libpinc": str(libhost)}
+    _run([HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", str(libhip), *hip_objs,
+          "-L/opt/rocm/lib", "-lrccl", "-lrocfft", "-Wl,-rpath,/opt/rocm/lib"])
+    _run(["gcc", "-shared", "-o", str(libhost), *c_objs, f"-L{LIB}", "-lpinc_hip", "-lm", "-ldl",
+          "-Wl,-rpath,$ORIGIN"])
+    STAMP.write_text(DEFINES.strip() + "\n")
     if verbose:
         print(out)
     return out
