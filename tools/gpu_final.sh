@@ -14,7 +14,7 @@ bash tools/profile_bench.sh --steps 10 --warmup 3 > $O/profile.log 2>&1 || { tai
 python3 tools/pmc_summary.py $T gpurun_out/prof gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/prof_bench.json > $O/pmc_summary.txt || exit 1
 cp profiles/${T}_* $O/ && cp gpurun_out/prof_bench.json $O/prof_bench_c4.json
 rm -rf gpurun_out/prof gpurun_out/pmc_fetch gpurun_out/pmc_write
-for w in c3 c2 c5; do
+for w in c3 c2 c5 c4ts; do
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof_$w -o run -- python3 bench.py --workload $w --steps 10 --warmup 3 --no-cpu-baseline > $O/bench_$w.json 2> $O/bench_$w.err || { tail -20 $O/bench_$w.err; exit 1; }
   python3 tools/db_stats.py $O/prof_$w $O/${T}_${w}_kernel_stats.csv && rm -rf $O/prof_$w
   python3 -c "
