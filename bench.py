@@ -140,6 +140,8 @@ def _cpu_baseline(size: int, ppc: int, steps: int, native: bool, workload: str =
         cfg["multigrid"]["extrapolate"] = str(extrapolate)
         cfg["multigrid"]["spectralCoarse"] = str(spectral_coarse)
     ini = configs.write_ini(cfg)
+    spread_note = (f" and the blocks' mean cell box grew {args.sort_spread:g}x since the last sort"
+                   if args.sort_spread > 0 else "")
     t_init = time.perf_counter()
     w = orc.World(ini)
     w.init(perturb=workload == "c2", maxwell=workload != "c2", seed=20260101)
@@ -230,6 +232,9 @@ def main() -> int:
                          "last sort (adaptive, per species; --sort-max pushes apart at most) instead of every "
                          "--sort-interval pushes")
     ap.add_argument("--sort-max", type=int, default=32)
+    ap.add_argument("--sort-spread", type=float, default=0.0,
+                    help="with --sort-fraction: a sort also waits until the blocks' mean input cell box has grown "
+                         "to this multiple of its size right after the last sort (0: off)")
     ap.add_argument("--sort-in-push", type=int, default=1,
                     help="1: the tile sort rides in every sort-interval-th push (default); 0: separate sort pass")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -303,7 +308,8 @@ def main() -> int:
                                mg_graph=args.mg_graph, obj_capacitance=args.obj_capacitance,
                                obj_second_guess=args.obj_second_guess, c5_fused=args.c5_fused, layout=args.layout,
                                sort_interval=args.sort_interval, sort_in_push=args.sort_in_push,
-                               sort_fraction=args.sort_fraction, sort_max=args.sort_max)
+                               sort_fraction=args.sort_fraction, sort_max=args.sort_max,
+                               sort_spread=args.sort_spread)
     nspecies = int(cfg["population"]["nSpecies"])
     ini = configs.write_ini(cfg)
 
@@ -436,7 +442,8 @@ def main() -> int:
             "particles": n_total,
             "decomposition": f"1,{world}" if c2 else f"1,1,{world}",
             "layout": args.layout + ((f" (per-species tile sort once {args.sort_fraction:g} of the particles left "
-                                      f"their cell, at most {args.sort_max} steps apart)" if args.sort_fraction > 0 else
+                                      f"their cell{spread_note}, at most {args.sort_max} steps apart)"
+                                      if args.sort_fraction > 0 else
                                       f" (tile sort every {args.sort_interval} steps)") if args.layout == "tiled" else ""),
             "poisson": ("spectral (sSolver, rocFFT r2c/c2r, global grid)" if c3 else
                         (f"multigrid mgVRecursive, 2 levels used ({S}^{nd}, {S // 2}^{nd} solved exactly), "

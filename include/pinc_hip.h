@@ -130,6 +130,8 @@ typedef struct {
 	int *cntNext;
 	int *perm;
 	unsigned long long *moved; /* if set: += particles that stay and changed cell */
+	unsigned long long *spread; /* if set: += each block's input cell-box volume (cells spanned by its
+	                             * items, periodic images nearest its first item) */
 	unsigned long long *tstamp; /* if set: 8 phase timestamps per block (diagnostics) */
 	unsigned long long *diag;   /* if set: [0] += items of a sorting push given a global slot one by
 	                             * one (outside its LDS boxes; diagnostics) */

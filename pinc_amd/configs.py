@@ -158,7 +158,7 @@ def bench_config(workload: str = "c4", size: int | None = None, ppc: int | None 
                  mg: str = "native", mg_shard: str = "auto", mg_extrapolate: int = 1, mg_spectral_coarse: int = 1,
                  mg_graph: int | None = None, obj_capacitance: str = "solve", obj_second_guess: str = "spectral",
                  c5_fused: int = 1, layout: str = "tiled", sort_interval: int = 8, sort_in_push: int = 1,
-                 sort_fraction: float = 0.8, sort_max: int = 32) -> dict:
+                 sort_fraction: float = 0.8, sort_max: int = 32, sort_spread: float = 0.0) -> dict:
     """bench.py's configuration of one rank's ini (its defaults are the
     bench's): workload c4 / c4ts / c5 / c3 / c2 at size^nd cells split into
     `world` slabs along the last dimension, ppc particles per cell per
@@ -198,6 +198,8 @@ def bench_config(workload: str = "c4", size: int | None = None, ppc: int | None 
         cfg["population"]["sortInPush"] = str(sort_in_push)
         cfg["population"]["sortFraction"] = str(sort_fraction)
         cfg["population"]["sortMax"] = str(sort_max)
+        if sort_spread > 0:
+            cfg["population"]["sortSpread"] = str(sort_spread)
     return cfg
 
 

@@ -1305,6 +1305,7 @@ struct PushArgs {
 	int *cntNext;
 	int *perm;           // perm[i] = destination of particle i
 	unsigned long long *moved;  // += particles that stay but changed cell (nullable)
+	unsigned long long *spread;  // += the block's input cell-box volume (nullable)
 	unsigned long long *tstamp;  // 8 phase timestamps per block (diagnostics, nullable)
 	unsigned long long *diag;    // [0] += sorting-push items given a global slot one by one (nullable)
 	const unsigned char *objIn;  // object ids of the padded nodes (nullable: no objects)
@@ -2519,6 +2520,12 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 		for (int w = 0; w < NW; w++) t += wmov[w];
 		if (t) atomicAdd(a.moved, (unsigned long long)t);
 	}
+	if (a.spread && threadIdx.x == 0 && !empty) {
+		unsigned long long v = 1;
+#pragma unroll
+		for (int d = 0; d < ND; d++) v *= (unsigned long long)(chi[d] - clo[d] + 1);
+		atomicAdd(a.spread, v);
+	}
 	// flush: one global atomic per touched node / output cell
 	for (int t = threadIdx.x; t < ((PINC_PUSH_SKIP & 4) ? 0 : rB.vol); t += kPushThreads) {
 		double v = rhoL[t];
@@ -2936,6 +2943,7 @@ extern "C" int pinc_hip_push(pinc_pop_t pop, int s, pinc_geom_t g, const pinc_pu
 	a.cntNext = args->cntNext;
 	a.perm = args->perm;
 	a.moved = args->moved;
+	a.spread = args->spread;
 	a.tstamp = args->tstamp;
 	a.diag = args->diag;
 	a.objIn = args->objInside;

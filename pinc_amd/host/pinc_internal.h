@@ -104,6 +104,13 @@ struct PincDevPop {
 	double sortFraction;
 	int sortMax;
 	unsigned long long *movedCnt;       /* device, per species, this push */
+	/* population:sortSpread > 0: a sort due by the displaced fraction waits
+	 * until the blocks' mean input cell box has grown to sortSpread times its
+	 * size in the first push after the last sort (a drifting beam changes
+	 * cell without spreading); sortMax still bounds the interval */
+	double sortSpread;
+	unsigned long long *spreadCnt;      /* device, per species, this push */
+	double spreadBase[PINC_MAX_SPECIES], spreadLast[PINC_MAX_SPECIES];
 	double movedFrac[PINC_MAX_SPECIES], lastRate[PINC_MAX_SPECIES];
 	int sinceSort[PINC_MAX_SPECIES], sortNext[PINC_MAX_SPECIES];
 	/* fused object collection (pinc_obj_attach): the push flags a particle

@@ -105,9 +105,13 @@ Population *pAlloc(const dictionary *ini) {
 		dv->sortFraction = iniHas(ini, "population:sortFraction") ? iniGetDouble(ini, "population:sortFraction") : 0.0;
 		dv->sortMax = iniHas(ini, "population:sortMax") ? iniGetInt(ini, "population:sortMax") : 32;
 		if (dv->sortFraction < 0 || dv->sortMax < 1) msg(ERROR, "population:sortFraction/sortMax out of range");
+		dv->sortSpread = iniHas(ini, "population:sortSpread") ? iniGetDouble(ini, "population:sortSpread") : 0.0;
+		if (dv->sortSpread < 0) msg(ERROR, "population:sortSpread out of range");
 		if (dv->sortFraction > 0) {
 			pinc_check(pinc_hip_malloc((void **)&dv->movedCnt, PINC_MAX_SPECIES * sizeof(unsigned long long)),
 			           "pAlloc moved");
+			pinc_check(pinc_hip_malloc((void **)&dv->spreadCnt, PINC_MAX_SPECIES * sizeof(unsigned long long)),
+			           "pAlloc spread");
 			for (int s = 0; s < PINC_MAX_SPECIES; s++) dv->sortNext[s] = 1;
 		}
 	}
@@ -176,6 +180,7 @@ void pFree(Population *p) {
 		}
 		pinc_hip_free(dv->perm);
 		pinc_hip_free(dv->movedCnt);
+		pinc_hip_free(dv->spreadCnt);
 		for (int s = 0; s < PINC_MAX_SPECIES; s++) pinc_hip_free(dv->sortWork[s]);
 		pinc_hip_free(dv->chunkCount);
 		pinc_hip_free(dv->ws[0].chunkOffset);

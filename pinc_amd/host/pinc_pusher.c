@@ -329,7 +329,9 @@ static int push_all(Population *pop, Grid *E, double *const *xout) {
 				/* sort when this push's input is the one predicted to pass
 				 * the displaced fraction (counted by the push before) */
 				sortS[s] = dv->sortNext[s];
-				countS[s] = !sortS[s] && (dv->movedFrac[s] + dv->lastRate[s] >= dv->sortFraction ||
+				const int spreadOk = dv->sortSpread <= 0 || dv->spreadBase[s] <= 0 ||
+				                     dv->spreadLast[s] >= dv->sortSpread * dv->spreadBase[s];
+				countS[s] = !sortS[s] && ((dv->movedFrac[s] + dv->lastRate[s] >= dv->sortFraction && spreadOk) ||
 				                          dv->sinceSort[s] + 1 >= dv->sortMax);
 			} else {
 				sortS[s] = dv->moves % dv->sortInterval == 0;
@@ -345,9 +347,12 @@ static int push_all(Population *pop, Grid *E, double *const *xout) {
 		dv->everSorted = 1;
 	}
 	int nd = pop->nDims;
-	if (adaptive)
+	if (adaptive) {
 		pinc_check(pinc_hip_memset(dv->movedCnt, 0, PINC_MAX_SPECIES * sizeof(unsigned long long), g_pinc.stream),
 		           "moved counts");
+		pinc_check(pinc_hip_memset(dv->spreadCnt, 0, PINC_MAX_SPECIES * sizeof(unsigned long long), g_pinc.stream),
+		           "spread counts");
+	}
 	for (int s = 0; s < pop->nSpecies; s++) {
 		int countNext = countS[s];
 		pinc_check(pinc_hip_zero(dv->rhoS[s], n, g_pinc.stream), "species charge zero");
@@ -378,7 +383,10 @@ static int push_all(Population *pop, Grid *E, double *const *xout) {
 		a.kePartial = dv->kePartial;
 		a.tileWidth = dv->tileWidth;
 		pinc_check(pinc_hip_memset(a.chunkCount, 0, chunks * sizeof(int), g_pinc.stream), "chunk counts");
-		if (adaptive) a.moved = dv->movedCnt + s;
+		if (adaptive) {
+			a.moved = dv->movedCnt + s;
+			if (dv->sortSpread > 0 || g_pinc.traceSort) a.spread = dv->spreadCnt + s;
+		}
 		if (dv->objInside && dv->objHi[0] >= dv->objLo[0]) { /* (empty box: no object node in this slab) */
 			a.objInside = dv->objInside;
 			a.objSy = dv->objSy;
@@ -450,18 +458,26 @@ static int push_all(Population *pop, Grid *E, double *const *xout) {
 		}
 	}
 	if (adaptive) {
-		unsigned long long mv[PINC_MAX_SPECIES];
+		unsigned long long mv[PINC_MAX_SPECIES], sp[PINC_MAX_SPECIES];
 		pinc_check(pinc_hip_d2h(mv, dv->movedCnt, pop->nSpecies * sizeof(mv[0]), g_pinc.stream), "moved readback");
+		pinc_check(pinc_hip_d2h(sp, dv->spreadCnt, pop->nSpecies * sizeof(sp[0]), g_pinc.stream), "spread readback");
 		for (int s = 0; s < pop->nSpecies; s++) {
 			long np = pop->iStop[s] - pop->iStart[s];
 			double rate = np > 0 ? (double)mv[s] / (double)np : 0.0;
+			/* mean input cell box of this push's blocks (1024 items each) */
+			const double blocks = (double)((np + 1023) / 1024);
+			dv->spreadLast[s] = blocks > 0 ? (double)sp[s] / blocks : 0.0;
+			if (sortS[s]) dv->spreadBase[s] = 0;
+			if (dv->sinceSort[s] == 1 && !sortS[s]) dv->spreadBase[s] = dv->spreadLast[s];
 			dv->movedFrac[s] = sortS[s] ? rate : dv->movedFrac[s] + rate;
 			dv->sinceSort[s] = sortS[s] ? 1 : dv->sinceSort[s] + 1;
 			dv->lastRate[s] = rate;
 			dv->sortNext[s] = countS[s];
 			if (g_pinc.traceSort)
-				fprintf(stderr, "[pinc] push %ld species %d: moved %.4f, displaced %.4f%s%s\n", dv->moves, s, rate,
-				        dv->movedFrac[s], sortS[s] ? ", sorted" : "", countS[s] ? ", counted" : "");
+				fprintf(stderr, "[pinc] push %ld species %d: moved %.4f, displaced %.4f, cell box %.1f (x%.2f)%s%s\n",
+				        dv->moves, s, rate, dv->movedFrac[s], dv->spreadLast[s],
+				        dv->spreadBase[s] > 0 ? dv->spreadLast[s] / dv->spreadBase[s] : 0.0, sortS[s] ? ", sorted" : "",
+				        countS[s] ? ", counted" : "");
 		}
 	}
 	dv->depValid = 1;
