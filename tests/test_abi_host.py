@@ -131,3 +131,15 @@ def test_ini_and_units_match_oracle(lib, name):
         assert mass[s] == m_o[s], (s, mass[s], m_o[s])
     h.uFree(u)
     h.iniClose(d)
+
+
+def test_bench_config_sort_spread():
+    """The opt-in spread gate of the adaptive sort reaches the ini only when
+    asked for (population:sortSpread; the default schedule is unchanged)."""
+    from pinc_amd import configs
+    base = configs.bench_config("c4ts", 32, 4)
+    assert "sortSpread" not in base["population"]
+    assert base["population"]["sortFraction"] == "0.8"
+    gated = configs.bench_config("c4ts", 32, 4, sort_spread=2.0)
+    assert gated["population"]["sortSpread"] == "2.0"
+    assert "sortSpread" not in configs.bench_config("c4", 32, 4, layout="reference")["population"]
