@@ -140,8 +140,6 @@ def _cpu_baseline(size: int, ppc: int, steps: int, native: bool, workload: str =
         cfg["multigrid"]["extrapolate"] = str(extrapolate)
         cfg["multigrid"]["spectralCoarse"] = str(spectral_coarse)
     ini = configs.write_ini(cfg)
-    spread_note = (f" and the blocks' mean cell box grew {args.sort_spread:g}x since the last sort"
-                   if args.sort_spread > 0 else "")
     t_init = time.perf_counter()
     w = orc.World(ini)
     w.init(perturb=workload == "c2", maxwell=workload != "c2", seed=20260101)
@@ -312,6 +310,8 @@ def main() -> int:
                                sort_spread=args.sort_spread)
     nspecies = int(cfg["population"]["nSpecies"])
     ini = configs.write_ini(cfg)
+    spread_note = (f" and the blocks' mean cell box grew {args.sort_spread:g}x since the last sort"
+                   if args.sort_spread > 0 else "")
 
     def barrier():
         if dist is not None:
