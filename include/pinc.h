@@ -114,6 +114,21 @@ funPtr selectInner(const dictionary *ini, const char *key, const char *list, ...
 #define select(ini, key, ...) selectInner(ini, key, #__VA_ARGS__, __VA_ARGS__)
 #endif
 
+/* --------------------------------------------------------------- aux -- */
+/* Timer (core.h:419-436, aux.c:48-85): wall time in nanoseconds; tStop waits
+ * for the device work queued so far, so a span measures what the reference's
+ * blocking loop measured */
+typedef struct {
+	long long start;
+	long long total;
+} Timer;
+Timer *tAlloc();        /* main.c:192 passes the rank; unused, as in aux.c */
+void tFree(Timer *t);
+void tStart(Timer *t);
+void tStop(Timer *t);
+void tReset(Timer *t);
+void tMsg(long long nanoSec, const char *string);
+
 /* ------------------------------------------------------------- units -- */
 Units *uAlloc(dictionary *ini);
 void uFree(Units *units);
@@ -152,6 +167,12 @@ void pToGlobalFrame(Population *pop, const MpiInfo *mpiInfo);
 void pSumKinEnergy(Population *pop);
 void pSyncToHost(Population *pop);
 void pSyncToDevice(Population *pop);
+/* main.c:206,219 (population.c:342-365, 316-340): msg(ERROR) if a velocity
+ * component exceeds max / a particle left the local frame.  The kernels that
+ * move and kick the particles record both conditions in a device word; these
+ * read it */
+void pVelAssertMax(const Population *pop, double max);
+void pPosAssertInLocalFrame(const Population *pop, const Grid *grid);
 /* generate lattice (+perturbation, +Maxwellian) directly on the device */
 void pInitDevice(const dictionary *ini, Population *pop, const MpiInfo *mpiInfo, int perturb,
                  int maxwell, unsigned long long seed);
@@ -174,6 +195,13 @@ funPtr puBoris3D1KE_set(dictionary *ini);
 void puBoris3D1(Population *pop, Grid *E, const double *T, const double *S);
 void puBoris3D1KE(Population *pop, Grid *E, const double *T, const double *S);
 void puGet3DRotationParameters(dictionary *ini, double *T, double *S);
+/* order 0, nearest grid point (pusher.c:310-391, 640-668, puInterpND0
+ * :1164-1180); puAccND0_set returns puAccND0KE as in the reference */
+funPtr puAccND0_set(dictionary *ini);
+funPtr puAccND0KE_set(dictionary *ini);
+funPtr puDistrND0_set(dictionary *ini);
+void puAccND0KE(Population *pop, Grid *E);
+void puDistrND0(const Population *pop, Grid *rho);
 funPtr puDistr3D1_set(dictionary *ini);
 funPtr puDistrND1_set(dictionary *ini);
 void puDistr3D1(const Population *pop, Grid *rho);
@@ -229,10 +257,17 @@ long sSolveCount(const SpectralSolver *solver);
 int sSolveDistributed(const SpectralSolver *solver);
 
 /* ------------------------------------------------ immersed objects -- */
-/* object.c on the device (pinc_obj.c): objects
- * from objects:sphere = cx,cy,cz,r or objects:file (an .h5 with /Object
- * [nz,ny,nx,1], values 1..K); population:fused = 0 */
+/* object.c on the device (pinc_obj.c).  As main.c:95,
+ * 126-127: oAlloc, then oOpenH5(ini, obj, mpiInfo, units, denorm, "test")
+ * names <files:output>_test.grid.h5 and oReadH5 reads its /Object [nz,ny,nx,1]
+ * (values 1..K) and builds the tables (object.c:717-756); a missing file or
+ * an all-zero mask is a run without objects.  Extension: objects:sphere =
+ * cx,cy,cz,r or objects:file = <.h5> in the ini builds them in oAlloc. */
 Object *oAlloc(const dictionary *ini);
+void oOpenH5(const dictionary *ini, Object *obj, const MpiInfo *mpiInfo, const Units *units, double denorm,
+             const char *fName);
+void oReadH5(Object *obj, const MpiInfo *mpiInfo);
+void oCloseH5(Object *obj);
 void oFree(Object *obj);
 void oComputeCapacitanceMatrix(Object *obj, const dictionary *ini, const MpiInfo *mpiInfo);
 void oApplyCapacitanceMatrix(Grid *rho, const Grid *phi, const Object *obj, const MpiInfo *mpiInfo);
@@ -264,8 +299,21 @@ int pinc_h5_dims(const char *path, const char *name, long *dimsOut);
 int pinc_h5_write(const char *path, const char *name, int rank, const long *dims, const double *data);
 
 /* ---------------------------------------------------------- run mode -- */
+/* regular (main.c:50-304): one process per GPU, the world taken from the
+ * launcher (pinc_boot.c: PINC_RANK/PINC_WORLD_SIZE, torchrun, Open MPI,
+ * MPICH/PMI or Slurm variables; RCCL over xGMI, or PINC_TRANSPORT=host) */
 void regular(dictionary *ini);
 funPtr regular_set(dictionary *ini);
+/* the reference's diagnostic run modes (multigrid.c:1731-1900, spectral.c:
+ * 117-150) are outside this build's hot path: their
+ * selectors exist so main.c's select list links; selecting one ends the run
+ * with msg(ERROR) */
+funPtr mgMode_set(dictionary *ini);
+funPtr mgModeErrorScaling_set(dictionary *ini);
+funPtr sMode_set(dictionary *ini);
+/* a process that sets its world through PincSimOpts (Python, bench.py)
+ * declares it before any other call, so that no launcher variable is read */
+void pinc_world_explicit(void);
 
 /* ====================================================== PincSim API ===== */
 /* One process per GPU.  A simulation owns the ini, units, population, grids

@@ -38,9 +38,11 @@ typedef struct {
 	int nloc;      /* true cells of this rank along the slab dimension */
 	int off;       /* first true cell of this rank along the slab dim */
 	int nranks;    /* slabs along the slab dimension */
-	int literal;   /* main.c's double rho FROMHALO (literal loop): deposits on
+	int literal;   /* main.c's double rho FROMHALO (literal loop): 1 = deposits on
 	                  periodic ghost nodes of the non-slab dims count twice per
-	                  ghost coordinate */
+	                  ghost coordinate; 2 = only the weight a plain deposit
+	                  misses for a second fold, (2^g - 1) per weight, doubled on
+	                  slab ghost planes (the second fold adds them once more) */
 } pinc_geom_t;
 
 /* a population on the device (by value; pointers are device pointers) */
@@ -264,6 +266,19 @@ int pinc_hip_deposit(pinc_pop_t pop, int s, pinc_geom_t g, double *rhoSlab, void
  * n doubles of the slab E grid; qm/mq are device arrays. */
 int pinc_hip_field_chain(const double *E, double *Es, long n, const double *qm, const double *mq,
                          double pre, int s, void *stream);
+
+/* order 0 (nearest grid point, node (int)(x + 0.5)): puDistrND0
+ * (pusher.c:640-668) adds one unit per particle of species s (the caller
+ * applies the 1/q, q chain); puAccND0KE (pusher.c:310-353, puInterpND0
+ * :1164-1180) v += Es at the node, KE partials as pinc_hip_accelerate */
+int pinc_hip_deposit_ngp(pinc_pop_t pop, int s, pinc_geom_t g, double *rhoSlab, void *stream);
+int pinc_hip_accelerate_ngp(pinc_pop_t pop, int s, pinc_geom_t g, const double *Es, double *kePartial,
+                            int *nBlocks, void *stream);
+/* pVelAssertMax (population.c:342-365) over species s: a velocity component
+ * above maxVel sets bit 0 of *errFlag */
+int pinc_hip_vel_assert(pinc_pop_t pop, int s, double maxVel, int *errFlag, void *stream);
+/* particles per workgroup of pinc_hip_push (a build constant) */
+long pinc_hip_push_chunk(void);
 
 /* puAcc3D1KE / puAccND1KE (pusher.c:178-265) with puInterp3D1/ND1
  * (pusher.c:1089-1162), gathering from Es (pinc_hip_field_chain).

@@ -103,8 +103,9 @@ typedef struct {
 	OMg mgRho, mgPhi, mgRes;
 } ORank;
 
-enum { ORC_ACC_3D1KE, ORC_ACC_ND1KE, ORC_ACC_3D1, ORC_ACC_ND1, ORC_ACC_BORIS3D1KE, ORC_ACC_BORIS3D1 };
-enum { ORC_DISTR_3D1, ORC_DISTR_ND1 };
+enum { ORC_ACC_3D1KE, ORC_ACC_ND1KE, ORC_ACC_3D1, ORC_ACC_ND1, ORC_ACC_BORIS3D1KE, ORC_ACC_BORIS3D1,
+       ORC_ACC_ND0KE, ORC_ACC_ND0 };
+enum { ORC_DISTR_3D1, ORC_DISTR_ND1, ORC_DISTR_ND0 };
 enum { ORC_MIG_3D, ORC_MIG_ND };
 enum { ORC_SMOOTH_GS3D, ORC_SMOOTH_GSND };
 enum { ORC_RESTR_3D, ORC_RESTR_ND };
@@ -181,6 +182,8 @@ void opu_rotation_params(int nSpecies, const double *BExt, const double *charge,
 void opu_accnd1(OPop *p, OGrid *E, int ke);
 void opu_distr3d1(const OPop *p, OGrid *rho);
 void opu_distrnd1(const OPop *p, OGrid *rho);
+void opu_accnd0(OPop *p, OGrid *E, int ke);
+void opu_distrnd0(const OPop *p, OGrid *rho);
 void opu_extract3d(OPop *p, OMpi *mpi);
 void opu_extractnd(OPop *p, OMpi *mpi);
 void ow_migrate(OWorld *w);

@@ -7,6 +7,8 @@
  *                   + puInterpND1(Inner)               pusher.c:1124-1162
  *   opu_distr3d1    puDistr3D1                         pusher.c:512-572
  *   opu_distrnd1    puDistrND1(+Inner)                 pusher.c:578-638
+ *   opu_accnd0      puAccND0KE + puInterpND0           pusher.c:310-353, 1164-1180
+ *   opu_distrnd0    puDistrND0                         pusher.c:640-668
  *   opu_extract3d   puExtractEmigrants3D               pusher.c:782-855
  *   opu_extractnd   puExtractEmigrantsND               pusher.c:862-910
  *   ow_migrate      puMigrate: exchangeNMigrants,      pusher.c:914-1035
@@ -217,6 +219,49 @@ void opu_distrnd1(const OPop *p, OGrid *rho){
 				q += in*sp[d+1];
 			}
 			distrnd_inner(rho->val, q, &sp[nd], sp[1], &dec[nd-1], &comp[nd-1], 1);
+		}
+		og_mul(rho, p->charge[s]);
+	}
+}
+
+/* order 0 (nearest grid point): puAccND0KE (pusher.c:310-353) with
+ * puInterpND0 (pusher.c:1164-1180), and puDistrND0 (pusher.c:640-668); the
+ * node is (int)(x + 0.5) per dimension */
+void opu_accnd0(OPop *p, OGrid *E, int ke){
+	int nd = p->nDims;
+	const long *sp = E->sizeProd;
+	for(int s = 0; s < p->nSpecies; s++){
+		og_mul(E, p->charge[s]/p->mass[s]);
+		if(ke) p->kinEnergy[s] = 0;
+		for(long i = p->iStart[s]; i < p->iStop[s]; i++){
+			const double *x = &p->pos[nd*i];
+			double *v = &p->vel[nd*i];
+			long q = 0;
+			for(int d = 0; d < nd; d++) q += sp[d+1]*(int)(x[d]+0.5);
+			double vs = 0;
+			for(int d = 0; d < nd; d++){
+				double dv = E->val[q+d];
+				vs += v[d]*(v[d]+dv);
+				v[d] += dv;
+			}
+			if(ke) p->kinEnergy[s] += vs;
+		}
+		if(ke) p->kinEnergy[s] *= 0.5*p->mass[s];
+		og_mul(E, p->mass[s]/p->charge[s]);
+	}
+}
+
+void opu_distrnd0(const OPop *p, OGrid *rho){
+	og_zero(rho);
+	int nd = p->nDims;
+	const long *sp = rho->sizeProd;
+	for(int s = 0; s < p->nSpecies; s++){
+		og_mul(rho, 1.0/p->charge[s]);
+		for(long i = p->iStart[s]; i < p->iStop[s]; i++){
+			const double *pos = &p->pos[nd*i];
+			long q = 0;
+			for(int d = 0; d < nd; d++) q += (int)(pos[d]+0.5)*sp[d+1];
+			rho->val[q]++;
 		}
 		og_mul(rho, p->charge[s]);
 	}

@@ -141,12 +141,16 @@ static void sanity(const OIni *ini, int dim, int order){
 
 static void select_methods(OWorld *w){
 	OIni *ini = w->ini;
-	const char *acc[] = {"puAcc3D1KE", "puAccND1KE", "puAcc3D1", "puAccND1", "puBoris3D1KE", "puBoris3D1"};
-	w->acc = pick(ini, "methods:acc", acc, 6);
-	sanity(ini, (w->acc == ORC_ACC_ND1KE || w->acc == ORC_ACC_ND1) ? 0 : 3, 1);
-	const char *distr[] = {"puDistr3D1", "puDistrND1"};
-	w->distr = pick(ini, "methods:distr", distr, 2);
-	sanity(ini, w->distr == ORC_DISTR_3D1 ? 3 : 0, 1);
+	const char *acc[] = {"puAcc3D1KE", "puAccND1KE", "puAcc3D1", "puAccND1", "puBoris3D1KE", "puBoris3D1",
+	                     "puAccND0KE", "puAccND0"};
+	w->acc = pick(ini, "methods:acc", acc, 8);
+	/* puAccND0_set returns puAccND0KE (pusher.c:356-358) */
+	if(w->acc == ORC_ACC_ND0) w->acc = ORC_ACC_ND0KE;
+	const int acc0 = w->acc == ORC_ACC_ND0KE;
+	sanity(ini, (w->acc == ORC_ACC_ND1KE || w->acc == ORC_ACC_ND1 || acc0) ? 0 : 3, acc0 ? 0 : 1);
+	const char *distr[] = {"puDistr3D1", "puDistrND1", "puDistrND0"};
+	w->distr = pick(ini, "methods:distr", distr, 3);
+	sanity(ini, w->distr == ORC_DISTR_3D1 ? 3 : 0, w->distr == ORC_DISTR_ND0 ? 0 : 1);
 	const char *mig[] = {"puExtractEmigrants3D", "puExtractEmigrantsND"};
 	w->migrate = pick(ini, "methods:migrate", mig, 2);
 	if(w->migrate == ORC_MIG_3D && oini_int(ini, "grid:nDims") != 3)
@@ -304,6 +308,7 @@ static void do_distr(OWorld *w){
 	PER_RANK
 	for(int r = 0; r < w->P; r++){
 		if(w->distr == ORC_DISTR_3D1) opu_distr3d1(&w->r[r].pop, &w->r[r].rho);
+		else if(w->distr == ORC_DISTR_ND0) opu_distrnd0(&w->r[r].pop, &w->r[r].rho);
 		else opu_distrnd1(&w->r[r].pop, &w->r[r].rho);
 		rho[r] = &w->r[r].rho;
 	}
@@ -336,6 +341,7 @@ static void do_acc(OWorld *w){
 		case ORC_ACC_ND1KE: opu_accnd1(p, E, 1); break;
 		case ORC_ACC_BORIS3D1KE: opu_boris3d1(p, E, w->borisT, w->borisS, 1); break;
 		case ORC_ACC_BORIS3D1:   opu_boris3d1(p, E, w->borisT, w->borisS, 0); break;
+		case ORC_ACC_ND0KE: opu_accnd0(p, E, 1); break;
 		default:            opu_accnd1(p, E, 0); break;
 		}
 	}
@@ -509,6 +515,7 @@ void orc_op(OWorld *w, const char *name){
 	else if(!strcmp(name, "distr_nohalo")){
 		for(int r = 0; r < w->P; r++){
 			if(w->distr == ORC_DISTR_3D1) opu_distr3d1(&w->r[r].pop, &w->r[r].rho);
+			else if(w->distr == ORC_DISTR_ND0) opu_distrnd0(&w->r[r].pop, &w->r[r].rho);
 			else opu_distrnd1(&w->r[r].pop, &w->r[r].rho);
 		}
 	}

@@ -63,6 +63,9 @@ def _load() -> tuple[C.CDLL, C.CDLL]:
 
 
 HIP, HOST = _load()
+# this process sets its world through PincSimOpts (rank, size, device, RCCL
+# id): the library must not read launcher variables (torchrun's RANK etc.)
+HOST.pinc_world_explicit()
 
 
 def runtime_stack() -> dict:

@@ -38,7 +38,7 @@ HIP_FLAGS = ["-std=c++17", "-O3", f"--offload-arch={ARCH}", "-ffp-contract=off",
 C_FLAGS = ["-std=c11", "-O2", "-fPIC", "-Wall", "-ffp-contract=off", f"-I{INC}", f"-I{HOST}"]
 
 HIP_SRC = ["runtime.hip", "k_particles.hip", "k_grid.hip", "k_mg.hip", "k_spectral.hip", "k_objects.hip"]
-C_SRC = ["pinc_core.c", "pinc_comm.c", "pinc_grid.c", "pinc_pop.c", "pinc_pusher.c", "pinc_mg.c", "pinc_spectral.c", "pinc_regular.c", "pinc_h5.c", "pinc_obj.c"]
+C_SRC = ["pinc_core.c", "pinc_boot.c", "pinc_comm.c", "pinc_grid.c", "pinc_pop.c", "pinc_pusher.c", "pinc_mg.c", "pinc_spectral.c", "pinc_regular.c", "pinc_h5.c", "pinc_obj.c"]
 
 
 def _run(cmd: list[str]) -> None:

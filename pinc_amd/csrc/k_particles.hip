@@ -420,20 +420,35 @@ __device__ __forceinline__ void cic_weights(const double *dec, const double *com
 // coordinates (checked against grid.c:340-406 applied twice).  Slab ghost
 // planes are kept on the device and folded twice by the caller; here the
 // non-slab dimensions, which are wrapped at deposit, get their factor.
+// literal == 2 is the second fold of a deposit made without that factor
+// (main.c's loop calling gHaloOp(addSlice, rho, FROMHALO) twice on a library
+// that was not told in advance, pinc_grid.c): the weight still missing,
+// (2^g_xy - 1) w, and twice that on a slab ghost plane, which the second fold
+// adds once more.
+template <int ND>
+__device__ __forceinline__ double literal_node_factor(const pinc_geom_t &g, const int *p) {
+	const int slab = g.nd - 1;
+	double m = 1.0, mz = 1.0;
+#pragma unroll
+	for (int d = 0; d < ND; d++) {
+		if (d == slab) {
+			if (g.literal == 2 && (p[d] == 0 || p[d] == g.nloc + 1)) mz = 2.0;
+			continue;
+		}
+		if (p[d] == 0 || p[d] == g.T[d] + 1) m *= 2.0;
+	}
+	return g.literal == 2 ? (m - 1.0) * mz : m;
+}
+
 template <int ND>
 __device__ __forceinline__ void literal_ghost_weights(const pinc_geom_t &g, const int *j, double *w) {
 	if (!g.literal) return;
-	const int slab = g.nd - 1;
 #pragma unroll
 	for (int c = 0; c < (1 << ND); c++) {
-		double m = 1.0;
+		int p[3];
 #pragma unroll
-		for (int d = 0; d < ND; d++) {
-			if (d == slab) continue;
-			int p = j[d] + ((c >> d) & 1);
-			if (p == 0 || p == g.T[d] + 1) m *= 2.0;
-		}
-		w[c] *= m;
+		for (int d = 0; d < ND; d++) p[d] = j[d] + ((c >> d) & 1);
+		w[c] *= literal_node_factor<ND>(g, p);
 	}
 }
 
@@ -2574,9 +2589,133 @@ __global__ void k_rho_combine(double *__restrict__ rho, CombineArgs c, long n) {
 	}
 }
 
+// ------------------------------------------------- order 0 (NGP) ---------
+// puDistrND0 (pusher.c:640-668) and puAccND0KE (pusher.c:310-353) with
+// puInterpND0 (pusher.c:1164-1180): the nearest node (int)(x + 0.5) of the
+// padded local frame takes the whole particle (one unit; the caller applies
+// the species' 1/q, q chain) and lends it its E.  Not on the hot path (main.c
+// offers them through select; the configs use CIC): one thread per particle,
+// global atomics.
+template <int ND>
+__global__ __launch_bounds__(kThreads) void k_deposit_ngp(const double *__restrict__ x0,
+                                                          const double *__restrict__ x1,
+                                                          const double *__restrict__ x2, long b0, long n,
+                                                          pinc_geom_t g, double *__restrict__ rho) {
+	Geo G = make_geo(g);
+	const double *xs[3] = {x0, x1, x2};
+	for (long i = (long)blockIdx.x * kThreads + threadIdx.x; i < n; i += (long)gridDim.x * kThreads) {
+		int j[3] = {0, 0, 0};
+		long off = 0;
+#pragma unroll
+		for (int d = 0; d < ND; d++) {
+			j[d] = (int)(xs[d][b0 + i] + 0.5);
+			off += node_off(G, d, j[d]);
+		}
+		const double w = g.literal ? literal_node_factor<ND>(g, j) : 1.0;
+		if (w != 0.0) unsafeAtomicAdd(&rho[off], w);
+	}
+}
+
+template <int ND>
+__global__ __launch_bounds__(kThreads) void k_accel_ngp(const double *__restrict__ x0, const double *__restrict__ x1,
+                                                        const double *__restrict__ x2, double *__restrict__ v0,
+                                                        double *__restrict__ v1, double *__restrict__ v2, long b0,
+                                                        long n, pinc_geom_t g, const double *__restrict__ E,
+                                                        double *__restrict__ kePartial) {
+	__shared__ double red[kThreads / 64];
+	Geo G = make_geo(g);
+	const double *xs[3] = {x0, x1, x2};
+	double *vs[3] = {v0, v1, v2};
+	double ke = 0.0;
+	// block b owns particles [b kAccChunk, (b+1) kAccChunk): the KE partials
+	// have pinc_hip_accelerate's layout
+	for (int k = 0; k < kAccItems; k++) {
+		const long i = (long)blockIdx.x * kAccChunk + (long)k * kThreads + threadIdx.x;
+		if (i >= n) break;
+		long off = 0;
+#pragma unroll
+		for (int d = 0; d < ND; d++) off += node_off(G, d, (int)(xs[d][b0 + i] + 0.5));
+		off *= ND;
+		double vsq = 0.0;
+#pragma unroll
+		for (int d = 0; d < ND; d++) {
+			const double dv = E[off + d];
+			const double vv = vs[d][b0 + i];
+			vsq += vv * (vv + dv);
+			vs[d][b0 + i] = vv + dv;
+		}
+		ke += vsq;
+	}
+	const double t = block_sum(ke, red);
+	if (threadIdx.x == 0) kePartial[blockIdx.x] = t;
+}
+
+// pVelAssertMax (population.c:342-365): a component above maxVel (signed, as
+// the reference) sets bit 0 of the assert word
+__global__ __launch_bounds__(kThreads) void k_vel_assert(const double *__restrict__ v0, const double *__restrict__ v1,
+                                                         const double *__restrict__ v2, long b0, long n, int nd,
+                                                         double maxVel, int *__restrict__ err) {
+	const double *vs[3] = {v0, v1, v2};
+	int bad = 0;
+	for (long i = (long)blockIdx.x * kThreads + threadIdx.x; i < n; i += (long)gridDim.x * kThreads)
+		for (int d = 0; d < nd; d++) bad |= vs[d][b0 + i] > maxVel;
+	if (bad) atomicOr(err, 1);
+}
+
 }  // namespace
 
 // =========================================================== C ABI ========
+extern "C" long pinc_hip_push_chunk(void) { return kPushChunk; }
+
+extern "C" int pinc_hip_deposit_ngp(pinc_pop_t pop, int s, pinc_geom_t g, double *rho, void *stream) {
+	long n = pop.iStop[s] - pop.iStart[s];
+	if (n <= 0) return 0;
+	long b0 = pop.iStart[s];
+	long nb = ceil_div(n, (long)kThreads);
+	if (nb > 65536) nb = 65536;
+	hipStream_t st = (hipStream_t)stream;
+	const double *x1 = g.nd > 1 ? pop.x[1] : nullptr, *x2 = g.nd > 2 ? pop.x[2] : nullptr;
+	if (g.nd == 3)
+		hipLaunchKernelGGL(k_deposit_ngp<3>, dim3(nb), dim3(kThreads), 0, st, pop.x[0], x1, x2, b0, n, g, rho);
+	else if (g.nd == 2)
+		hipLaunchKernelGGL(k_deposit_ngp<2>, dim3(nb), dim3(kThreads), 0, st, pop.x[0], x1, x2, b0, n, g, rho);
+	else
+		hipLaunchKernelGGL(k_deposit_ngp<1>, dim3(nb), dim3(kThreads), 0, st, pop.x[0], x1, x2, b0, n, g, rho);
+	return check_launch("deposit (NGP)");
+}
+
+extern "C" int pinc_hip_accelerate_ngp(pinc_pop_t pop, int s, pinc_geom_t g, const double *Es, double *kePartial,
+                                       int *nBlocks, void *stream) {
+	long n = pop.iStop[s] - pop.iStart[s];
+	*nBlocks = 0;
+	if (n <= 0) return 0;
+	long b0 = pop.iStart[s];
+	long nb = ceil_div(n, (long)kAccChunk);
+	*nBlocks = (int)nb;
+	hipStream_t st = (hipStream_t)stream;
+	if (g.nd == 3)
+		hipLaunchKernelGGL(k_accel_ngp<3>, dim3(nb), dim3(kThreads), 0, st, pop.x[0], pop.x[1], pop.x[2], pop.v[0],
+		                   pop.v[1], pop.v[2], b0, n, g, Es, kePartial);
+	else if (g.nd == 2)
+		hipLaunchKernelGGL(k_accel_ngp<2>, dim3(nb), dim3(kThreads), 0, st, pop.x[0], pop.x[1], nullptr, pop.v[0],
+		                   pop.v[1], nullptr, b0, n, g, Es, kePartial);
+	else
+		hipLaunchKernelGGL(k_accel_ngp<1>, dim3(nb), dim3(kThreads), 0, st, pop.x[0], nullptr, nullptr, pop.v[0],
+		                   nullptr, nullptr, b0, n, g, Es, kePartial);
+	return check_launch("accelerate (NGP)");
+}
+
+extern "C" int pinc_hip_vel_assert(pinc_pop_t pop, int s, double maxVel, int *errFlag, void *stream) {
+	long n = pop.iStop[s] - pop.iStart[s];
+	if (n <= 0) return 0;
+	long nb = ceil_div(n, (long)kThreads * 8);
+	if (nb > 16384) nb = 16384;
+	long b0 = pop.iStart[s];
+	hipLaunchKernelGGL(k_vel_assert, dim3(nb), dim3(kThreads), 0, (hipStream_t)stream, pop.v[0],
+	                   pop.nd > 1 ? pop.v[1] : nullptr, pop.nd > 2 ? pop.v[2] : nullptr, b0, n, pop.nd, maxVel,
+	                   errFlag);
+	return check_launch("velocity assert");
+}
 extern "C" int pinc_hip_move_classify(pinc_pop_t pop, int s, int doMove, const double *thr,
                                       unsigned char *flags, int *chunkCount, double maxVel,
                                       int *errFlag, int wrapMask, void *stream) {

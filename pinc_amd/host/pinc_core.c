@@ -19,6 +19,15 @@ PincCtx g_pinc;
 /* ---------------------------------------------------------------- msg -- */
 static char g_lastError[1024];
 
+/* rank 0 prints (io.c:170-217); before the world is set up (gAllocMpi) the
+ * rank comes from the launcher's environment, as MPI_Init has it in main() */
+static int msg_rank(void) {
+	if (g_pinc.initialised) return g_pinc.rank;
+	int r, n, l;
+	pinc_launcher_env(&r, &n, &l);
+	return r;
+}
+
 void msg(msgKind kind, const char *format, ...) {
 	char buf[1024];
 	va_list ap;
@@ -34,7 +43,7 @@ void msg(msgKind kind, const char *format, ...) {
 	default: break;
 	}
 	if ((kind & 0x0F) == ERROR) snprintf(g_lastError, sizeof(g_lastError), "%s", buf);
-	if ((kind & ALL) || g_pinc.rank == 0) {
+	if ((kind & ALL) || msg_rank() == 0) {
 		/* STATUS lines print as in the reference (only regular() emits them);
 		 * PINC_QUIET silences them */
 		if ((kind & 0x0F) != STATUS || !getenv("PINC_QUIET")) fprintf(stream, "%s: %s\n", prefix, buf);
@@ -469,7 +478,10 @@ void uNormalize(dictionary *ini, const Units *u) {
 }
 
 /* ------------------------------------------------------------ context -- */
-void pinc_ctx_require(void) {
+/* the device context of this process; its world (rank, size, device) comes
+ * from the PincSim options or, for a main.c-style caller, from the launcher
+ * (pinc_boot.c) */
+void pinc_ctx_init(void) {
 	if (g_pinc.initialised) return;
 	pinc_check(pinc_hip_set_device(g_pinc.device), "set device");
 	pinc_check(pinc_hip_stream_create(&g_pinc.stream), "stream");
@@ -482,6 +494,11 @@ void pinc_ctx_require(void) {
 	g_pinc.traceSort = getenv("PINC_TRACE_SORT") ? atoi(getenv("PINC_TRACE_SORT")) : 0;
 	for (int i = 0; i < 2 * PINC_NPHASES; i++) pinc_check(pinc_hip_event_create(&g_pinc.ev[i]), "event");
 	g_pinc.initialised = 1;
+}
+
+void pinc_ctx_require(void) {
+	if (g_pinc.initialised) return;
+	pinc_boot_world();
 }
 
 void pinc_phase_begin(int p) {
@@ -570,4 +587,43 @@ double pinc_reduce_host(int nParts, double div) {
 	double v = 0;
 	pinc_check(pinc_hip_d2h(&v, PINC_SLOT(0), sizeof(double), g_pinc.stream), "reduce readback");
 	return v;
+}
+
+/* -------------------------------------------------------------- timer -- */
+/* aux.c:48-85 (Timer, core.h:419-436).  The operators queue device work, so
+ * tStop first waits for the stream: a tStart/tStop span then covers the work
+ * issued inside it, as the reference's blocking loop did. */
+#include <time.h>
+static long long now_ns(void) {
+	struct timespec t;
+	clock_gettime(CLOCK_MONOTONIC, &t);
+	return (long long)t.tv_sec * 1000000000LL + t.tv_nsec;
+}
+
+Timer *tAlloc() {
+	Timer *t = malloc(sizeof(*t));
+	t->start = 0;
+	t->total = 0;
+	return t;
+}
+
+void tFree(Timer *t) { free(t); }
+
+void tStart(Timer *t) {
+	if (g_pinc.initialised) pinc_check(pinc_hip_stream_sync(g_pinc.stream), "tStart");
+	t->start = now_ns();
+}
+
+void tStop(Timer *t) {
+	if (g_pinc.initialised) pinc_check(pinc_hip_stream_sync(g_pinc.stream), "tStop");
+	t->total += now_ns() - t->start;
+}
+
+void tReset(Timer *t) { t->total = 0; }
+
+void tMsg(long long nanoSec, const char *string) {
+	if (nanoSec >= 1000000000LL) msg(TIMER, "%s %6.2fs ", string, (double)nanoSec / 1e9);
+	else if (nanoSec > 1000000LL) msg(TIMER, "%s %6.2fms ", string, (double)nanoSec / 1e6);
+	else if (nanoSec > 1000LL) msg(TIMER, "%s %6.2fus ", string, (double)nanoSec / 1e3);
+	else msg(TIMER, "%s %6.2fns ", string, (double)nanoSec);
 }

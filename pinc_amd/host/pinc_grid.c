@@ -151,6 +151,7 @@ void gFree(Grid *g) {
 		pinc_hip_free(g->dev->recv[0]);
 		pinc_hip_free(g->dev->recv[1]);
 		pinc_hip_free(g->dev->scaled);
+		pinc_hip_free(g->dev->lit);
 		free(g->dev);
 	}
 	free(g->val);
@@ -273,6 +274,9 @@ void gHaloOp(funPtr sliceOp, Grid *grid, const MpiInfo *mpiInfo, opDirection dir
 	long ps = dv->planeSize * dv->nValues;
 	int nl = geo.nloc;
 	if (sliceOp == (funPtr)addSlice && dir == FROMHALO) {
+		/* main.c:232's second fold of one deposit (main.c:226 was the first) */
+		if (dv->depPop && dv->folds == 1 && !geo.literal) pinc_literal_second_fold(dv->depPop, grid, dv->depOrder);
+		dv->folds++;
 		if (g_pinc.nranks == 1) {
 			pinc_check(pinc_hip_fold_self(dv->d, geo, g_pinc.stream), "fold");
 		} else {
@@ -341,6 +345,7 @@ void gMul(Grid *grid, double num) {
 void gZero(Grid *grid) {
 	pinc_check(pinc_hip_zero(grid->dev->d, grid->dev->n, g_pinc.stream), "gZero");
 	grid->dev->ghostsValid = 0;
+	grid->dev->depPop = NULL;
 }
 
 void gAddTo(Grid *result, Grid *addition) {

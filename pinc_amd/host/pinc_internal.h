@@ -13,6 +13,8 @@
 
 #define PINC_NNE 27
 
+typedef struct PincObj PincObj;
+
 /* one process drives one GPU: stream, communicator and scratch are global,
  * as the reference relies on MPI_COMM_WORLD */
 typedef struct {
@@ -120,7 +122,12 @@ struct PincDevPop {
 	long objSy, objSz, objNodes;
 	int *objCount;
 	int objK;
+	PincObj *objOwner;                  /* the object set attached (pFree detaches it) */
 	int objLo[3], objHi[3];
+	/* the host mirror was written (pPosLattice, pPosPerturb, pVelZero,
+	 * pVelMaxwell) and is the truth until the next device operator uploads
+	 * it (pinc_pop_flush_host): main.c never calls pSyncToDevice */
+	int hostDirty;
 	/* multi-rank migration buffers (AoS records: nd pos, nd vel, ne) */
 	double *sendBuf[2], *recvBuf[2];
 	long sendCap, recvCap;
@@ -142,10 +149,15 @@ struct PincDevGrid {
 	double *ext;
 	int extOff, extPlanes;
 	int extStale;       /* owned planes written (gSyncToDevice), halo not yet refreshed */
+	/* main.c's second gHaloOp(addSlice, rho, FROMHALO) of a step
+	 * (main.c:226,232): the population of the last deposit, its order (0 NGP,
+	 * 1 CIC) and the folds since; lit is the scratch of the missing weight */
+	const Population *depPop;
+	int depOrder, folds;
+	double *lit;
 };
 
 /* immersed objects (pinc_obj.c; object.c, config C5) */
-typedef struct PincObj PincObj;
 PincObj *pinc_obj_create(const dictionary *ini, const Grid *rho);
 void pinc_obj_free(PincObj *o);
 void pinc_obj_capacitance(PincObj *o, Grid *rho, Grid *phi, void *solver,
@@ -155,6 +167,8 @@ void pinc_obj_add_rho(PincObj *o, Grid *rho);
 void pinc_obj_attach(PincObj *o, Population *pop);
 double pinc_obj_apply(PincObj *o, Grid *rho, const Grid *phi);
 long pinc_obj_nsurface(const PincObj *o);
+/* the attached population is being freed (main.c frees pop before obj) */
+void pinc_obj_forget_pop(PincObj *o);
 /* slab-distributed Poisson solve with a slab plan (pinc_spectral.c) */
 void pinc_slab_poisson(pinc_fft_slab_t *plan, const double *rhoSlab, double *phiSlab, const char *what);
 double pinc_obj_collected(const PincObj *o);
@@ -215,6 +229,18 @@ void pinc_comm_allgather(const double *send, double *recv, long count, const cha
 void pinc_comm_allreduce_sum(double *buf, long count, const char *what);
 int pinc_comm_host_transport(void);
 void pinc_ext_halo(double *a, long ps, int nloc, int h);
+
+/* process world and device context (pinc_boot.c, pinc_core.c) */
+int pinc_boot_world(void);
+void pinc_boot_configured(void);
+const char *pinc_launcher_env(int *rank, int *size, int *local);
+void pinc_ctx_init(void);
+
+/* upload a host-written population before a device operator reads it */
+void pinc_pop_flush_host(const Population *pop);
+/* the weight a deposit without the literal factor misses for the second fold
+ * of main.c:232 (pinc_pusher.c) */
+void pinc_literal_second_fold(const Population *pop, Grid *rho, int order);
 
 /* helpers shared by the host translation units */
 void pinc_ctx_require(void);

@@ -77,6 +77,11 @@ struct PincObj {
 	int bbLo[3], bbHi[3]; /* bounding box of this rank's interior nodes (padded coordinates) */
 	PincDevPop *pop;     /* population attached for the fused collection */
 	int T[3];
+	/* main.c's order (oAlloc, oOpenH5, oReadH5): the tables are built when
+	 * oReadH5 reads the mask named by oOpenH5 */
+	int pending;
+	pinc_geom_t geom;
+	char *h5path;
 };
 
 static void invert(double *A, double *inv, long n) {
@@ -138,8 +143,20 @@ static double *read_mask(const dictionary *ini, const int T[3]) {
 	return mk;
 }
 
-static PincObj *obj_create(const dictionary *ini, const pinc_geom_t *g) {
-	if (!iniHas(ini, "objects:sphere") && !iniHas(ini, "objects:file")) return NULL;
+static int capacitance_green(const dictionary *ini) {
+	int green = 0;
+	if (iniHas(ini, "objects:capacitance")) {
+		char *c = iniGetStr(ini, "objects:capacitance");
+		if (!strcmp(c, "green")) green = 1;
+		else if (strcmp(c, "solve")) msg(ERROR, "objects:capacitance=%s (solve or green)", c);
+		free(c);
+	}
+	return green;
+}
+
+/* the lookup tables of a mask over the true nodes (mk, [z][y][x] object
+ * ids, consumed); an all-zero mask gives an object set with nObj = 0 */
+static PincObj *obj_from_mask(double *mk, const pinc_geom_t *g, int green) {
 	if (g->nd != 3) msg(ERROR, "objects are 3-D (object.c)");
 	PincObj *o = calloc(1, sizeof(*o));
 	const int T[3] = {g->T[0], g->T[1], g->T[2]};
@@ -148,7 +165,7 @@ static PincObj *obj_create(const dictionary *ini, const pinc_geom_t *g) {
 	o->sy = S[0];
 	o->sz = (long)S[0] * S[1];
 	o->nNodes = o->sz * S[2];
-	double *mk = read_mask(ini, T);
+	o->geom = *g;
 	/* object ids (oFillLookupTables, object.c:117-121: the highest value is
 	 * the object count) */
 	int nObj = 0;
@@ -157,11 +174,11 @@ static PincObj *obj_create(const dictionary *ini, const pinc_geom_t *g) {
 	if (nObj > 255) msg(ERROR, "objects: at most 255 objects");
 	o->nObj = nObj;
 	for (int d = 0; d < 3; d++) o->T[d] = T[d];
-	if (iniHas(ini, "objects:capacitance")) {
-		char *c = iniGetStr(ini, "objects:capacitance");
-		if (!strcmp(c, "green")) o->green = 1;
-		else if (strcmp(c, "solve")) msg(ERROR, "objects:capacitance=%s (solve or green)", c);
-		free(c);
+	o->green = green;
+	if (nObj == 0) {
+		free(mk);
+		o->haveCap = 1;
+		return o;
 	}
 #define ID(x, y, z) ((int)(mk[((x) + T[0]) % T[0] + (long)T[0] * (((y) + T[1]) % T[1] + (long)T[1] * (((z) + T[2]) % T[2]))] + 0.5))
 	/* interior bytes of the local padded nodes (ghosts excluded, as the
@@ -248,6 +265,13 @@ static PincObj *obj_create(const dictionary *ini, const pinc_geom_t *g) {
 	return o;
 }
 
+static PincObj *obj_create(const dictionary *ini, const pinc_geom_t *g) {
+	if (!iniHas(ini, "objects:sphere") && !iniHas(ini, "objects:file")) return NULL;
+	if (g->nd != 3) msg(ERROR, "objects are 3-D (object.c)");
+	const int T[3] = {g->T[0], g->T[1], g->T[2]};
+	return obj_from_mask(read_mask(ini, T), g, capacitance_green(ini));
+}
+
 PincObj *pinc_obj_create(const dictionary *ini, const Grid *rho) {
 	if (!iniHas(ini, "objects:sphere") && !iniHas(ini, "objects:file")) return NULL;
 	if (rho->rank != 4) msg(ERROR, "objects are 3-D (object.c)");
@@ -257,9 +281,10 @@ PincObj *pinc_obj_create(const dictionary *ini, const Grid *rho) {
 void pinc_obj_free(PincObj *o) {
 	if (!o) return;
 	if (o->pop) {
-		/* the population outlives the objects (main.c:283-290) */
+		/* a population that outlives the objects tests no object any more */
 		o->pop->objInside = NULL;
 		o->pop->objCount = NULL;
+		o->pop->objOwner = NULL;
 	}
 	pinc_hip_free(o->dPushCount);
 	pinc_hip_free(o->dInside);
@@ -268,6 +293,7 @@ void pinc_obj_free(PincObj *o) {
 	pinc_hip_free(o->dPhiS);
 	pinc_hip_free(o->dM);
 	pinc_hip_free(o->dCount);
+	free(o->h5path);
 	free(o->surfNode);
 	free(o->surfOff);
 	free(o->capOff);
@@ -279,6 +305,7 @@ void pinc_obj_free(PincObj *o) {
 }
 
 long pinc_obj_nsurface(const PincObj *o) { return o ? o->nSurf : 0; }
+void pinc_obj_forget_pop(PincObj *o) { o->pop = NULL; }
 double pinc_obj_collected(const PincObj *o) {
 	double t = 0;
 	for (int a = 0; o && a < o->nObj; a++) t += o->collected[a];
@@ -303,6 +330,7 @@ static void surface_phi(PincObj *o, const Grid *phi, long s0, long n, double *ds
  * reference's); rho and phi are restored afterwards */
 void pinc_obj_capacitance(PincObj *o, Grid *rho, Grid *phi, void *solver,
                           void (*solve)(void *, Grid *, Grid *, const MpiInfo *), const MpiInfo *mpi) {
+	if (!o->nObj) return; /* no objects: nothing to solve for */
 	long n = o->nSurf, N = rho->dev->n;
 	double *saveR = NULL, *saveP = NULL;
 	pinc_check(pinc_hip_malloc((void **)&saveR, N * sizeof(double)), "cap save");
@@ -422,7 +450,7 @@ void pinc_obj_capacitance(PincObj *o, Grid *rho, Grid *phi, void *solver,
  * with the emigrants' back-fill (k_push, pinc_pusher.c extract). */
 void pinc_obj_attach(PincObj *o, Population *pop) {
 	PincDevPop *dv = pop->dev;
-	if (!o || !dv->fused) return;
+	if (!o || !o->nObj || !dv->fused) return;
 	long n = (long)PINC_MAX_SPECIES * o->nObj;
 	pinc_check(pinc_hip_malloc((void **)&o->dPushCount, n * sizeof(int)), "object push counts");
 	pinc_check(pinc_hip_memset(o->dPushCount, 0, n * sizeof(int), g_pinc.stream), "object push counts");
@@ -432,6 +460,7 @@ void pinc_obj_attach(PincObj *o, Population *pop) {
 	dv->objNodes = o->nNodes;
 	dv->objK = o->nObj;
 	dv->objCount = o->dPushCount;
+	dv->objOwner = o;
 	for (int d = 0; d < 3; d++) {
 		dv->objLo[d] = o->bbLo[d];
 		dv->objHi[d] = o->bbHi[d];
@@ -447,6 +476,8 @@ void pinc_obj_attach(PincObj *o, Population *pop) {
  * only the particles imported since -- [depEnd, iStop) of each species --
  * go through the flag pass. */
 void pinc_obj_collect(PincObj *o, Population *pop, int discard) {
+	if (!o->nObj) return; /* an all-zero mask (main.c with no object) */
+	pinc_pop_flush_host(pop);
 	PincDevPop *dv = pop->dev;
 	int K = o->nObj;
 	double *cnt = calloc(K + 1, sizeof(double));
@@ -535,6 +566,7 @@ void pinc_obj_add_rho(PincObj *o, Grid *rho) {
 
 /* object.c:301-366; returns phi_c */
 double pinc_obj_apply(PincObj *o, Grid *rho, const Grid *phi) {
+	if (!o->nObj) return 0.0;
 	if (!o->haveCap) msg(ERROR, "objects: capacitance matrix not computed");
 	long n = o->nSurf;
 	/* phi at every object's surface first: the corrections do not change
@@ -561,17 +593,73 @@ double pinc_obj_apply(PincObj *o, Grid *rho, const Grid *phi) {
 /* ---------------------------------------------- the reference's API -- */
 /* object.h:8-21: Object is this build's PincObj (include/pinc.h) */
 
+/* object.c:671-699.  With objects:sphere / objects:file (extensions) the
+ * tables are built here; otherwise the object waits for oOpenH5 + oReadH5,
+ * the reference's order (main.c:95,126-127). */
 Object *oAlloc(const dictionary *ini) {
 	pinc_geom_t g = pinc_geom_current();
 	PincObj *o = obj_create(ini, &g);
-	if (!o) msg(ERROR, "oAlloc: set objects:sphere or objects:file");
+	if (o) return o;
+	o = calloc(1, sizeof(*o));
+	o->pending = 1;
+	o->geom = g;
+	o->green = capacitance_green(ini);
+	o->haveCap = 1; /* nothing to solve until a mask arrives */
 	return o;
 }
 
 void oFree(Object *obj) { pinc_obj_free(obj); }
 
+/* object.c:721-725 -> gOpenH5 -> openH5File (io.c:566-602): the file is
+ * <files:output><sep><fName>.grid.h5, sep "_" unless the prefix ends in "/"
+ * ("/" if it is "."); only its /Object dataset is read */
+void oOpenH5(const dictionary *ini, Object *obj, const MpiInfo *mpiInfo, const Units *units, double denorm,
+             const char *fName) {
+	(void)mpiInfo;
+	(void)units;
+	(void)denorm;
+	char *pre = iniGetStr(ini, "files:output");
+	size_t n = strlen(pre);
+	const char *sep = !strcmp(pre, ".") ? "/" : (n > 0 && pre[n - 1] != '/' ? "_" : "");
+	free(obj->h5path);
+	if (asprintf(&obj->h5path, "%s%s%s.grid.h5", pre, sep, fName) < 0) msg(ERROR, "oOpenH5: out of memory");
+	free(pre);
+}
+
+/* object.c:727-756: read /Object, then oFillLookupTables and
+ * oFindObjectSurfaceNodes.  An object built from the ini (extensions) keeps
+ * its tables.  No file at the oOpenH5 path: a run without objects (the
+ * reference would read an absent dataset). */
+void oReadH5(Object *obj, const MpiInfo *mpiInfo) {
+	(void)mpiInfo;
+	if (!obj->pending) return;
+	obj->pending = 0;
+	if (!obj->h5path) msg(ERROR, "oReadH5 before oOpenH5");
+	FILE *f = fopen(obj->h5path, "rb");
+	if (!f) {
+		msg(WARNING, "oReadH5: no %s, the run has no objects", obj->h5path);
+		return;
+	}
+	fclose(f);
+	const int *T = obj->geom.T;
+	long nTrue = (long)T[0] * T[1] * T[2];
+	double *mk = calloc(nTrue, sizeof(double));
+	long got = pinc_h5_read(obj->h5path, "/Object", 0, mk, nTrue);
+	if (got != nTrue)
+		msg(ERROR, "oReadH5: %s /Object must hold %ld values (grid %dx%dx%d), got %ld", obj->h5path, nTrue, T[0],
+		    T[1], T[2], got);
+	PincObj *t = obj_from_mask(mk, &obj->geom, obj->green);
+	t->h5path = obj->h5path;
+	*obj = *t; /* the caller holds obj */
+	free(t);
+	if (obj->nObj) msg(STATUS, "oReadH5: %d object(s), %ld surface nodes", obj->nObj, obj->nSurf);
+}
+
+void oCloseH5(Object *obj) { (void)obj; /* nothing stays open (the read opens and closes) */ }
+
 /* object.c:163-298: the reference allocates its own solver for the columns */
 void oComputeCapacitanceMatrix(Object *obj, const dictionary *ini, const MpiInfo *mpiInfo) {
+	if (!obj->nObj) return;
 	Grid *rho = gAlloc(ini, SCALAR), *phi = gAlloc(ini, SCALAR);
 	MultigridSolver *S = mgAllocSolver(ini, rho, phi);
 	pinc_obj_capacitance(obj, rho, phi, S, (void (*)(void *, Grid *, Grid *, const MpiInfo *))mgSolve, mpiInfo);
@@ -582,6 +670,7 @@ void oComputeCapacitanceMatrix(Object *obj, const dictionary *ini, const MpiInfo
 
 void oApplyCapacitanceMatrix(Grid *rho, const Grid *phi, const Object *obj, const MpiInfo *mpiInfo) {
 	(void)mpiInfo;
+	if (!obj->nObj) return;
 	pinc_obj_apply((PincObj *)obj, rho, phi);
 }
 

@@ -155,13 +155,62 @@ Population *pAlloc(const dictionary *ini) {
 	pinc_check(pinc_hip_h2d(dv->mq, mq, sizeof(mq), g_pinc.stream), "pAlloc mq");
 	dv->geom = pinc_geom_current();
 	p->dev = dv;
+	/* the bound the kernels check velocities against (pVelAssertMax) */
+	g_pinc.maxVel = iniHas(ini, "population:maxVel") ? iniGetDouble(ini, "population:maxVel") : INFINITY;
 	return p;
+}
+
+void pinc_pop_flush_host(const Population *pop) {
+	if (pop->dev->hostDirty) pSyncToDevice((Population *)pop);
+}
+
+/* population.c:342-365 and 316-340.  On the device the two checks run where
+ * the kernels touch the particles: the velocity bound in the kick of the
+ * fused push (or the move), the local frame after the move's periodic shift;
+ * both set bits of one assert word.  The calls main.c makes each step read
+ * that word (4 bytes) and end the run with msg(ERROR) as the reference does.
+ * A velocity the move has not yet seen is reported by the
+ * pPosAssertInLocalFrame of the same step, before anything deposits it.  A
+ * bound other than the kernels' (population:maxVel) is adopted from this call
+ * on, and the velocities present now are checked against it here. */
+static int assert_word(void) {
+	int err = 0;
+	pinc_check(pinc_hip_d2h(&err, g_pinc.dErr, sizeof(int), g_pinc.stream), "assert word");
+	return err;
+}
+
+void pVelAssertMax(const Population *pop, double max) {
+	PincDevPop *dv = pop->dev;
+	const int fresh = dv->hostDirty; /* velocities no kernel has checked yet */
+	pinc_pop_flush_host(pop);
+	if (max != g_pinc.maxVel || fresh) {
+		g_pinc.maxVel = max;
+		pinc_pop_t p = pinc_devpop(pop);
+		/* a pending sorted push keeps the kicked velocities in altV (same
+		 * ranges, slot order) */
+		if (dv->pending && dv->pendingSorted)
+			for (int d = 0; d < pop->nDims; d++) p.v[d] = dv->altV[d];
+		for (int s = 0; s < pop->nSpecies; s++)
+			pinc_check(pinc_hip_vel_assert(p, s, max, g_pinc.dErr, g_pinc.stream), "pVelAssertMax");
+	}
+	if (assert_word() & 1)
+		msg(ERROR, "Particle travels too fast (population:maxVel=%g exceeded, population.c:342-365)", max);
+}
+
+void pPosAssertInLocalFrame(const Population *pop, const Grid *grid) {
+	(void)grid; /* the bounds are MpiInfo's thresholds, from the same grid size */
+	int err = assert_word();
+	if (err & 2) msg(ERROR, "Particle is out of bounds after migration (population.c:316-340)");
+	if (err & 1) msg(ERROR, "Particle travels too fast (population:maxVel exceeded, population.c:342-365)");
+	(void)pop;
 }
 
 void pFree(Population *p) {
 	if (!p) return;
 	PincDevPop *dv = p->dev;
 	if (dv) {
+		/* main.c:297-298 frees the population before the objects */
+		if (dv->objOwner) pinc_obj_forget_pop(dv->objOwner);
 		for (int d = 0; d < p->nDims; d++) {
 			pinc_hip_free(dv->p.x[d]);
 			pinc_hip_free(dv->p.v[d]);
@@ -280,6 +329,7 @@ void pPosLattice(const dictionary *ini, Population *p, const MpiInfo *m) {
 	}
 	pToLocalFrame(p, m);
 	free(nPart);
+	p->dev->hostDirty = 1;
 }
 
 void pPosPerturb(const dictionary *ini, Population *p, const MpiInfo *m) {
@@ -299,6 +349,7 @@ void pPosPerturb(const dictionary *ini, Population *p, const MpiInfo *m) {
 	pToLocalFrame(p, m);
 	free(amp);
 	free(mode);
+	p->dev->hostDirty = 1;
 }
 
 void pVelZero(Population *p) {
@@ -307,6 +358,7 @@ void pVelZero(Population *p) {
 	for (int s = 0; s < p->nSpecies; s++)
 		for (long i = p->iStart[s]; i < p->iStop[s]; i++)
 			for (int d = 0; d < nd; d++) p->vel[i * nd + d] = 0;
+	p->dev->hostDirty = 1;
 }
 
 static unsigned long long mix64(unsigned long long z) {
@@ -336,6 +388,7 @@ void pVelMaxwell(const dictionary *ini, Population *p, unsigned long long seed) 
 		}
 	free(drift);
 	free(vth);
+	p->dev->hostDirty = 1;
 }
 
 void pSumKinEnergy(Population *p) {
@@ -345,6 +398,7 @@ void pSumKinEnergy(Population *p) {
 }
 
 void pSyncToHost(Population *p) {
+	if (p->dev->hostDirty && p->pos) return; /* the host mirror is the truth */
 	host_arrays(p);
 	int nd = p->nDims;
 	PincDevPop *dv = p->dev;
@@ -377,6 +431,7 @@ void pSyncToDevice(Population *p) {
 	if (!p->pos) msg(ERROR, "pSyncToDevice without host particles");
 	int nd = p->nDims;
 	PincDevPop *dv = p->dev;
+	dv->hostDirty = 0;
 	/* new particles: a pending fused move and its deposits no longer apply */
 	dv->pending = dv->pendingSorted = dv->depValid = dv->depExtracted = 0;
 	dv->everSorted = 0;
@@ -428,6 +483,7 @@ void pInitDevice(const dictionary *ini, Population *p, const MpiInfo *m, int per
 		p->iStop[s] = p->iStart[s] + n;
 	}
 	p->dev->flagsValid = 0;
+	p->dev->hostDirty = 0;
 	free(nPart);
 	free(amp);
 	free(mode);

@@ -115,6 +115,11 @@ funPtr puBoris3D1KE_set(dictionary *ini) {
 	g_boris.ready = 0;
 	return (funPtr)boris_sel_ke;
 }
+/* order 0 (nearest grid point, pusher.c:310-391, 640-668); puAccND0_set
+ * returns the KE variant, as the reference does (pusher.c:356-358) */
+funPtr puAccND0_set(dictionary *ini) { puSanity(ini, "puAccND0", 0, 0); return (funPtr)puAccND0KE; }
+funPtr puAccND0KE_set(dictionary *ini) { puSanity(ini, "puAccND0KE", 0, 0); return (funPtr)puAccND0KE; }
+funPtr puDistrND0_set(dictionary *ini) { puSanity(ini, "puDistrND0", 0, 0); return (funPtr)puDistrND0; }
 funPtr puDistr3D1_set(dictionary *ini) { puSanity(ini, "puDistr3D1", 3, 1); return (funPtr)puDistr3D1; }
 funPtr puDistrND1_set(dictionary *ini) { puSanity(ini, "puDistrND1", 0, 1); return (funPtr)puDistrND1; }
 funPtr puExtractEmigrants3D_set(dictionary *ini) {
@@ -499,6 +504,7 @@ static void swap_pos(PincDevPop *dv, int nd, int vel) {
 }
 
 static void classify(Population *pop, int doMove) {
+	pinc_pop_flush_host(pop);
 	if (!g_pinc.thrSet) msg(ERROR, "gCreateNeighborhood must run before puMove/extract");
 	PincDevPop *dv = pop->dev;
 	int nd = pop->nDims;
@@ -558,6 +564,7 @@ void puMove(Population *pop, Object *obj) {
 
 /* ------------------------------------------------------------- extract -- */
 static void extract(Population *pop, MpiInfo *m) {
+	pinc_pop_flush_host(pop);
 	PincDevPop *dv = pop->dev;
 	if (!dv->flagsValid) classify(pop, 0);
 	pinc_phase_begin(1);
@@ -721,6 +728,7 @@ static void puMigrateImport(Population *pop, MpiInfo *m) {
 
 void puMigrate(Population *pop, MpiInfo *m, Grid *grid) {
 	(void)grid;
+	pinc_pop_flush_host(pop);
 	pinc_phase_begin(2);
 	PincDevPop *dv = pop->dev;
 	int ns = pop->nSpecies;
@@ -743,8 +751,12 @@ void puMigrate(Population *pop, MpiInfo *m, Grid *grid) {
 /* gZero; per species gMul(1/q), scatter, gMul(q) (pusher.c:512-572): the
  * consecutive gMul(q_{s-1}), gMul(1/q_s) become one two-rounding pass. */
 static void distr(const Population *pop, Grid *rho) {
+	pinc_pop_flush_host(pop);
 	pinc_phase_begin(3);
 	PincDevGrid *g = rho->dev;
+	g->depPop = pop;
+	g->depOrder = 1;
+	g->folds = 0;
 	PincDevPop *dvp = pop->dev;
 	if (dvp->depValid && dvp->depExtracted && dvp->rhoN == g->n) {
 		/* fused push: the particles that stayed are in rhoS; add the ones
@@ -786,11 +798,62 @@ static void distr(const Population *pop, Grid *rho) {
 	pinc_phase_end(3);
 }
 
+/* gZero; per species gMul(1/q), one unit per particle at its nearest node,
+ * gMul(q) (puDistrND0, pusher.c:640-668).  A fused push's CIC deposit is not
+ * used. */
+void puDistrND0(const Population *pop, Grid *rho) {
+	pinc_pop_flush_host(pop);
+	pinc_phase_begin(3);
+	PincDevGrid *g = rho->dev;
+	g->depPop = pop;
+	g->depOrder = 0;
+	g->folds = 0;
+	pop->dev->depValid = pop->dev->depExtracted = 0;
+	pinc_check(pinc_hip_zero(g->d, g->n, g_pinc.stream), "distr zero");
+	pinc_pop_t p = pinc_devpop(pop);
+	for (int s = 0; s < pop->nSpecies; s++) {
+		if (s > 0)
+			pinc_check(pinc_hip_scale2(g->d, g->n, pop->charge[s - 1], 1.0 / pop->charge[s], g_pinc.stream),
+			           "distr scale");
+		pinc_check(pinc_hip_deposit_ngp(p, s, g->geom, g->d, g_pinc.stream), "deposit (NGP)");
+	}
+	pinc_check(pinc_hip_scale(g->d, g->n, pop->charge[pop->nSpecies - 1], g_pinc.stream), "distr scale");
+	g->ghostsValid = 0;
+	pinc_phase_end(3);
+}
+
+/* main.c:226 and :232 both call gHaloOp(addSlice, rho, FROMHALO) on one
+ * deposit; ghost values are not cleared in between, so a
+ * weight on a node with g ghost coordinates counts 2^g times.  Slab ghost
+ * planes are stored and folded again by the second call; the non-slab
+ * dimensions were wrapped at deposit.  Before that second fold, add the
+ * weight the plain deposit did not carry (geom.literal = 2,
+ * literal_node_factor in k_particles.hip), with the species chain of the
+ * deposit. */
+void pinc_literal_second_fold(const Population *pop, Grid *rho, int order) {
+	PincDevGrid *g = rho->dev;
+	pinc_geom_t geo = g->geom;
+	geo.literal = 2;
+	if (!g->lit) pinc_check(pinc_hip_malloc((void **)&g->lit, g->n * sizeof(double)), "second fold scratch");
+	pinc_check(pinc_hip_zero(g->lit, g->n, g_pinc.stream), "second fold");
+	pinc_pop_t p = pinc_devpop(pop);
+	for (int s = 0; s < pop->nSpecies; s++) {
+		if (s > 0)
+			pinc_check(pinc_hip_scale2(g->lit, g->n, pop->charge[s - 1], 1.0 / pop->charge[s], g_pinc.stream),
+			           "second fold scale");
+		if (order == 0) pinc_check(pinc_hip_deposit_ngp(p, s, geo, g->lit, g_pinc.stream), "second fold (NGP)");
+		else pinc_check(pinc_hip_deposit(p, s, geo, g->lit, g_pinc.stream), "second fold");
+	}
+	pinc_check(pinc_hip_scale(g->lit, g->n, pop->charge[pop->nSpecies - 1], g_pinc.stream), "second fold scale");
+	pinc_check(pinc_hip_add(g->d, g->lit, g->n, g_pinc.stream), "second fold add");
+}
+
 void puDistr3D1(const Population *pop, Grid *rho) { distr(pop, rho); }
 void puDistrND1(const Population *pop, Grid *rho) { distr(pop, rho); }
 
 /* ----------------------------------------------------------- accelerate -- */
 static void acc(Population *pop, Grid *E, int ke) {
+	pinc_pop_flush_host(pop);
 	pinc_phase_begin(6);
 	PincDevPop *dv = pop->dev;
 	if (dv->fused) {
@@ -837,6 +900,7 @@ static void acc(Population *pop, Grid *E, int ke) {
 
 /* per species: E as rescaled for s, half kick, rotation, half kick, KE */
 static void boris(Population *pop, Grid *E, const double *T, const double *S, int ke) {
+	pinc_pop_flush_host(pop);
 	pinc_phase_begin(6);
 	PincDevPop *dv = pop->dev;
 	if (dv->pending) msg(ERROR, "Boris push after a fused puAcc without its puMove");
@@ -868,6 +932,31 @@ static void boris(Population *pop, Grid *E, const double *T, const double *S, in
 
 void puBoris3D1(Population *pop, Grid *E, const double *T, const double *S) { boris(pop, E, T, S, 0); }
 void puBoris3D1KE(Population *pop, Grid *E, const double *T, const double *S) { boris(pop, E, T, S, 1); }
+
+/* puAccND0KE (pusher.c:310-353): per species E as rescaled for it, v += E at
+ * the nearest node, KE.  Not fused: the next puMove moves on its own. */
+void puAccND0KE(Population *pop, Grid *E) {
+	pinc_pop_flush_host(pop);
+	pinc_phase_begin(6);
+	PincDevPop *dv = pop->dev;
+	if (dv->pending) msg(ERROR, "puAccND0KE after a fused puAcc without its puMove");
+	pinc_pop_t p = pinc_devpop(pop);
+	int ns = pop->nSpecies;
+	PincDevGrid *eg = E->dev;
+	if (!eg->scaled) pinc_check(pinc_hip_malloc((void **)&eg->scaled, eg->n * sizeof(double)), "E scaled");
+	for (int s = 0; s < ns; s++) {
+		int nb = 0;
+		pinc_check(pinc_hip_field_chain(eg->d, eg->scaled, eg->n, dv->qm, dv->mq, 1.0, s, g_pinc.stream), "E chain");
+		pinc_check(pinc_hip_accelerate_ngp(p, s, eg->geom, eg->scaled, dv->kePartial, &nb, g_pinc.stream),
+		           "accelerate (NGP)");
+		if (nb > 0) pinc_check(pinc_hip_sum(dv->kePartial, nb, g_pinc.dScratch, PINC_SLOT(16 + s), g_pinc.stream), "ke");
+		else pinc_check(pinc_hip_memset(PINC_SLOT(16 + s), 0, sizeof(double), g_pinc.stream), "ke");
+	}
+	double sums[PINC_MAX_SPECIES];
+	pinc_check(pinc_hip_d2h(sums, PINC_SLOT(16), ns * sizeof(double), g_pinc.stream), "ke readback");
+	for (int s = 0; s < ns; s++) pop->kinEnergy[s] = sums[s] * (0.5 * pop->mass[s]);
+	pinc_phase_end(6);
+}
 
 void puAcc3D1(Population *pop, Grid *E) { acc(pop, E, 0); }
 void puAcc3D1KE(Population *pop, Grid *E) { acc(pop, E, 1); }

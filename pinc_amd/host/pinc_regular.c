@@ -21,6 +21,21 @@ funPtr regular_set(dictionary *ini) {
 	return (funPtr)regular;
 }
 
+/* main.c:32-35 also offers the reference's diagnostic run modes (multigrid
+ * convergence studies, multigrid.c:1731-1900; the spectral check,
+ * spectral.c:117-150).  They are outside the hot path;
+ * the selectors exist so that main.c links against this library unchanged */
+static void mode_unavailable(const char *name) {
+	msg(ERROR, "methods:mode=%s is a diagnostic run mode of the reference that this build does not provide "
+	           "(use methods:mode=regular)", name);
+}
+static void mgMode(dictionary *ini) { (void)ini; mode_unavailable("mgMode"); }
+static void mgModeErrorScaling(dictionary *ini) { (void)ini; mode_unavailable("mgModeErrorScaling"); }
+static void sMode(dictionary *ini) { (void)ini; mode_unavailable("sMode"); }
+funPtr mgMode_set(dictionary *ini) { (void)ini; return (funPtr)mgMode; }
+funPtr mgModeErrorScaling_set(dictionary *ini) { (void)ini; return (funPtr)mgModeErrorScaling; }
+funPtr sMode_set(dictionary *ini) { (void)ini; return (funPtr)sMode; }
+
 struct PincSim {
 	dictionary *ini;
 	Units *units;
@@ -54,20 +69,28 @@ static void check_errors(void) {
 static PincSim *sim_build(dictionary *ini, const PincSimOpts *opts) {
 	PincSim *S = calloc(1, sizeof(*S));
 	S->ini = ini;
-	if (opts) S->opts = *opts;
-	else {
-		S->opts.nranks = 1;
+	if (opts) {
+		/* the caller sets the world (PincSimOpts: rank, size, device, RCCL id) */
+		S->opts = *opts;
+		if (S->opts.nranks < 1) S->opts.nranks = 1;
+		pinc_boot_configured();
+		g_pinc.device = S->opts.device;
+		g_pinc.rank = S->opts.rank;
+		g_pinc.nranks = S->opts.nranks;
+		g_pinc.timing = S->opts.timing;
+		pinc_ctx_require();
+		if (S->opts.nranks > 1 && !g_pinc.comm && !pinc_comm_host_transport()) {
+			if (!S->opts.commId) msg(ERROR, "multi-rank run without a communicator id");
+			pinc_check(pinc_hip_comm_init(&g_pinc.comm, S->opts.commId, S->opts.nranks, S->opts.rank), "comm init");
+		}
+	} else {
+		/* regular() as main.c runs it: the world comes from the launcher
+		 * (mpirun, torchrun, srun or PINC_RANK/PINC_WORLD_SIZE), DESIGN.md 7 */
 		S->opts.perturb = 1;
-	}
-	if (S->opts.nranks < 1) S->opts.nranks = 1;
-	g_pinc.device = S->opts.device;
-	g_pinc.rank = S->opts.rank;
-	g_pinc.nranks = S->opts.nranks;
-	g_pinc.timing = S->opts.timing;
-	pinc_ctx_require();
-	if (S->opts.nranks > 1 && !g_pinc.comm && !pinc_comm_host_transport()) {
-		if (!S->opts.commId) msg(ERROR, "multi-rank run without a communicator id");
-		pinc_check(pinc_hip_comm_init(&g_pinc.comm, S->opts.commId, S->opts.nranks, S->opts.rank), "comm init");
+		pinc_boot_world();
+		S->opts.rank = g_pinc.rank;
+		S->opts.nranks = g_pinc.nranks;
+		S->opts.device = g_pinc.device;
 	}
 	/* method selection (main.c:55-79) */
 	S->acc = (void (*)(Population *, Grid *))select(ini, "methods:acc", puAcc3D1_set, puAcc3D1KE_set, puAccND1_set,
@@ -251,7 +274,10 @@ void regular(dictionary *ini) {
 	for (int n = 1; n <= nTimeSteps; n++) {
 		msg(STATUS, "Computing time-step %i", n);
 		sim_step(S);
-		msg(STATUS, "KE %.17g PE %.17g", S->pop->kinEnergy[S->pop->nSpecies], S->pop->potEnergy[S->pop->nSpecies]);
+		/* summed over the ranks, as pWriteEnergy's MPI_SUM rows (population.c:658-698) */
+		double ke, pe;
+		pinc_sim_energy(S, &ke, &pe, NULL);
+		msg(STATUS, "KE %.17g PE %.17g", ke, pe);
 		if (h5) output_write(S, (double)n);
 	}
 	S->ini = NULL; /* owned by the caller */

@@ -1,6 +1,7 @@
 """Compile the C callers under tests/c_driver/ (pinc_main.c: regular()
 through select(); pinc_objmain.c: main.c's object loop through the
-reference's object API) against the in-tree libpinc.so (test
+reference's object API; pinc_mainc.c: main.c's main() and regular() call for
+call) against the in-tree libpinc.so (test
 infrastructure; called by __graft_entry__.build() and the tests)."""
 from __future__ import annotations
 
@@ -28,3 +29,4 @@ def build(name: str = "pinc_main") -> Path:
 if __name__ == "__main__":
     print(build())
     print(build("pinc_objmain"))
+    print(build("pinc_mainc"))

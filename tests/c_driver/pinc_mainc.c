@@ -1,0 +1,165 @@
+/*
+ * pinc_mainc.c -- the reference's main() and regular() call for call
+ * (src/main.c:19-304), linked against libpinc.so (TEST DRIVER, VERDICT r03
+ * item 1).  Every library call of main.c is made in main.c's order with
+ * main.c's arguments:
+ *   - select() over the full lists of main.c:32-35 and 55-74 (run modes,
+ *     CIC and NGP accelerators and distributors);
+ *   - the objects through oAlloc, oOpenH5(..., "test"), oReadH5,
+ *     oComputeCapacitanceMatrix, oCollectObjectCharge, gAddTo and
+ *     oApplyCapacitanceMatrix (main.c:95,126-127,141,163-166,221-238);
+ *   - rho folded twice per step (main.c:226,232), the literal loop;
+ *   - pVelAssertMax / pPosAssertInLocalFrame each step (main.c:206,219);
+ *   - every output file of main.c:121-131,172-177,228-229,269-273 and the
+ *     Timer of main.c:192,208,257,276.
+ * Differences, each forced by the environment and stated here:
+ *   - no MPI_Init/MPI_Barrier/MPI_Finalize: the library takes the world
+ *     from the launcher (PINC_RANK / PINC_WORLD_SIZE, torchrun, mpirun or
+ *     srun variables, pinc_boot.c); a PINC build links MPI itself;
+ *   - no gsl_rng: main.c allocates the generators but never draws from them
+ *     (pPosUniform and pVelMaxwell are commented out, main.c:144,148);
+ *   - pPosPerturb is called (main.c:152 has it commented out, which leaves a
+ *     cold lattice that never moves): the harness of SURVEY.md Appendix A.
+ * Each rank also prints its own "KE <ke> PE <pe>" per step (msg STATUS|ALL),
+ * which the test sums over ranks; the history file holds the summed values.
+ *
+ *   pinc_mainc <file.ini> [section:key=value ...]
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <sys/select.h> /* before pinc.h, which defines the select() macro */
+#include "pinc.h"
+
+void regular(dictionary *ini);
+funPtr regular_set(dictionary *ini) {
+	(void)ini;
+	return (funPtr)regular;
+}
+
+int main(int argc, char *argv[]) {
+	dictionary *ini = iniOpen(argc, argv);
+	msg(STATUS, "PINC (MI355X drop-in test driver) started.");
+	void (*run)() = select(ini, "methods:mode", regular_set, mgMode_set, mgModeErrorScaling_set, sMode_set);
+	run(ini);
+	iniClose(ini);
+	msg(STATUS, "PINC completed successfully!");
+	return 0;
+}
+
+void regular(dictionary *ini) {
+	void (*acc)() = select(ini, "methods:acc", puAcc3D1_set, puAcc3D1KE_set, puAccND1_set, puAccND1KE_set, puAccND0_set,
+	                       puAccND0KE_set);
+	void (*distr)() = select(ini, "methods:distr", puDistr3D1_set, puDistrND1_set, puDistrND0_set);
+	void (*extractEmigrants)() = select(ini, "methods:migrate", puExtractEmigrants3D_set, puExtractEmigrantsND_set);
+	void (*solverInterface)() = select(ini, "methods:poisson", mgSolver_set, sSolver_set);
+	void (*solve)() = NULL;
+	void *(*solverAlloc)() = NULL;
+	void (*solverFree)() = NULL;
+	solverInterface(&solve, &solverAlloc, &solverFree);
+
+	Units *units = uAlloc(ini);
+	uNormalize(ini, units);
+	MpiInfo *mpiInfo = gAllocMpi(ini);
+	Population *pop = pAlloc(ini);
+	Grid *E = gAlloc(ini, VECTOR);
+	Grid *rho = gAlloc(ini, SCALAR);
+	Grid *rhoObj = gAlloc(ini, SCALAR);
+	Grid *phi = gAlloc(ini, SCALAR);
+	void *solver = solverAlloc(ini, rho, phi);
+	Object *obj = oAlloc(ini);
+	gCreateNeighborhood(ini, mpiInfo, rho);
+	gSetBndSlices(phi, mpiInfo);
+
+	double denorm = 1.;
+	pOpenH5(ini, pop, units, "pop");
+	gOpenH5(ini, rho, mpiInfo, units, denorm, "rho");
+	gOpenH5(ini, rhoObj, mpiInfo, units, denorm, "rhoObj");
+	gOpenH5(ini, phi, mpiInfo, units, denorm, "phi");
+	gOpenH5(ini, E, mpiInfo, units, denorm, "E");
+	oOpenH5(ini, obj, mpiInfo, units, denorm, "test");
+	oReadH5(obj, mpiInfo);
+	long long history = xyOpenH5(ini, "history");
+	pCreateEnergyDatasets(history, pop);
+
+	oComputeCapacitanceMatrix(obj, ini, mpiInfo);
+	pPosLattice(ini, pop, mpiInfo);
+	pVelZero(pop);
+	double maxVel = iniGetDouble(ini, "population:maxVel");
+	pPosPerturb(ini, pop, mpiInfo);
+	extractEmigrants(pop, mpiInfo);
+	puMigrate(pop, mpiInfo, rho);
+
+	gZero(rhoObj);
+	oCollectObjectCharge(pop, rhoObj, obj, mpiInfo);
+	gZero(rhoObj);
+
+	distr(pop, rho);
+	gHaloOp((funPtr)addSlice, rho, mpiInfo, FROMHALO);
+	gWriteH5(rho, mpiInfo, (double)0);
+	solve(solver, rho, phi, mpiInfo);
+	gWriteH5(phi, mpiInfo, (double)0);
+	gFinDiff1st(phi, E);
+	gHaloOp((funPtr)setSlice, E, mpiInfo, TOHALO);
+	gMul(E, -1.);
+	gMul(E, 0.5);
+	acc(pop, E);
+	gMul(E, 2.0);
+
+	Timer *t = tAlloc(mpiInfo->mpiRank);
+	int nTimeSteps = iniGetInt(ini, "time:nTimeSteps");
+	for (int n = 1; n <= nTimeSteps; n++) {
+		msg(STATUS, "Computing time-step %i", n);
+		msg(STATUS, "Nr. of particles %i: ", (int)(pop->iStop[0] - pop->iStart[0]));
+		pVelAssertMax(pop, maxVel);
+		tStart(t);
+		puMove(pop, obj);
+		extractEmigrants(pop, mpiInfo);
+		puMigrate(pop, mpiInfo, rho);
+		pPosAssertInLocalFrame(pop, rho);
+		oCollectObjectCharge(pop, rhoObj, obj, mpiInfo);
+		distr(pop, rho);
+		gHaloOp((funPtr)addSlice, rho, mpiInfo, FROMHALO);
+		gWriteH5(rho, mpiInfo, (double)n);
+		gWriteH5(rhoObj, mpiInfo, (double)n);
+		gAddTo(rho, rhoObj);
+		gHaloOp((funPtr)addSlice, rho, mpiInfo, FROMHALO);
+		solve(solver, rho, phi, mpiInfo);
+		oApplyCapacitanceMatrix(rho, phi, obj, mpiInfo);
+		solve(solver, rho, phi, mpiInfo);
+		gHaloOp((funPtr)setSlice, phi, mpiInfo, TOHALO);
+		gFinDiff1st(phi, E);
+		gHaloOp((funPtr)setSlice, E, mpiInfo, TOHALO);
+		gMul(E, -1.);
+		acc(pop, E);
+		tStop(t);
+		pSumKinEnergy(pop);
+		gPotEnergy(rho, phi, pop);
+		gWriteH5(E, mpiInfo, (double)n);
+		gWriteH5(rho, mpiInfo, (double)n);
+		gWriteH5(phi, mpiInfo, (double)n);
+		pWriteH5(pop, mpiInfo, (double)n, (double)n + 0.5);
+		pWriteEnergy(history, pop, (double)n);
+		long np = 0;
+		for (int s = 0; s < pop->nSpecies; s++) np += pop->iStop[s] - pop->iStart[s];
+		msg(STATUS | ALL, "rank %d KE %.17g PE %.17g N %ld", mpiInfo->mpiRank, pop->kinEnergy[pop->nSpecies],
+		    pop->potEnergy[pop->nSpecies], np);
+	}
+	if (mpiInfo->mpiRank == 0) tMsg(t->total, "Time spent: ");
+
+	gFreeMpi(mpiInfo);
+	pCloseH5(pop);
+	gCloseH5(rho);
+	gCloseH5(rhoObj);
+	gCloseH5(phi);
+	gCloseH5(E);
+	oCloseH5(obj);
+	xyCloseH5(history);
+	gFree(rho);
+	gFree(rhoObj);
+	gFree(phi);
+	gFree(E);
+	pFree(pop);
+	oFree(obj);
+	tFree(t);
+	(void)solverFree;
+}
