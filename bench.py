@@ -180,6 +180,39 @@ def _cpu_baseline(size: int, ppc: int, steps: int, native: bool, workload: str =
             "phase_ms_per_step": ph}
 
 
+def _multi_rank_summary(info: list, steps: int, dom: str, transport: str) -> dict:
+    """What an N-GPU line needs to say where the time went: every phase's
+    maximum (and minimum) over the ranks, each collective kind's device time,
+    payload bytes and calls per step (pinc_comm.c statistics; the maximum
+    over the ranks), and each rank's roofline of the dominant kernel
+    (algorithmic bytes per launch over its mean launch time)."""
+    phases = sorted(info[0]["phase_ms"])
+    out = {"transport": transport, "ranks": len(info),
+           "phase_ms_per_step_max": {k: max(i["phase_ms"][k] for i in info) / steps for k in phases},
+           "phase_ms_per_step_min": {k: min(i["phase_ms"][k] for i in info) / steps for k in phases}}
+    comm = {}
+    for kind in info[0]["comm"]:
+        per = [i["comm"][kind] for i in info]
+        # calls beyond the event pool are counted but not timed: scale
+        ms = [c["ms"] * (c["calls"] / c["timed_calls"]) if c["timed_calls"] else 0.0 for c in per]
+        comm[kind] = {"ms_per_step_max": max(ms) / steps, "ms_per_step_mean": sum(ms) / len(ms) / steps,
+                      "bytes_per_step_per_rank_max": max(c["bytes"] for c in per) / steps,
+                      "calls_per_step": max(c["calls"] for c in per) / steps}
+    out["comm_per_step"] = comm
+    out["comm_ms_per_step_max_total"] = sum(v["ms_per_step_max"] for v in comm.values())
+    per_rank = []
+    for i in info:
+        p = i["probes"].get(dom)
+        r = {"rank": i["rank"], "particles": i["particles"], "wall_s": i["wall_s"]}
+        if p and p["mean_ms"] > 0:
+            gbs = p["mean_bytes"] / (p["mean_ms"] * 1e-3) / 1e9
+            r["roofline"] = {"kernel": dom, "bytes_per_launch": p["mean_bytes"], "mean_launch_ms": p["mean_ms"],
+                             "achieved_GBs": gbs, "frac": gbs / HBM_PEAK_GBS, "launches": p["launches"]}
+        per_rank.append(r)
+    out["per_rank"] = per_rank
+    return out
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -338,6 +371,8 @@ def main() -> int:
     sim.timers_reset()
     c0 = sim.cycles
     _lib.probe_start("all", 4096)
+    if world > 1:
+        _lib.comm_stats_start(1 << 15)
 
     barrier()
     torch.cuda.synchronize()
@@ -367,6 +402,13 @@ def main() -> int:
 
     dt_max = dt
     n_total = n_local
+    comm = _lib.comm_stats_read() if world > 1 else {}
+    rank_info = {"rank": rank, "wall_s": dt, "particles": n_local, "phase_ms": phases, "comm": comm,
+                 "probes": {k: p for k, p in probes.items() if p["samples"] > 0}}
+    all_info = [rank_info]
+    if dist is not None:
+        all_info = [None] * world
+        dist.all_gather_object(all_info, rank_info)
     if dist is not None:
         t = torch.tensor([dt], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -497,6 +539,9 @@ def main() -> int:
         "push_kinds": sub,
         "cpu_baseline": None,
     }
+    if world > 1:
+        result["multi_rank"] = _multi_rank_summary(all_info, K, dom, "host (gloo rehearsal, one GPU)"
+                                                   if args.host_transport else "rccl")
     result["config"]["traffic_key"] = traffic_key
     result["config"]["runtime_stack"] = _lib.runtime_stack()
     tr = _pmc_traffic(dk["rocprof_name"].rstrip("*").rstrip(" ,").split("*")[0], traffic_key)

@@ -402,6 +402,18 @@ long pinc_sim_total_particles(PincSim *sim);
  * these callbacks (0 = success).  exchange: op i sends sendBytes[i] to
  * sendPeer[i] and receives recvBytes[i] from recvPeer[i]; the peer's send
  * op i pairs with this rank's receive op i.  NULL restores RCCL. */
+/* Statistics of the collectives by kind (0 halo: gHaloOp's plane exchanges,
+ * 1 ext_halo: the sharded multigrid's deep halo, 2 migrate: migrant counts
+ * and records, 3 allgather, 4 allreduce, 5 spectral_transpose: the slab
+ * solve's all-to-all): start (up to maxCalls calls timed with HIP events on
+ * the library's stream), then read device ms, this rank's payload bytes,
+ * calls and timed calls per kind.  Returns PINC_COMM_KINDS, -1 if never
+ * started. */
+#define PINC_COMM_KINDS 6
+int pinc_comm_stats_start(int maxCalls);
+int pinc_comm_stats_read(double *ms, double *bytes, long *calls, long *timedCalls);
+const char *pinc_comm_kind_name(int kind);
+
 typedef struct {
 	int (*exchange)(void *user, int nOps, const int *sendPeer, const void *const *sendbuf, const long *sendBytes,
 	                const int *recvPeer, void *const *recvbuf, const long *recvBytes);

@@ -463,6 +463,10 @@ int pinc_hip_comm_exchange(void *comm, int nOps, const int *sendPeer, void *cons
                            const long *recvBytes, void *stream);
 int pinc_hip_comm_allgather(void *comm, const double *send, double *recv, long count, void *stream);
 int pinc_hip_comm_allreduce_sum(void *comm, const double *send, double *recv, long count, void *stream);
+/* test hook: occupy the stream for `seconds` (at most 30) of wall time with a
+ * one-lane kernel that ends by itself (tests/test_gpu_rccl_watchdog.py holds
+ * an RCCL call behind it) */
+int pinc_hip_test_spin(double seconds, void *stream);
 
 #ifdef __cplusplus
 }

@@ -122,6 +122,9 @@ _sigs = {
     "pinc_sim_total_particles": (C.c_long, [C.c_void_p]),
     "pinc_probe_start": (C.c_int, [C.c_int, C.c_int]),
     "pinc_set_host_transport": (C.c_int, [C.c_void_p]),
+    "pinc_comm_stats_start": (C.c_int, [C.c_int]),
+    "pinc_comm_stats_read": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "pinc_comm_kind_name": (C.c_char_p, [C.c_int]),
     "pinc_probe_read": (C.c_int, [C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_int),
                                   C.POINTER(C.c_long)]),
 }
@@ -136,6 +139,26 @@ def probe_start(kernel: str = "all", max_samples: int = 4096) -> None:
     k = -1 if kernel == "all" else PROBES[kernel]
     if HOST.pinc_probe_start(k, max_samples):
         raise ValueError(f"bad probe {kernel!r}")
+
+
+COMM_KINDS = 6
+
+
+def comm_stats_start(max_calls: int = 16384) -> None:
+    """Time and count the library's collectives by kind (pinc_comm.c)."""
+    HOST.pinc_comm_stats_start(max_calls)
+
+
+def comm_stats_read() -> dict:
+    """Per collective kind: device ms (over the timed calls), this rank's
+    payload bytes, calls, timed calls; {} if statistics were never started."""
+    import numpy as _np
+    ms, by = _np.zeros(COMM_KINDS), _np.zeros(COMM_KINDS)
+    calls, timed = _np.zeros(COMM_KINDS, dtype=_np.int64), _np.zeros(COMM_KINDS, dtype=_np.int64)
+    if HOST.pinc_comm_stats_read(ms.ctypes.data, by.ctypes.data, calls.ctypes.data, timed.ctypes.data) < 0:
+        return {}
+    return {HOST.pinc_comm_kind_name(k).decode(): {"ms": float(ms[k]), "bytes": float(by[k]), "calls": int(calls[k]),
+                                                   "timed_calls": int(timed[k])} for k in range(COMM_KINDS)}
 
 
 def probe_read(kernel: str) -> dict:

@@ -9,6 +9,7 @@ CPU checker under oracle/ (test infrastructure, not part of this package).
 from __future__ import annotations
 
 import concurrent.futures as cf
+import json
 import os
 import subprocess
 import sys
@@ -27,12 +28,32 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("PINC_ARCH", "gfx950")
 # -ffp-contract=off: the kernels reproduce the reference's fp64 association
 # order; a fused multiply-add would change the rounding.
-# (a variant library records its defines in build_flags.txt, so that a
-# rebuild without PINC_HIP_DEFINES in the environment keeps them)
+# build_flags.txt records what a library was built with (arch, compiler,
+# defines); a change of any of them rebuilds.  A variant library (PINC_LIBDIR)
+# keeps its defines when rebuilt without PINC_HIP_DEFINES in the environment;
+# the default library never inherits defines: it is built with exactly what
+# the environment says (none, normally), so bench and tests cannot silently
+# run a variant kernel.
 STAMP = LIB / "build_flags.txt"
+VARIANT = LIB != (ROOT / "pinc_amd" / "lib").resolve()
+
+
+def _read_stamp() -> dict:
+    try:
+        return json.loads(STAMP.read_text())
+    except (OSError, ValueError):
+        return {}
+
+
 DEFINES = os.environ.get("PINC_HIP_DEFINES")
 if DEFINES is None:
-    DEFINES = STAMP.read_text().strip() if STAMP.exists() else ""
+    DEFINES = _read_stamp().get("defines", "") if VARIANT else ""
+DEFINES = DEFINES.strip()
+
+
+def stamp() -> dict:
+    """What the libraries in LIB are (to be) built with."""
+    return {"arch": ARCH, "hipcc": HIPCC, "defines": DEFINES}
 HIP_FLAGS = ["-std=c++17", "-O3", f"--offload-arch={ARCH}", "-ffp-contract=off", "-fPIC",
              "-munsafe-fp-atomics", f"-I{INC}", f"-I{CSRC}", *DEFINES.split()]
 C_FLAGS = ["-std=c11", "-O2", "-fPIC", "-Wall", "-ffp-contract=off", f"-I{INC}", f"-I{HOST}"]
@@ -56,12 +77,11 @@ def _newer(src: Path, dst: Path, deps: list[Path]) -> bool:
 
 def _up_to_date(libs: list[Path], inputs: list[Path]) -> bool:
     """The libraries exist, are newer than every source and header, and were
-    built with these defines.  (The object directory is not consulted: it
+    built with this arch, compiler and defines.  (The object directory is not consulted: it
     does not travel to the GPU box, where the libraries are used as built.)"""
     if not all(p.exists() for p in libs):
         return False
-    stamp = STAMP.read_text().strip() if STAMP.exists() else ""
-    if stamp != DEFINES.strip():
+    if _read_stamp() != stamp():
         return False
     t = min(p.stat().st_mtime for p in libs)
     return all(p.stat().st_mtime <= t for p in inputs)
@@ -80,7 +100,7 @@ def build(verbose: bool = False, jobs: int = 8) -> dict:
         return out
     LIB.mkdir(parents=True, exist_ok=True)
     OBJ.mkdir(parents=True, exist_ok=True)
-    flags_changed = (STAMP.read_text().strip() if STAMP.exists() else "") != DEFINES.strip()
+    flags_changed = _read_stamp() != stamp()
     jobs_list = []
     for f in HIP_SRC:
         src, obj = CSRC / f, OBJ / (f + ".o")
@@ -98,7 +118,7 @@ def build(verbose: bool = False, jobs: int = 8) -> dict:
           "-L/opt/rocm/lib", "-lrccl", "-lrocfft", "-Wl,-rpath,/opt/rocm/lib"])
     _run(["gcc", "-shared", "-o", str(libhost), *c_objs, f"-L{LIB}", "-lpinc_hip", "-lm", "-ldl",
           "-Wl,-rpath,$ORIGIN"])
-    STAMP.write_text(DEFINES.strip() + "\n")
+    STAMP.write_text(json.dumps(stamp()) + "\n")
     if verbose:
         print(out)
     return out

@@ -375,3 +375,23 @@ extern "C" int pinc_hip_comm_allreduce_sum(void *comm, const double *send, doubl
 	if (r != ncclSuccess) return nccl_error(r, "allreduce");
 	return watch_mark((hipStream_t)stream, "allreduce");
 }
+
+// ------------------------------------------------------------ test hook ---
+// A kernel that occupies the stream for `seconds` of wall time (one lane
+// polling s_memrealtime, 100 MHz, with s_sleep between polls), so that a test
+// can hold an RCCL call behind it and watch the watchdog fire (or not).  The
+// bound is the kernel's own: every launch ends by itself.
+namespace {
+__global__ void k_test_spin(unsigned long long ticks) {
+	if (threadIdx.x != 0) return;
+	const unsigned long long t0 = wall_clock64();
+	while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+}
+}  // namespace
+
+extern "C" int pinc_hip_test_spin(double seconds, void *stream) {
+	if (!(seconds >= 0.0) || seconds > 30.0) return set_error(hipErrorInvalidValue, "test spin: 0..30 s");
+	hipLaunchKernelGGL(k_test_spin, dim3(1), dim3(64), 0, (hipStream_t)stream,
+	                   (unsigned long long)(seconds * 1e8));
+	return check_launch("test spin");
+}

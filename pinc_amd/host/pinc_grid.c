@@ -409,7 +409,11 @@ static long slab_node(const PincDevGrid *dv, const int *c) {
 
 void gSyncToHost(Grid *grid) {
 	PincDevGrid *dv = grid->dev;
-	if (dv->global) gHaloOp((funPtr)setSlice, grid, NULL, TOHALO);
+	/* the potential's truth is the solver's global view: bring the slab (and
+	 * its ghost planes) up to date first.  rho's slab is its own truth, ghost
+	 * planes included: a gWriteH5 between main.c's two folds (main.c:226-232)
+	 * must not replace the ghost deposits with periodic images */
+	if (dv->global && dv->globalIsTruth) gHaloOp((funPtr)setSlice, grid, NULL, TOHALO);
 	int rank = grid->rank;
 	long total = grid->sizeProd[rank];
 	if (!grid->val) grid->val = calloc(total, sizeof(double));

@@ -205,6 +205,16 @@ static void make_groups(hid_t h5, const char *name) {
 }
 
 static void write_dataset(hid_t h5, const char *name, int rank, const hsize_t *dims, const double *data) {
+	/* main.c writes rho twice per step under one name (main.c:228 and 270):
+	 * the reference's second H5Dcreate fails and the file keeps the first
+	 * write; so here, without the error stack */
+	if (H.Lexists(h5, name, H5P_DEFAULT) > 0) {
+		static int warned = 0;
+		if (!warned++)
+			msg(WARNING, "HDF5 output: dataset %s exists (main.c:228,270 write rho twice per step); the first "
+			             "write is kept, as the reference's H5Dcreate leaves it", name);
+		return;
+	}
 	hid_t sp = H.Screate_simple(rank, dims, NULL);
 	hid_t d = H.Dcreate2(h5, name, *H.f64le, sp, H5P_DEFAULT, H5P_DEFAULT, H5P_DEFAULT);
 	if (d < 0) msg(ERROR, "HDF5 output: cannot create dataset %s (exists already?)", name);

@@ -141,6 +141,8 @@ struct PincDevGrid {
 	pinc_geom_t geom;
 	double *global;     /* global periodic view (rho, phi) */
 	int ownsGlobal;
+	int globalIsTruth;  /* the solver writes global (phi): the slab follows by TOHALO; for rho
+	                       the slab is the truth and global its gathered copy */
 	int ghostsValid;    /* slab ghost planes already hold periodic images */
 	double *recv[2];    /* halo receive planes (multi-rank) */
 	double *scaled;     /* E as rescaled for the species being pushed (lazy) */

@@ -184,11 +184,13 @@ MultigridSolver *mgAllocSolver(const dictionary *ini, Grid *rho, Grid *phi) {
 	} else if (g_pinc.nranks == 1) {
 		rho->dev->global = rho->dev->d + ps;
 		phi->dev->global = phi->dev->d + ps;
+		phi->dev->globalIsTruth = 1;
 	} else {
 		pinc_check(pinc_hip_malloc((void **)&rho->dev->global, S->N[0] * sizeof(double)), "global rho");
 		pinc_check(pinc_hip_malloc((void **)&phi->dev->global, S->N[0] * sizeof(double)), "global phi");
 		pinc_check(pinc_hip_memset(phi->dev->global, 0, S->N[0] * sizeof(double), g_pinc.stream), "global phi");
 		rho->dev->ownsGlobal = phi->dev->ownsGlobal = 1;
+		phi->dev->globalIsTruth = 1;
 	}
 	if (!S->shard) {
 		S->rho[0] = rho->dev->global;

@@ -427,10 +427,13 @@ static int push_all(Population *pop, Grid *E, double *const *xout) {
 		int nb = 0;
 		unsigned long long *ts = NULL;
 		if (g_pinc.traceSort > 1) {
-			pinc_check(pinc_hip_malloc((void **)&ts, ((np / 1024 + 1) * 8 + 4) * sizeof(*ts)), "push timestamps");
-			pinc_check(pinc_hip_memset(ts + (np / 1024 + 1) * 8, 0, 4 * sizeof(*ts), g_pinc.stream), "push diagnostics");
+			/* 8 timestamps per push block (pinc_hip_push_chunk particles), then
+			 * the diagnostic counters */
+			const long nbk = np / pinc_hip_push_chunk() + 1;
+			pinc_check(pinc_hip_malloc((void **)&ts, (nbk * 8 + 4) * sizeof(*ts)), "push timestamps");
+			pinc_check(pinc_hip_memset(ts + nbk * 8, 0, 4 * sizeof(*ts), g_pinc.stream), "push diagnostics");
 			a.tstamp = ts;
-			a.diag = ts + (np / 1024 + 1) * 8;
+			a.diag = ts + nbk * 8;
 		}
 		const int kind = sortS[s] ? PINC_PROBE_PUSH_SORT : countNext ? PINC_PROBE_PUSH_COUNT : PINC_PROBE_PUSH_PLAIN;
 		int slot = E ? pinc_probe_begin(PINC_PROBE_PUSH) : -1;
@@ -469,8 +472,9 @@ static int push_all(Population *pop, Grid *E, double *const *xout) {
 		for (int s = 0; s < pop->nSpecies; s++) {
 			long np = pop->iStop[s] - pop->iStart[s];
 			double rate = np > 0 ? (double)mv[s] / (double)np : 0.0;
-			/* mean input cell box of this push's blocks (1024 items each) */
-			const double blocks = (double)((np + 1023) / 1024);
+			/* mean input cell box of this push's blocks */
+			const long chunk = pinc_hip_push_chunk();
+			const double blocks = (double)((np + chunk - 1) / chunk);
 			dv->spreadLast[s] = blocks > 0 ? (double)sp[s] / blocks : 0.0;
 			if (sortS[s]) dv->spreadBase[s] = 0;
 			if (dv->sinceSort[s] == 1 && !sortS[s]) dv->spreadBase[s] = dv->spreadLast[s];

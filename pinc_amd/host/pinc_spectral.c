@@ -72,11 +72,13 @@ SpectralSolver *sAlloc(const dictionary *ini, Grid *rho, Grid *phi) {
 	if (g_pinc.nranks == 1) {
 		rho->dev->global = rho->dev->d + ps;
 		phi->dev->global = phi->dev->d + ps;
+		phi->dev->globalIsTruth = 1;
 	} else if (!rho->dev->global) {
 		pinc_check(pinc_hip_malloc((void **)&rho->dev->global, S->N * sizeof(double)), "global rho");
 		pinc_check(pinc_hip_malloc((void **)&phi->dev->global, S->N * sizeof(double)), "global phi");
 		pinc_check(pinc_hip_memset(phi->dev->global, 0, S->N * sizeof(double), g_pinc.stream), "global phi");
 		rho->dev->ownsGlobal = phi->dev->ownsGlobal = 1;
+		phi->dev->globalIsTruth = 1;
 	}
 	return S;
 }

@@ -64,3 +64,26 @@ def test_rehearsal_collectives_pair_under_rccl_rules(built, tmp_path, world, wor
     if workload == "c3":
         # the slab-distributed solve's all-to-all transposes, not an all-gather of rho
         assert ("X", "spectral transpose") in stats and not any(k == "G" for k, _ in stats), stats
+    # the N>1 bench line says where the time went:
+    # per-phase max/min over the ranks, every collective kind's time, bytes
+    # and calls per step, and each rank's roofline of the dominant kernel
+    mr = line["multi_rank"]
+    assert mr["ranks"] == world and mr["transport"].startswith("host")
+    for k in ("move", "extract", "migrate", "deposit", "solve", "efield", "accelerate", "energy"):
+        assert k in mr["phase_ms_per_step_max"] and k in mr["phase_ms_per_step_min"]
+        assert mr["phase_ms_per_step_max"][k] >= mr["phase_ms_per_step_min"][k]
+    comm = mr["comm_per_step"]
+    assert set(comm) == {"halo", "ext_halo", "migrate", "allgather", "allreduce", "spectral_transpose"}
+    for v in comm.values():
+        assert set(v) == {"ms_per_step_max", "ms_per_step_mean", "bytes_per_step_per_rank_max", "calls_per_step"}
+    assert comm["migrate"]["calls_per_step"] >= 2 and comm["migrate"]["bytes_per_step_per_rank_max"] > 0
+    assert comm["halo"]["calls_per_step"] >= 1 and comm["allreduce"]["calls_per_step"] > 0
+    if workload == "c4":
+        assert comm["ext_halo"]["calls_per_step"] > 0 and comm["ext_halo"]["ms_per_step_max"] > 0
+    if workload == "c3":
+        assert comm["spectral_transpose"]["calls_per_step"] > 0
+    assert mr["comm_ms_per_step_max_total"] > 0
+    assert len(mr["per_rank"]) == world
+    for r in mr["per_rank"]:
+        assert r["particles"] > 0 and r["roofline"]["achieved_GBs"] > 0 and r["roofline"]["kernel"] == \
+            line["roofline"]["kernel"]

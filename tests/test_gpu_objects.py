@@ -12,6 +12,8 @@ runs that agree to solver tolerance, so fields and energies are compared
 to 1e-7 relative.  Parity is against the corrected algorithm (the
 reference's object.c does not compile; parity unpinned against it).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -384,3 +386,47 @@ def test_object_extrapolated_guesses_match_checker(built, fused, second):
         phi_g = s.grid(1)[1:-1, 1:-1, 1:-1]
         phi_o = w.grid(1)[1:-1, 1:-1, 1:-1]
         assert np.max(np.abs(phi_g - phi_o)) <= 1e-7 * np.abs(phi_o).max()
+
+
+def test_c5_bench_flags_match_checker(built):
+    """Config C5 with the bench's exact flags (configs.bench_config("c5"):
+    the sphere at the grid centre with radius S/32, fused collection in the
+    push, tiled layout with the adaptive in-push sort, native multigrid with
+    the extrapolated guesses, the exact level-1 solve and the spectral second
+    guess, the capacitance matrix by one solve per surface node -- the
+    reference's) at 64^3 x 16 ppc, 8 steps of main.c:197-274 against the
+    checker's object loop (oracle/orc_obj.c with orc_native.c's guesses) on
+    the same Maxwellian initial state: particle counts
+    exact, KE/PE to 1e-7 (the tolerances above)."""
+    from pinc_amd import Sim
+    S, ppc, steps, seed = 64, 16, 8, 20260101
+    cfg = configs.bench_config("c5", size=S, ppc=ppc)
+    o = cfg["objects"]
+    assert o["capacitance"] == "solve" and o["secondGuess"] == "spectral" and cfg["population"]["fused"] == "1"
+    assert cfg["multigrid"]["extrapolate"] == "1" and cfg["multigrid"]["spectralCoarse"] == "1"
+    sphere = [float(v) for v in o["sphere"].split(",")]
+    ini = configs.write_ini(cfg)
+    try:
+        w = orc.World(ini)
+        w.init(perturb=False, maxwell=True, seed=seed)
+        ob = orc.Objects(w, _sphere((S, S, S), sphere[:3], sphere[3]))
+        ob.capacitance()
+        ob.init_collect()
+        w.init_fields()
+        with Sim(ini, maxwell=True, perturb=False, device_init=True, seed=seed) as s:
+            s.init()
+            for k in range(steps):
+                ob.step()
+                s.step()
+                ke_o, pe_o = w.energy()
+                ke, pe, _ = s.energy()
+                print(f"step {k}: N {s.count(0)}+{s.count(1)} KE {ke:.13g}/{ke_o:.13g} PE {pe:.13g}/{pe_o:.13g}")
+                for sp in range(2):
+                    assert s.count(sp) == w.count(sp), (k, sp, s.count(sp), w.count(sp))
+                assert abs(ke - ke_o) <= 1e-7 * abs(ke_o), (k, ke, ke_o)
+                assert abs(pe - pe_o) <= 1e-7 * abs(pe_o), (k, pe, pe_o)
+            collected = s.obj_collected
+        assert collected != 0.0 and ob.collected(0) != 0.0
+        w.close()
+    finally:
+        os.unlink(ini)

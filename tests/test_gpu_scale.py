@@ -89,15 +89,21 @@ def test_c4_per_gpu_load_matches_oracle(built):
     assert sum(g for g, _ in cyc) <= 3 * steps + 2   # the extrapolated guess: ~3 cycles per solve
 
 
-def test_c4ts_matches_oracle(built):
+_C4TS_SORTS = {}
+
+
+@pytest.mark.parametrize("spread", [0.0, 1.5])
+def test_c4ts_matches_oracle(built, spread):
     """C4's two-stream variant (bench --workload c4ts) at 32^3: two electron
     beams drifting +-0.1 cells/step per component and ions, all on the same
     lattice sites; the bench's flags; counts per species exact, energies to
     1e-8 for 12 steps (the beams cross cells every ~8 steps per component,
-    so the sort schedule runs)."""
+    so the sort schedule runs).  With population:sortSpread = 1.5 (ADVICE
+    r03) the gate holds back sorts the displaced fraction calls for: fewer
+    sorting pushes than the ungated run, with the same parity."""
     import orc
-    from pinc_amd import Sim
-    cfg = configs.bench_config("c4ts", size=32, ppc=8)
+    from pinc_amd import Sim, _lib
+    cfg = configs.bench_config("c4ts", size=32, ppc=8, sort_spread=spread)
     ini = configs.write_ini(cfg)
     try:
         w = orc.World(ini)
@@ -106,13 +112,19 @@ def test_c4ts_matches_oracle(built):
         with Sim(ini, maxwell=True, perturb=False, device_init=True, seed=SEED) as s:
             s.init()
             assert s.nspecies == 3
+            _lib.probe_start("all", 64)
             _energy_series_match(s, w, 12, 3)
+            sorts = _probe_launches("push_sort")
             v0 = s.particles(0)[1].mean(axis=0)
             v1 = s.particles(1)[1].mean(axis=0)
         w.close()
     finally:
         os.unlink(ini)
     assert np.all(np.abs(v0 - 0.1) < 0.01) and np.all(np.abs(v1 + 0.1) < 0.01), (v0, v1)
+    _C4TS_SORTS[spread] = sorts
+    assert sorts >= 1
+    if 0.0 in _C4TS_SORTS and 1.5 in _C4TS_SORTS:
+        assert _C4TS_SORTS[1.5] < _C4TS_SORTS[0.0], _C4TS_SORTS
 
 
 def _full_size_run(workload: str, steps: int, extra=None):
