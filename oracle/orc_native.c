@@ -15,7 +15,8 @@
  *   stop at RMS residual <= 1e-10              multigrid.c:1688-1724
  * -- and changes the cycle: the restricted residual is scaled by 4 (the
  * coarse h^2), every coarse visit starts from zero (correction scheme), no
- * neutralisation after each colour (once per level visit instead), and the
+ * neutralisation after each colour (once per level visit instead; level 0's
+ * rho once per solve; none between prolongation and post-smoothing), and the
  * hierarchy continues down to 2 points per dimension.
  *
  * The solve runs on the global periodic grid (no ghosts, x fastest),
@@ -261,12 +262,14 @@ static void vrec(ONative *S, OWorld *w, int q){
 		prolong_add(S, q-1);
 		return;
 	}
-	neutralize(S->rho[q], S->L[q].N);
+	/* level 0's rho is neutralised once per solve (ow_native_solve); no
+	 * neutralisation between the prolongation and the post-smoothing
+	 * (pinc_mg.c vrec, k_mg_coarse) */
+	if(q > 0) neutralize(S->rho[q], S->L[q].N);
 	smooth(S, q, w->nPre, pre);
 	residual(S, q);
 	restrict4(S, q);
 	vrec(S, w, q+1);
-	neutralize(S->phi[q], S->L[q].N);
 	smooth(S, q, w->nPost, post);
 	neutralize(S->phi[q], S->L[q].N);
 	if(q > 0) prolong_add(S, q-1);
@@ -327,6 +330,7 @@ void ow_native_solve(OWorld *w){
 	double barRes = 2.;
 	long c = 0;
 	w->mgHistN = 0;
+	if(S->nLevels > 1) neutralize(S->rho[0], N);
 	while(barRes > 1.E-10){
 		vrec(S, w, 0);
 		w->cycles++;

@@ -1111,7 +1111,9 @@ __global__ __launch_bounds__(1024) void k_mg_coarse(const double *__restrict__ r
 			f.phi[g] += prol_low<ND, 0>(c.phi, c.L, cf);
 		}
 		__syncthreads();
-		blk_neutralize(f.phi, f.N, wred);
+		// no neutralisation before the post-smoothing (native mode, round 4):
+		// the smoother commutes with adding a constant, the one after it
+		// removes the mean
 		blk_smooth<ND>(f.phi, f.rho, f.L, a.nPost, gs3d);
 		blk_neutralize(f.phi, f.N, wred);
 	}
@@ -1217,7 +1219,158 @@ __global__ void k_prolong_add_slab(double *__restrict__ phiX, pinc_lvl_t Lxp, in
 	}
 }
 
+// ------------------------------------------ level-0 transfers, 3-D (round 4)
+// The three point stencils around the coarse correction, restructured so
+// that each thread does the work of a whole coarse cell and no point index is
+// divided per fine point; each value is the same expression as before, so the
+// results are bit-identical to k_residual + k_restrict (+ the native x4) and
+// to k_prolong_add.
+//
+// Restricted residual: coarse point c gets the half-weight restriction
+// (mgHalfRestrict3D, multigrid.c:844-911, or the ND form) of the fine
+// residual (mgResidual, multigrid.c:1385-1403) at its fine point 2c and the
+// six neighbours, the residual computed on the fly (residual_at's order), so
+// the fine residual is never written and read back; times `scale` (4 in
+// native mode: exact, a power of two).
+template <bool HW3D>
+__global__ __launch_bounds__(kThreads) void k_resid_restrict3(const double *__restrict__ phi,
+                                                              const double *__restrict__ rho,
+                                                              double *__restrict__ coarse, pinc_lvl_t Lcp,
+                                                              double scale) {
+	pinc_lvl_t Lfp = Lcp;
+	for (int d = 0; d < 3; d++) Lfp.T[d] = 2 * Lcp.T[d];
+	const Lv F = make_lv(Lfp);
+	const unsigned CX = Lcp.T[0], CY = Lcp.T[1];
+	const unsigned n = CX * CY * (unsigned)Lcp.T[2];
+	for (unsigned gc = blockIdx.x * blockDim.x + threadIdx.x; gc < n; gc += gridDim.x * blockDim.x) {
+		const unsigned r = gc / CX;
+		int cf[3] = {2 * (int)(gc - r * CX), 2 * (int)(r % CY), 2 * (int)(r / CY)};
+		const long gf = (long)cf[0] + cf[1] * F.s[1] + cf[2] * F.s[2];
+		auto res_nb = [&](int d, int up) {
+			int c[3] = {cf[0], cf[1], cf[2]};
+			const long o = up ? nb_up(F, cf, d) : nb_dn(F, cf, d);
+			c[d] = up ? (cf[d] + 1 < F.T[d] ? cf[d] + 1 : 0) : (cf[d] > 0 ? cf[d] - 1 : F.T[d] - 1);
+			return residual_at<3>(phi, rho, F, c, gf + o);
+		};
+		const double f0 = residual_at<3>(phi, rho, F, cf, gf);
+		const double xp = res_nb(0, 1), xm = res_nb(0, 0), yp = res_nb(1, 1), ym = res_nb(1, 0);
+		const double zp = res_nb(2, 1), zm = res_nb(2, 0);
+		double v;
+		if (HW3D) {
+			v = (1. / 12.) * (6 * f0 + xp + xm + yp + ym + zp + zm);
+		} else {
+			v = (2. * 3) * f0;
+			v += xp + xm;
+			v += yp + ym;
+			v += zp + zm;
+			v *= 1. / (3 * 4);
+		}
+		coarse[gc] = v * scale;
+	}
+}
+
+// phi_f += P(phi_c) (mgBilinProl3D + gAddTo): one thread per coarse cell
+// writes its 2 x 2 x 2 fine points (x pairs as 16-byte accesses) from the 8
+// coarse corner values, each point with prol_low's nesting (x outermost, z
+// innermost; 0.5 * (a + b) per odd dimension).
+__global__ __launch_bounds__(kThreads) void k_prolong_add3c(double *__restrict__ phiF,
+                                                            const double *__restrict__ phiC, pinc_lvl_t Lcp) {
+	const unsigned CX = Lcp.T[0], CY = Lcp.T[1], CZ = Lcp.T[2];
+	const long sy = (long)CX, sz = (long)CX * CY;
+	const long fx = 2L * CX, fxy = fx * 2L * CY;
+	const unsigned n = CX * CY * CZ;
+	for (unsigned gc = blockIdx.x * blockDim.x + threadIdx.x; gc < n; gc += gridDim.x * blockDim.x) {
+		const unsigned r = gc / CX;
+		const int cx = (int)(gc - r * CX), cy = (int)(r % CY), cz = (int)(r / CY);
+		const int cx1 = cx + 1 < (int)CX ? cx + 1 : 0, cy1 = cy + 1 < (int)CY ? cy + 1 : 0;
+		const int cz1 = cz + 1 < (int)CZ ? cz + 1 : 0;
+		double c[2][2][2];  // [dx][dy][dz]
+		const int xs[2] = {cx, cx1}, ys[2] = {cy, cy1}, zs[2] = {cz, cz1};
+#pragma unroll
+		for (int a = 0; a < 2; a++)
+#pragma unroll
+			for (int b = 0; b < 2; b++)
+#pragma unroll
+				for (int e = 0; e < 2; e++) c[a][b][e] = phiC[xs[a] + ys[b] * sy + zs[e] * sz];
+#pragma unroll
+		for (int k = 0; k < 2; k++) {
+#pragma unroll
+			for (int j = 0; j < 2; j++) {
+				double zv[2][2];  // [dx][dy]: z step
+#pragma unroll
+				for (int a = 0; a < 2; a++)
+#pragma unroll
+					for (int b = 0; b < 2; b++) zv[a][b] = k ? 0.5 * (c[a][b][0] + c[a][b][1]) : c[a][b][0];
+				double yv[2];
+#pragma unroll
+				for (int a = 0; a < 2; a++) yv[a] = j ? 0.5 * (zv[a][0] + zv[a][1]) : zv[a][0];
+				const double v0 = yv[0], v1 = 0.5 * (yv[0] + yv[1]);
+				double2 *f = reinterpret_cast<double2 *>(phiF + 2L * cx + (2L * cy + j) * fx + (2L * cz + k) * fxy);
+				double2 t = *f;
+				t.x += v0;
+				t.y += v1;
+				*f = t;
+			}
+		}
+	}
+}
+
+// RMS residual norm (mgSumTrueSquared of mgResidual, multigrid.c:1471-1481):
+// block b takes rows (y, z) b, b + nb, ... with a thread per x, so the only
+// division is per row; the block partials are in a fixed order.
+__global__ __launch_bounds__(kThreads) void k_residual_sumsq3r(const double *__restrict__ phi,
+                                                               const double *__restrict__ rho, pinc_lvl_t Lp,
+                                                               double *__restrict__ partial) {
+	__shared__ double red[kThreads / 64];
+	const Lv L = make_lv(Lp);
+	const unsigned rows = (unsigned)L.T[1] * L.T[2];
+	double acc = 0.;
+	for (unsigned row = blockIdx.x; row < rows; row += gridDim.x) {
+		const int y = (int)(row % (unsigned)L.T[1]), z = (int)(row / (unsigned)L.T[1]);
+		for (int x = threadIdx.x; x < L.T[0]; x += blockDim.x) {
+			const int c[3] = {x, y, z};
+			const long g = (long)x + y * L.s[1] + z * L.s[2];
+			const double v = residual_at<3>(phi, rho, L, c, g);
+			acc += v * v;
+		}
+	}
+	const double t = block_sum(acc, red);
+	if (threadIdx.x == 0) partial[blockIdx.x] = t;
+}
+
 }  // namespace
+
+extern "C" int pinc_hip_resid_restrict(const double *phi, const double *rho, double *coarse, pinc_lvl_t Lc,
+                                       int hw3d, double scale, void *stream) {
+	if (Lc.nd != 3) return set_error(hipErrorInvalidValue, "resid_restrict: 3-D levels only");
+	if (8 * npts(Lc) >= (1L << 31)) return set_error(hipErrorInvalidValue, "resid_restrict: level too large");
+	hipStream_t st = (hipStream_t)stream;
+	const unsigned nb = blocks_for(npts(Lc));
+	if (hw3d) hipLaunchKernelGGL(k_resid_restrict3<true>, dim3(nb), dim3(kThreads), 0, st, phi, rho, coarse, Lc, scale);
+	else hipLaunchKernelGGL(k_resid_restrict3<false>, dim3(nb), dim3(kThreads), 0, st, phi, rho, coarse, Lc, scale);
+	return check_launch("resid_restrict");
+}
+
+extern "C" int pinc_hip_prolong_add3(double *phiF, const double *phiC, pinc_lvl_t Lc, void *stream) {
+	if (Lc.nd != 3) return set_error(hipErrorInvalidValue, "prolong_add3: 3-D levels only");
+	if (8 * npts(Lc) >= (1L << 31)) return set_error(hipErrorInvalidValue, "prolong_add3: level too large");
+	if (reinterpret_cast<unsigned long>(phiF) & 15)
+		return set_error(hipErrorInvalidValue, "prolong_add3: fine grid not 16-byte aligned");
+	hipLaunchKernelGGL(k_prolong_add3c, dim3(blocks_for(npts(Lc))), dim3(kThreads), 0, (hipStream_t)stream, phiF,
+	                   phiC, Lc);
+	return check_launch("prolong_add3");
+}
+
+extern "C" int pinc_hip_residual_sumsq_rows(const double *phi, const double *rho, pinc_lvl_t L, double *partial,
+                                            int *nBlocks, void *stream) {
+	if (L.nd != 3) return set_error(hipErrorInvalidValue, "residual_sumsq_rows: 3-D levels only");
+	if (npts(L) >= (1L << 31)) return set_error(hipErrorInvalidValue, "residual_sumsq_rows: level too large");
+	long rows = (long)L.T[1] * L.T[2];
+	unsigned nb = (unsigned)(rows < kMaxBlocks ? rows : kMaxBlocks);
+	*nBlocks = (int)nb;
+	hipLaunchKernelGGL(k_residual_sumsq3r, dim3(nb), dim3(kThreads), 0, (hipStream_t)stream, phi, rho, L, partial);
+	return check_launch("residual_sumsq_rows");
+}
 
 extern "C" int pinc_hip_gs_pass(double *phi, const double *rho, pinc_lvl_t L, int pass, int nd3,
                                 const double *muPrev, double *partial, int *nBlocks, void *stream) {

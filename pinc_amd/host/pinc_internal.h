@@ -184,6 +184,9 @@ struct MultigridSolver {
 	pinc_lvl_t L[PINC_MAX_LEVELS];
 	long N[PINC_MAX_LEVELS];
 	double *rho[PINC_MAX_LEVELS], *phi[PINC_MAX_LEVELS], *res[PINC_MAX_LEVELS];
+	/* native smoothing ping-pongs phi[q] and res[q] by swapping the
+	 * pointers; swapped[q] = 1 while they are exchanged (pp_restore) */
+	int swapped[PINC_MAX_LEVELS];
 	long cycles;
 	Grid *rhoGrid, *phiGrid;
 	int native;

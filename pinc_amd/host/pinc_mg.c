@@ -19,6 +19,7 @@
 #define _GNU_SOURCE
 #include "pinc_internal.h"
 #include <math.h>
+#include <stdint.h>
 
 #define MU_SLOT 32   /* two alternating mean slots of the smoother */
 #define TMP_SLOT 40
@@ -387,6 +388,8 @@ static void prolong_into(MultigridSolver *S, int qf) {
 		pinc_check(pinc_hip_prolong_add_slab(S->phi[0], S->L[0], S->z0, S->L[1].T[2] * 2, S->phi[1], S->L[1],
 		                                     g_pinc.stream),
 		           "prolong slab");
+	else if (S->L[qf].nd == 3 && !((uintptr_t)S->phi[qf] & 15))
+		pinc_check(pinc_hip_prolong_add3(S->phi[qf], S->phi[qf + 1], S->L[qf + 1], g_pinc.stream), "prolong");
 	else pinc_check(pinc_hip_prolong_add(S->phi[qf], S->phi[qf + 1], S->L[qf], g_pinc.stream), "prolong");
 }
 
@@ -403,6 +406,14 @@ static void restrict_residual(MultigridSolver *S, int q) {
 		long n1 = (long)S->L1s.T[0] * S->L1s.T[1] * S->L1s.T[2];
 		if (g_pinc.nranks > 1) pinc_comm_allgather(S->rho1Slab, S->rho[1], n1, "gather level 1");
 		else pinc_check(pinc_hip_d2d(S->rho[1], S->rho1Slab, n1 * sizeof(double), g_pinc.stream), "level 1");
+		return;
+	}
+	if (S->L[q].nd == 3) {
+		/* residual and restriction in one pass (the fine residual is never
+		 * stored); the native x4 folded in */
+		pinc_check(pinc_hip_resid_restrict(S->phi[q], S->rho[q], S->rho[q + 1], S->L[q + 1], S->restr3d,
+		                                   S->native ? 4.0 : 1.0, g_pinc.stream),
+		           "residual restrict");
 		return;
 	}
 	pinc_check(pinc_hip_residual(S->res[q], S->phi[q], S->rho[q], S->L[q], g_pinc.stream), "residual");
@@ -427,7 +438,22 @@ static void smooth_native(MultigridSolver *S, int q, int nIter, int nd3) {
 	/* two iterations per launch (pinc_hip_gs_sweep2x) in pairs, so that the
 	 * ping-pong ends in phi */
 	int fused2 = fused && L.T[0] % 32 == 0 && L.T[1] % 8 == 0;
-	if (fused2) {
+	if (fused2 && !(q == 0 && S->shard)) {
+		/* one launch per two iterations, phi[q] -> res[q], then the pointers
+		 * swap (round 4: a smoothing of 10 is five double sweeps instead of
+		 * four and a pair of single ones; the V-cycle's other kernels take
+		 * whichever buffer holds the iterate, pp_restore puts it back) */
+		for (; k + 2 <= nIter; k += 2) {
+			int slot = q == 0 && (k & 2) == 0 ? pinc_probe_begin(PINC_PROBE_GS) : -1;
+			pinc_check(pinc_hip_gs_sweep2x(S->phi[q], S->res[q], S->rho[q], L, g_pinc.stream), "gs sweep2x");
+			pinc_probe_end(PINC_PROBE_GS, slot, 24.0 * S->N[q]);
+			double *t = S->phi[q];
+			S->phi[q] = S->res[q];
+			S->res[q] = t;
+			S->swapped[q] ^= 1;
+		}
+	}
+	if (fused2 && q == 0 && S->shard) {
 		for (; k + 4 <= nIter; k += 4) {
 			int slot = q == 0 ? pinc_probe_begin(PINC_PROBE_GS) : -1;
 			pinc_check(pinc_hip_gs_sweep2x(S->phi[q], S->res[q], S->rho[q], L, g_pinc.stream), "gs sweep2x");
@@ -452,6 +478,16 @@ static void smooth_native(MultigridSolver *S, int q, int nIter, int nd3) {
 			           "gs pass");
 		}
 	}
+}
+
+/* the iterate back into phi[q]'s own buffer after a swapped smoothing */
+static void pp_restore(MultigridSolver *S, int q) {
+	if (!S->swapped[q]) return;
+	pinc_check(pinc_hip_d2d(S->res[q], S->phi[q], S->N[q] * sizeof(double), g_pinc.stream), "mg ping-pong");
+	double *t = S->phi[q];
+	S->phi[q] = S->res[q];
+	S->res[q] = t;
+	S->swapped[q] = 0;
 }
 
 static void smooth(MultigridSolver *S, int q, int nIter, int nd3) {
@@ -529,16 +565,23 @@ static void vrec(MultigridSolver *S, int q) {
 		neutralize(S->rho[q], S->N[q]);
 		smooth(S, q, S->nCoarse, S->coarse3d);
 		neutralize(S->phi[q], S->N[q]);
+		pp_restore(S, q);
 		prolong_into(S, q - 1);
 		return;
 	}
-	neutralize_level(S, q, S->rho[q]);
+	/* native mode: level 0's rho is neutralised once per solve (mgSolve),
+	 * not per cycle -- it does not change during the solve -- and phi is not
+	 * neutralised between the prolongation and the post-smoothing: the
+	 * smoother commutes with adding a constant and the neutralisation after
+	 * it removes the mean (round 4; the oracle's native solve mirrors both) */
+	if (!(S->native && q == 0)) neutralize_level(S, q, S->rho[q]);
 	smooth(S, q, S->nPre, S->pre3d);
 	restrict_residual(S, q);
 	vrec(S, q + 1);
-	neutralize_level(S, q, S->phi[q]);
+	if (!S->native) neutralize_level(S, q, S->phi[q]);
 	smooth(S, q, S->nPost, S->post3d);
 	neutralize_level(S, q, S->phi[q]);
+	pp_restore(S, q);
 	if (q > 0) prolong_into(S, q - 1);
 }
 
@@ -568,6 +611,7 @@ void mgSolve(MultigridSolver *S, Grid *rho, Grid *phi, const MpiInfo *mpiInfo) {
 		double barRes = 2.;
 		long c = 0;
 		S->histN = 0;
+		if (S->native) neutralize_level(S, 0, S->rho[0]);
 		while (barRes > 1.E-10) {
 			if (S->useGraph) {
 				/* the V-cycle is a fixed launch sequence on fixed buffers:
@@ -597,8 +641,14 @@ void mgSolve(MultigridSolver *S, Grid *rho, Grid *phi, const MpiInfo *mpiInfo) {
 				pinc_check(pinc_hip_reduce(g_pinc.dScratch, nb, 1.0, PINC_SLOT(TMP_SLOT + 1), g_pinc.stream), "norm");
 				if (g_pinc.nranks > 1) pinc_comm_allreduce_sum(PINC_SLOT(TMP_SLOT + 1), 1, "norm");
 			} else {
-				pinc_check(pinc_hip_residual_sumsq(S->phi[0], S->rho[0], S->L[0], g_pinc.dScratch, &nb, g_pinc.stream),
-				           "residual norm");
+				if (S->L[0].nd == 3)
+					pinc_check(pinc_hip_residual_sumsq_rows(S->phi[0], S->rho[0], S->L[0], g_pinc.dScratch, &nb,
+					                                        g_pinc.stream),
+					           "residual norm");
+				else
+					pinc_check(pinc_hip_residual_sumsq(S->phi[0], S->rho[0], S->L[0], g_pinc.dScratch, &nb,
+					                                   g_pinc.stream),
+					           "residual norm");
 				pinc_probe_end(PINC_PROBE_RESIDUAL, slot, 16.0 * S->N[0]);
 				pinc_check(pinc_hip_reduce(g_pinc.dScratch, nb, 1.0, PINC_SLOT(TMP_SLOT + 1), g_pinc.stream), "norm");
 			}
@@ -627,6 +677,7 @@ void mgSolve(MultigridSolver *S, Grid *rho, Grid *phi, const MpiInfo *mpiInfo) {
 		for (int c = 0; c < S->mgCycles; c++) {
 			neutralize(S->rho[0], S->N[0]);
 			smooth(S, 0, S->nCoarse, S->coarse3d);
+			pp_restore(S, 0);
 		}
 	}
 	guess_end(S, role);
