@@ -180,6 +180,39 @@ def _cpu_baseline(size: int, ppc: int, steps: int, native: bool, workload: str =
             "phase_ms_per_step": ph}
 
 
+def _push_order(samples: list) -> list:
+    """Per species, the fused push launches of the timed steps by kind
+    (`_lib.probe_samples("push")`, launch order): mean plain, count and sort
+    launch, the "fresh" plain launch (the first after each sort of that
+    species, or the run's first), and the ratios the sort schedule is judged
+    by -- the plain push's decay between sorts and the sorting push's cost."""
+    names = ("plain", "count", "sort")   # _lib.PUSH_KIND_NAMES
+    by = {}
+    for ms, tag in samples:
+        by.setdefault(tag & 0xff, []).append((ms, names[tag >> 8]))
+    out = []
+    for s in sorted(by):
+        seq = by[s]
+        kinds = {k: [m for m, kk in seq if kk == k] for k in names}
+        fresh, after_sort = [], True
+        for m, k in seq:
+            if k == "plain" and after_sort:
+                fresh.append(m)
+            after_sort = k == "sort"
+        mean = {k: (sum(v) / len(v) if v else None) for k, v in kinds.items()}
+        f = sum(fresh) / len(fresh) if fresh else None
+        row = {"species": s, "launches": len(seq), "sorts": len(kinds["sort"]), "counts": len(kinds["count"]),
+               "plain_ms": mean["plain"], "count_ms": mean["count"], "sort_ms": mean["sort"], "fresh_plain_ms": f,
+               "all_ms": sum(m for m, _ in seq) / len(seq)}
+        if mean["plain"] and f:
+            row["plain_vs_fresh"] = mean["plain"] / f
+        for k in ("count", "sort"):
+            if mean[k] and mean["plain"]:
+                row[f"{k}_vs_plain"] = mean[k] / mean["plain"]
+        out.append(row)
+    return out
+
+
 def _multi_rank_summary(info: list, steps: int, dom: str, transport: str) -> dict:
     """What an N-GPU line needs to say where the time went: every phase's
     maximum (and minimum) over the ranks, each collective kind's device time,
@@ -451,6 +484,9 @@ def main() -> int:
         for k in ("push_count", "push_sort"):
             if k in sub:
                 sub[k]["vs_plain"] = sub[k]["mean_launch_ms"] / sub["push_plain"]["mean_launch_ms"]
+    push_order = _push_order(_lib.probe_samples("push"))
+    if push_order:
+        sub["by_species"] = push_order
     # configuration key of the PMC traffic profiles (tools/pmc_summary.py)
     traffic_key = {"workload": args.workload, "grid": [S] * nd, "ppc_per_species": args.ppc, "n_gpus": world,
                    "layout": args.layout}

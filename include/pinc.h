@@ -393,6 +393,10 @@ int pinc_sim_timers_reset(PincSim *sim);
 #define PINC_PROBE_ALL (-1)
 int pinc_probe_start(int kernel, int maxSamples);
 int pinc_probe_read(int kernel, double *meanMs, double *meanBytes, int *samples, long *launches);
+/* Duration (ms) of recorded launch i of a probed kernel, in launch order, and
+ * its tag (PINC_PROBE_PUSH: species | kind << 8, kind 0 plain, 1 count,
+ * 2 sort; 0 for the other kernels).  Returns 1 if i is not recorded. */
+int pinc_probe_sample(int kernel, int i, double *ms, int *tag);
 long pinc_sim_total_particles(PincSim *sim);
 
 /* Host transport for the multi-rank collectives (testing and CI: several

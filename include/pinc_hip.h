@@ -404,12 +404,10 @@ int pinc_hip_prolong_add(double *phiFine, const double *phiCoarse, pinc_lvl_t Lf
  * to the point kernels above): coarse = scale * restrict(residual(phi, rho))
  * (mgResidual + mgHalfRestrict3D / ND without writing the fine residual;
  * scale 4 in native mode); phi_f += P(phi_c) for the coarse level Lc (phi_f
- * 16-byte aligned); the residual norm's block partials (*nBlocks) */
+ * 16-byte aligned) */
 int pinc_hip_resid_restrict(const double *phi, const double *rho, double *coarse, pinc_lvl_t Lc, int hw3d,
                             double scale, void *stream);
 int pinc_hip_prolong_add3(double *phiFine, const double *phiCoarse, pinc_lvl_t Lc, void *stream);
-int pinc_hip_residual_sumsq_rows(const double *phi, const double *rho, pinc_lvl_t L, double *partial, int *nBlocks,
-                                 void *stream);
 
 /* ---------------------------------------------------------- spectral -- */
 /* Spectral Poisson solve on rocFFT, replacing sAlloc/sSolve/sFree

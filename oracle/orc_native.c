@@ -16,7 +16,7 @@
  * -- and changes the cycle: the restricted residual is scaled by 4 (the
  * coarse h^2), every coarse visit starts from zero (correction scheme), no
  * neutralisation after each colour (once per level visit instead; level 0's
- * rho once per solve; none between prolongation and post-smoothing), and the
+ * rho and phi once per solve; none between prolongation and post-smoothing), and the
  * hierarchy continues down to 2 points per dimension.
  *
  * The solve runs on the global periodic grid (no ghosts, x fastest),
@@ -262,16 +262,16 @@ static void vrec(ONative *S, OWorld *w, int q){
 		prolong_add(S, q-1);
 		return;
 	}
-	/* level 0's rho is neutralised once per solve (ow_native_solve); no
-	 * neutralisation between the prolongation and the post-smoothing
-	 * (pinc_mg.c vrec, k_mg_coarse) */
+	/* level 0's rho and phi are neutralised once per solve
+	 * (ow_native_solve); no neutralisation between the prolongation and the
+	 * post-smoothing (pinc_mg.c vrec, k_mg_coarse) */
 	if(q > 0) neutralize(S->rho[q], S->L[q].N);
 	smooth(S, q, w->nPre, pre);
 	residual(S, q);
 	restrict4(S, q);
 	vrec(S, w, q+1);
 	smooth(S, q, w->nPost, post);
-	neutralize(S->phi[q], S->L[q].N);
+	if(q > 0) neutralize(S->phi[q], S->L[q].N);
 	if(q > 0) prolong_add(S, q-1);
 }
 
@@ -350,6 +350,7 @@ void ow_native_solve(OWorld *w){
 		if(w->mgCap > 0 && ++c >= w->mgCap) break;
 		if(!isfinite(barRes)) orc_die("native multigrid diverged (residual %g)", barRes);
 	}
+	if(S->nLevels > 1) neutralize(S->phi[0], N);
 	if(role == ON_GUESS_FIRST){
 		double *t = S->B; S->B = S->A; S->A = t;
 		memcpy(S->A, ph, N*sizeof(double));

@@ -127,6 +127,7 @@ _sigs = {
     "pinc_comm_kind_name": (C.c_char_p, [C.c_int]),
     "pinc_probe_read": (C.c_int, [C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_int),
                                   C.POINTER(C.c_long)]),
+    "pinc_probe_sample": (C.c_int, [C.c_int, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int)]),
 }
 PROBES = {"gs_pass": 0, "accelerate": 1, "move_classify": 2, "deposit": 3, "residual_sumsq": 4, "spectral": 5, "push": 6,
           "mg_cycle": 7, "push_plain": 8, "push_count": 9, "push_sort": 10}
@@ -159,6 +160,20 @@ def comm_stats_read() -> dict:
         return {}
     return {HOST.pinc_comm_kind_name(k).decode(): {"ms": float(ms[k]), "bytes": float(by[k]), "calls": int(calls[k]),
                                                    "timed_calls": int(timed[k])} for k in range(COMM_KINDS)}
+
+
+PUSH_KIND_NAMES = ("plain", "count", "sort")
+
+
+def probe_samples(kernel: str) -> list[tuple[float, int]]:
+    """(ms, tag) of every recorded launch of a probed kernel, in launch order
+    (push: tag = species | kind << 8, PUSH_KIND_NAMES[kind])."""
+    out, i = [], 0
+    ms, tag = C.c_double(), C.c_int()
+    while HOST.pinc_probe_sample(PROBES[kernel], i, C.byref(ms), C.byref(tag)) == 0:
+        out.append((ms.value, tag.value))
+        i += 1
+    return out
 
 
 def probe_read(kernel: str) -> dict:

@@ -62,10 +62,42 @@ HIP_SRC = ["runtime.hip", "k_particles.hip", "k_grid.hip", "k_mg.hip", "k_spectr
 C_SRC = ["pinc_core.c", "pinc_boot.c", "pinc_comm.c", "pinc_grid.c", "pinc_pop.c", "pinc_pusher.c", "pinc_mg.c", "pinc_spectral.c", "pinc_regular.c", "pinc_h5.c", "pinc_obj.c"]
 
 
-def _run(cmd: list[str]) -> None:
+def _run(cmd: list[str], log: Path | None = None) -> None:
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"command failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    if log is not None:
+        log.write_text(r.stderr)
+
+
+def _resources_log(src: str) -> Path:
+    """The compiler's per-kernel resource report of one HIP source (VGPRs,
+    spills, LDS, occupancy: -Rpass-analysis=kernel-resource-usage)."""
+    return LIB / f"{src}.resources.txt"
+
+
+def kernel_resources(lib: Path | None = None) -> dict:
+    """{kernel (mangled): {"vgprs", "vgpr_spill", "sgpr_spill", "occupancy", "lds"}} from the
+    resource reports the last build wrote next to the libraries."""
+    import re
+    out = {}
+    for f in HIP_SRC:
+        p = (lib or LIB) / f"{f}.resources.txt"
+        if not p.exists():
+            continue
+        cur = None
+        for line in p.read_text().splitlines():
+            m = re.search(r"remark: Function Name: (\S+)", line)
+            if m:
+                cur = out.setdefault(m.group(1), {"source": f})
+                continue
+            m = re.search(r"remark:\s+(VGPRs|VGPRs Spill|SGPRs Spill|Occupancy \[waves/SIMD\]|LDS Size \[bytes/block\]): (\d+)",
+                          line)
+            if m and cur is not None:
+                key = {"VGPRs": "vgprs", "VGPRs Spill": "vgpr_spill", "SGPRs Spill": "sgpr_spill",
+                       "Occupancy [waves/SIMD]": "occupancy", "LDS Size [bytes/block]": "lds"}[m.group(1)]
+                cur[key] = int(m.group(2))
+    return out
 
 
 def _newer(src: Path, dst: Path, deps: list[Path]) -> bool:
@@ -104,14 +136,15 @@ def build(verbose: bool = False, jobs: int = 8) -> dict:
     jobs_list = []
     for f in HIP_SRC:
         src, obj = CSRC / f, OBJ / (f + ".o")
-        if flags_changed or _newer(src, obj, hip_deps):
-            jobs_list.append([HIPCC, *HIP_FLAGS, "-c", str(src), "-o", str(obj)])
+        if flags_changed or _newer(src, obj, hip_deps) or not _resources_log(f).exists():
+            jobs_list.append(([HIPCC, *HIP_FLAGS, "-Rpass-analysis=kernel-resource-usage", "-c", str(src), "-o",
+                               str(obj)], _resources_log(f)))
     for f in C_SRC:
         src, obj = HOST / f, OBJ / (f + ".o")
         if _newer(src, obj, c_deps):
-            jobs_list.append(["gcc", *C_FLAGS, "-c", str(src), "-o", str(obj)])
+            jobs_list.append((["gcc", *C_FLAGS, "-c", str(src), "-o", str(obj)], None))
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        list(ex.map(_run, jobs_list))
+        list(ex.map(lambda j: _run(*j), jobs_list))
     hip_objs = [str(OBJ / (f + ".o")) for f in HIP_SRC]
     c_objs = [str(OBJ / (f + ".o")) for f in C_SRC]
     _run([HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", str(libhip), *hip_objs,

@@ -1315,29 +1315,6 @@ __global__ __launch_bounds__(kThreads) void k_prolong_add3c(double *__restrict__
 	}
 }
 
-// RMS residual norm (mgSumTrueSquared of mgResidual, multigrid.c:1471-1481):
-// block b takes rows (y, z) b, b + nb, ... with a thread per x, so the only
-// division is per row; the block partials are in a fixed order.
-__global__ __launch_bounds__(kThreads) void k_residual_sumsq3r(const double *__restrict__ phi,
-                                                               const double *__restrict__ rho, pinc_lvl_t Lp,
-                                                               double *__restrict__ partial) {
-	__shared__ double red[kThreads / 64];
-	const Lv L = make_lv(Lp);
-	const unsigned rows = (unsigned)L.T[1] * L.T[2];
-	double acc = 0.;
-	for (unsigned row = blockIdx.x; row < rows; row += gridDim.x) {
-		const int y = (int)(row % (unsigned)L.T[1]), z = (int)(row / (unsigned)L.T[1]);
-		for (int x = threadIdx.x; x < L.T[0]; x += blockDim.x) {
-			const int c[3] = {x, y, z};
-			const long g = (long)x + y * L.s[1] + z * L.s[2];
-			const double v = residual_at<3>(phi, rho, L, c, g);
-			acc += v * v;
-		}
-	}
-	const double t = block_sum(acc, red);
-	if (threadIdx.x == 0) partial[blockIdx.x] = t;
-}
-
 }  // namespace
 
 extern "C" int pinc_hip_resid_restrict(const double *phi, const double *rho, double *coarse, pinc_lvl_t Lc,
@@ -1359,17 +1336,6 @@ extern "C" int pinc_hip_prolong_add3(double *phiF, const double *phiC, pinc_lvl_
 	hipLaunchKernelGGL(k_prolong_add3c, dim3(blocks_for(npts(Lc))), dim3(kThreads), 0, (hipStream_t)stream, phiF,
 	                   phiC, Lc);
 	return check_launch("prolong_add3");
-}
-
-extern "C" int pinc_hip_residual_sumsq_rows(const double *phi, const double *rho, pinc_lvl_t L, double *partial,
-                                            int *nBlocks, void *stream) {
-	if (L.nd != 3) return set_error(hipErrorInvalidValue, "residual_sumsq_rows: 3-D levels only");
-	if (npts(L) >= (1L << 31)) return set_error(hipErrorInvalidValue, "residual_sumsq_rows: level too large");
-	long rows = (long)L.T[1] * L.T[2];
-	unsigned nb = (unsigned)(rows < kMaxBlocks ? rows : kMaxBlocks);
-	*nBlocks = (int)nb;
-	hipLaunchKernelGGL(k_residual_sumsq3r, dim3(nb), dim3(kThreads), 0, (hipStream_t)stream, phi, rho, L, partial);
-	return check_launch("residual_sumsq_rows");
 }
 
 extern "C" int pinc_hip_gs_pass(double *phi, const double *rho, pinc_lvl_t L, int pass, int nd3,

@@ -1371,12 +1371,22 @@ constexpr int kPushGroupMin = PINC_PUSH_GROUP_MIN;
 #ifndef PINC_PUSH_CONSEC
 #define PINC_PUSH_CONSEC 1
 #endif
+// lane pairs (PINC_PUSH_CONSEC 0): nontemporal particle loads and stores
+#ifndef PINC_PUSH_NT
+#define PINC_PUSH_NT 0
+#endif
 #ifndef PINC_PUSH_RHO_LDS
 #define PINC_PUSH_RHO_LDS 2048
 #endif
 constexpr int kRhoLds = PINC_PUSH_COPIES ? PINC_PUSH_RHO_LDS : 1024;
 
 constexpr int kPushGroups = PINC_PUSH_GROUPS;
+// 1: the sorting push ranks its items with wave-aggregated LDS atomics
+// (lds_agg_add, round 3); 0: plain LDS atomics (measured at C4: electron
+// sorting push 36.2 -> 33.5 ms)
+#ifndef PINC_PUSH_AGG
+#define PINC_PUSH_AGG 0
+#endif
 // 8 waves x 4 particles per thread per PINC_CHUNK block: fewer live VGPRs
 // (px) than 4 waves x 8, so more waves per SIMD hide the gather latency
 #ifndef PINC_PUSH_ITEMS
@@ -1757,7 +1767,8 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	// the sorting push stages its sorted output in the same LDS once the
 	// kick has read E (a barrier separates the last E read from the first
 	// staged write)
-	constexpr int kEL = KICK ? EC * ND : 1, kST = SORT ? kPushChunk : 1;
+	// (the sorted output is staged two components at a time)
+	constexpr int kEL = KICK ? EC * ND : 1, kST = SORT ? 2 * kPushChunk : 1;
 	__shared__ __attribute__((aligned(16))) double eLs[kEL > kST ? kEL : kST];
 	double *const eL = eLs;
 	__shared__ int cntIn[SORT ? kInCellCap : 1];
@@ -1834,7 +1845,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 		for (int d = 0; d < ND; d++) {
 			if (ok1 && al) {
 				// streamed once per step (far beyond L2/MALL): non-temporal
-#if PINC_PUSH_CONSEC
+#if PINC_PUSH_CONSEC || !PINC_PUSH_NT
 				const dvec2 x = *reinterpret_cast<const dvec2 *>(a.xi[d] + i);
 				const dvec2 v = *reinterpret_cast<const dvec2 *>(a.vi[d] + i);
 #else
@@ -1966,6 +1977,8 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	}
 	__syncthreads();
 
+	int resBase = 0;      // sorting push: this thread's brick reservation
+	bool resCell = false;  // sorting push: cell threadIdx.x of iB has items
 	PUSH_TS(2);
 	// ---- phase C (sorted output): rank of every item inside its input cell,
 	// and one global reservation per input cell of the block.  Per item, in
@@ -1985,8 +1998,16 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 			const bool ok = (valid >> k) & 1u;
 			if (ok && iB.inside(c, ND)) lc = iB.index(c, ND);
 			else if (ok) lb = brick_inside<ND>(a.tg, ib, c);
+			// plain LDS atomics: a wave's lanes share a few cells (16-way
+			// same-address conflicts at most for sorted input), cheaper than
+			// aggregating the groups with ballots and shuffles
+#if PINC_PUSH_AGG
 			const int rank = lds_agg_add<true>(cntIn, lc < 0 ? 0 : lc, lc >= 0);
 			const int rankB = lds_agg_add<true>(bCnt, lb < 0 ? 0 : lb, lb >= 0);
+#else
+			const int rank = lc >= 0 ? atomicAdd(&cntIn[lc], 1) : 0;
+			const int rankB = lb >= 0 ? atomicAdd(&bCnt[lb], 1) : 0;
+#endif
 			const bool out = ok && lc < 0 && lb < 0;
 			const int g = agg_add(a.cursor, out ? brick_first_key<ND>(a.tg, c) : 0, out);
 			rl[k] = lc >= 0 ? (rank << 9 | lc) : lb >= 0 ? (rankB << 9 | 256 | lb) : (ok ? ~g : -1);
@@ -2017,7 +2038,9 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 		}
 		__syncthreads();
 		const int bm = (int)threadIdx.x < ib.vol ? bCnt[threadIdx.x] : 0;
-		if (bm) bBase[threadIdx.x] = atomicAdd(&a.cursor[brick_key<ND>(a.tg, ib, threadIdx.x)], bm);
+		// the global reservation's result is first needed by the stores after
+		// the kick: its round trip overlaps the kick (resBase, one VGPR)
+		if (bm) resBase = atomicAdd(&a.cursor[brick_key<ND>(a.tg, ib, threadIdx.x)], bm);
 		// block slot of each brick's run: exclusive scan of the brick counts
 		const int inc = wave_incl_scan(bm);
 		if (lane == 63) red[wv] = inc;
@@ -2031,11 +2054,13 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 			cbox[0] = t;  // items in the boxes (the box bounds are in registers by now)
 		}
 		__syncthreads();
-		// each cell of iB: global start and block slot of its run
+		// each cell of iB: block slot of its run; its brick and offset in the
+		// brick's run for the global start (after the kick)
 		if (m) {
-			cntIn[threadIdx.x] = bBase[lb] + bo;
+			cntIn[threadIdx.x] = lb << 16 | bo;
 			locStart[threadIdx.x] = bCnt[lb] + bo;
 		}
+		resCell = m != 0;
 		__syncthreads();
 	}
 
@@ -2257,7 +2282,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 #pragma unroll
 			for (int d = 0; d < ND; d++) {
 				if (ok1 && al) {
-#if PINC_PUSH_CONSEC
+#if PINC_PUSH_CONSEC || !PINC_PUSH_NT
 					*reinterpret_cast<dvec2 *>(a.xo[d] + i) = dvec2{p[k][d], p[k + 1][d]};
 					if (wv) *reinterpret_cast<dvec2 *>(a.vo[d] + i) = dvec2{vv[k][d], vv[k + 1][d]};
 #else
@@ -2276,6 +2301,15 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	}
 	PUSH_TS(4);
 	if (SORT) {
+		// global start of each cell run of iB: its brick's reservation + its
+		// offset in the brick's run
+		if ((int)threadIdx.x < ib.vol) bBase[threadIdx.x] = resBase;
+		__syncthreads();
+		if (resCell) {
+			const int pk = cntIn[threadIdx.x];
+			cntIn[threadIdx.x] = bBase[pk >> 16] + (pk & 0xffff);
+		}
+		__syncthreads();
 		{
 			// items in the box: block slots 0..nv-1, stored through LDS;
 			// the others straight to their global slot
@@ -2314,24 +2348,28 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 				a.flags[o] = (unsigned char)f;
 				if (f != a.center) atomicAdd(&a.chunkCount[o / PINC_CHUNK], 1);
 			}
-			auto flush = [&](double *out) {
-				__syncthreads();
-				for (int t = threadIdx.x; t < nv; t += kPushThreads) __builtin_nontemporal_store(stage[t], out + gdst[t]);
-				__syncthreads();
-			};
+			// components c = 0 .. 2 ND - 1 (positions, then velocities), two
+			// per round: half the barriers of one at a time
+			auto comp = [&](int k, int c) -> double { return c < ND ? p[k][c] : vv[k][c - ND]; };
+			auto dst = [&](int c) -> double * { return c < ND ? a.xo[c] : a.vo[c - ND]; };
 #pragma unroll
-			for (int d = 0; d < ND; d++) {
-#pragma unroll
-				for (int k = 0; k < kPushItems; k++)
-					if (slot[k] >= 0) stage[slot[k]] = p[k][d];
-				flush(a.xo[d]);
-			}
-#pragma unroll
-			for (int d = 0; d < ND; d++) {
+			for (int c = 0; c < 2 * ND; c += 2) {
+				// (the first round's writes follow the barrier after the kick's
+				// last E read and the slot assignment above)
+				if (c) __syncthreads();
 #pragma unroll
 				for (int k = 0; k < kPushItems; k++)
-					if (slot[k] >= 0) stage[slot[k]] = vv[k][d];
-				flush(a.vo[d]);
+					if (slot[k] >= 0) {
+						stage[slot[k]] = comp(k, c);
+						stage[kPushChunk + slot[k]] = comp(k, c + 1);
+					}
+				__syncthreads();
+				double *const o0 = dst(c), *const o1 = dst(c + 1);
+				for (int t = threadIdx.x; t < nv; t += kPushThreads) {
+					const int g = gdst[t];
+					__builtin_nontemporal_store(stage[t], o0 + g);
+					__builtin_nontemporal_store(stage[kPushChunk + t], o1 + g);
+				}
 			}
 		}
 	}
@@ -2345,6 +2383,8 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 #pragma unroll
 			for (int d = 0; d < ND; d++) c[d] = (int)p[k][d];
 			const int lb = mine ? brick_inside<ND>(a.tg, obb, c) : -1;
+			// (aggregated: plain atomics here cost the plain instance, which
+			// carries this code behind a runtime test, 52 spilled VGPRs)
 			lds_agg_add<false>(cntOut, lb < 0 ? 0 : lb, lb >= 0);
 			if (mine && lb < 0) atomicAdd(&a.cntNext[brick_first_key<ND>(a.tg, c)], 1);
 		}
@@ -3104,21 +3144,19 @@ extern "C" int pinc_hip_push(pinc_pop_t pop, int s, pinc_geom_t g, const pinc_pu
 	*nBlocks = (int)nb;
 	hipStream_t st = (hipStream_t)stream;
 	const bool kick = args->kick != 0;
-#define LAUNCH_PUSH(ND, V3D)                                                                                 \
-	do {                                                                                                     \
-		if (kick && sort) hipLaunchKernelGGL((k_push<ND, V3D, true, true>), dim3(nb), dim3(kPushThreads), 0, st, a);   \
-		else if (kick) hipLaunchKernelGGL((k_push<ND, V3D, true, false>), dim3(nb), dim3(kPushThreads), 0, st, a);     \
-		else if (sort) hipLaunchKernelGGL((k_push<ND, V3D, false, true>), dim3(nb), dim3(kPushThreads), 0, st, a);     \
-		else hipLaunchKernelGGL((k_push<ND, V3D, false, false>), dim3(nb), dim3(kPushThreads), 0, st, a);              \
+	// a sorting push never counts (its brick counters use the count's LDS)
+	if (sort) a.cntNext = nullptr;
+#define LAUNCH_PUSH(ND, V3D, OBJ)                                                                                       \
+	do {                                                                                                                \
+		if (kick && sort) hipLaunchKernelGGL((k_push<ND, V3D, true, true, OBJ>), dim3(nb), dim3(kPushThreads), 0, st, a); \
+		else if (kick) hipLaunchKernelGGL((k_push<ND, V3D, true, false, OBJ>), dim3(nb), dim3(kPushThreads), 0, st, a);   \
+		else if (sort) hipLaunchKernelGGL((k_push<ND, V3D, false, true, OBJ>), dim3(nb), dim3(kPushThreads), 0, st, a);   \
+		else hipLaunchKernelGGL((k_push<ND, V3D, false, false, OBJ>), dim3(nb), dim3(kPushThreads), 0, st, a);            \
 	} while (0)
-	if (nd == 3 && a.objIn) {
-		if (kick && sort) hipLaunchKernelGGL((k_push<3, true, true, true, true>), dim3(nb), dim3(kPushThreads), 0, st, a);
-		else if (kick) hipLaunchKernelGGL((k_push<3, true, true, false, true>), dim3(nb), dim3(kPushThreads), 0, st, a);
-		else if (sort) hipLaunchKernelGGL((k_push<3, true, false, true, true>), dim3(nb), dim3(kPushThreads), 0, st, a);
-		else hipLaunchKernelGGL((k_push<3, true, false, false, true>), dim3(nb), dim3(kPushThreads), 0, st, a);
-	} else if (nd == 3) LAUNCH_PUSH(3, true);
-	else if (nd == 2) LAUNCH_PUSH(2, false);
-	else LAUNCH_PUSH(1, false);
+	if (nd == 3 && a.objIn) LAUNCH_PUSH(3, true, true);
+	else if (nd == 3) LAUNCH_PUSH(3, true, false);
+	else if (nd == 2) LAUNCH_PUSH(2, false, false);
+	else LAUNCH_PUSH(1, false, false);
 #undef LAUNCH_PUSH
 	return check_launch("push");
 }

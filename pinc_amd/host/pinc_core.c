@@ -523,9 +523,11 @@ static void probe_release(void) {
 			for (int i = 0; i < 2 * g_pinc.probeMax; i++) pinc_hip_event_destroy(g_pinc.probeEv[k][i]);
 			free(g_pinc.probeEv[k]);
 			free(g_pinc.probeBytes[k]);
+			free(g_pinc.probeTag[k]);
 		}
 		g_pinc.probeEv[k] = NULL;
 		g_pinc.probeBytes[k] = NULL;
+		g_pinc.probeTag[k] = NULL;
 		g_pinc.probeOn[k] = 0;
 		g_pinc.probeN[k] = 0;
 		g_pinc.probeLaunches[k] = 0;
@@ -542,6 +544,7 @@ int pinc_probe_start(int kernel, int maxSamples) {
 		g_pinc.probeOn[k] = 1;
 		g_pinc.probeEv[k] = calloc(2 * maxSamples, sizeof(void *));
 		g_pinc.probeBytes[k] = calloc(maxSamples, sizeof(double));
+		g_pinc.probeTag[k] = calloc(maxSamples, sizeof(int));
 		for (int i = 0; i < 2 * maxSamples; i++)
 			pinc_check(pinc_hip_event_create(&g_pinc.probeEv[k][i]), "probe event");
 	}
@@ -561,6 +564,19 @@ void pinc_probe_end(int k, int slot, double bytes) {
 	if (slot < 0 || !g_pinc.probeOn[k]) return;
 	pinc_check(pinc_hip_event_record(g_pinc.probeEv[k][2 * slot + 1], g_pinc.stream), "probe");
 	g_pinc.probeBytes[k][slot] = bytes;
+}
+
+void pinc_probe_tag(int k, int slot, int tag) {
+	if (slot >= 0 && g_pinc.probeOn[k]) g_pinc.probeTag[k][slot] = tag;
+}
+
+int pinc_probe_sample(int k, int i, double *ms, int *tag) {
+	if (k < 0 || k >= PINC_NPROBES || !g_pinc.probeOn[k] || i < 0 || i >= g_pinc.probeN[k]) return 1;
+	float t = 0;
+	pinc_check(pinc_hip_event_elapsed(&t, g_pinc.probeEv[k][2 * i], g_pinc.probeEv[k][2 * i + 1]), "probe read");
+	*ms = t;
+	*tag = g_pinc.probeTag[k][i];
+	return 0;
 }
 
 int pinc_probe_read(int k, double *meanMs, double *meanBytes, int *samples, long *launches) {

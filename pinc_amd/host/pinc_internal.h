@@ -42,11 +42,13 @@ typedef struct {
 	void **probeEv[PINC_NPROBES];   /* 2*probeMax events per kernel */
 	double *probeBytes[PINC_NPROBES]; /* algorithmic bytes of each recorded launch */
 	long probeLaunches[PINC_NPROBES]; /* launches seen (recorded or not) */
+	int *probeTag[PINC_NPROBES];     /* tag of each recorded launch (pinc_probe_tag) */
 } PincCtx;
 
 /* probe hooks around a launch of kernel k with algorithmic byte count b */
 int pinc_probe_begin(int k);
 void pinc_probe_end(int k, int slot, double bytes);
+void pinc_probe_tag(int k, int slot, int tag);
 
 extern PincCtx g_pinc;
 
@@ -100,6 +102,7 @@ struct PincDevPop {
 	int cntValid[PINC_MAX_SPECIES];
 	int everSorted;                     /* input already in cell order once */
 	int *perm;                          /* slot of each particle after a sorted push */
+	int permId[PINC_MAX_SPECIES];       /* ... identity for species s (left in order: perm not written) */
 	/* adaptive sort schedule (population:sortFraction > 0): a species is
 	 * sorted once the fraction of its particles that left their cell since
 	 * its last sort would pass sortFraction, at most sortMax pushes apart */
@@ -245,6 +248,8 @@ void pinc_ctx_init(void);
 void pinc_pop_flush_host(const Population *pop);
 /* the weight a deposit without the literal factor misses for the second fold
  * of main.c:232 (pinc_pusher.c) */
+/* kicked velocities pending after a sorting push, in the current order */
+void pinc_unsort_vel(const Population *pop, int s, int d, double *dst);
 void pinc_literal_second_fold(const Population *pop, Grid *rho, int order);
 
 /* helpers shared by the host translation units */

@@ -569,18 +569,19 @@ static void vrec(MultigridSolver *S, int q) {
 		prolong_into(S, q - 1);
 		return;
 	}
-	/* native mode: level 0's rho is neutralised once per solve (mgSolve),
-	 * not per cycle -- it does not change during the solve -- and phi is not
-	 * neutralised between the prolongation and the post-smoothing: the
-	 * smoother commutes with adding a constant and the neutralisation after
-	 * it removes the mean (round 4; the oracle's native solve mirrors both) */
+	/* native mode: level 0's rho and phi are neutralised once per solve
+	 * (mgSolve), not per cycle -- rho does not change during the solve, and
+	 * the V-cycle commutes with adding a constant to phi (the residual,
+	 * hence the correction, does not see it; the smoother carries it) -- and
+	 * no level's phi between the prolongation and the post-smoothing, for the
+	 * same reason (round 4; the oracle's native solve mirrors this) */
 	if (!(S->native && q == 0)) neutralize_level(S, q, S->rho[q]);
 	smooth(S, q, S->nPre, S->pre3d);
 	restrict_residual(S, q);
 	vrec(S, q + 1);
 	if (!S->native) neutralize_level(S, q, S->phi[q]);
 	smooth(S, q, S->nPost, S->post3d);
-	neutralize_level(S, q, S->phi[q]);
+	if (!(S->native && q == 0)) neutralize_level(S, q, S->phi[q]);
 	pp_restore(S, q);
 	if (q > 0) prolong_into(S, q - 1);
 }
@@ -641,14 +642,8 @@ void mgSolve(MultigridSolver *S, Grid *rho, Grid *phi, const MpiInfo *mpiInfo) {
 				pinc_check(pinc_hip_reduce(g_pinc.dScratch, nb, 1.0, PINC_SLOT(TMP_SLOT + 1), g_pinc.stream), "norm");
 				if (g_pinc.nranks > 1) pinc_comm_allreduce_sum(PINC_SLOT(TMP_SLOT + 1), 1, "norm");
 			} else {
-				if (S->L[0].nd == 3)
-					pinc_check(pinc_hip_residual_sumsq_rows(S->phi[0], S->rho[0], S->L[0], g_pinc.dScratch, &nb,
-					                                        g_pinc.stream),
-					           "residual norm");
-				else
-					pinc_check(pinc_hip_residual_sumsq(S->phi[0], S->rho[0], S->L[0], g_pinc.dScratch, &nb,
-					                                   g_pinc.stream),
-					           "residual norm");
+				pinc_check(pinc_hip_residual_sumsq(S->phi[0], S->rho[0], S->L[0], g_pinc.dScratch, &nb, g_pinc.stream),
+				           "residual norm");
 				pinc_probe_end(PINC_PROBE_RESIDUAL, slot, 16.0 * S->N[0]);
 				pinc_check(pinc_hip_reduce(g_pinc.dScratch, nb, 1.0, PINC_SLOT(TMP_SLOT + 1), g_pinc.stream), "norm");
 			}
@@ -673,6 +668,7 @@ void mgSolve(MultigridSolver *S, Grid *rho, Grid *phi, const MpiInfo *mpiInfo) {
 				break;
 			}
 		}
+		if (S->native) neutralize_level(S, 0, S->phi[0]);
 	} else {
 		for (int c = 0; c < S->mgCycles; c++) {
 			neutralize(S->rho[0], S->N[0]);

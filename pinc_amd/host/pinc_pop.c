@@ -416,7 +416,7 @@ void pSyncToHost(Population *p) {
 			for (long i = 0; i < n; i++) p->pos[(a + i) * nd + d] = tmp[i];
 			const double *vsrc = dv->p.v[d] + a;
 			if (dtmp) {
-				pinc_check(pinc_hip_gather_perm(dv->altV[d] + a, dv->perm + a, n, dtmp, g_pinc.stream), "pSyncToHost");
+				pinc_unsort_vel(p, s, d, dtmp);
 				vsrc = dtmp;
 			}
 			pinc_check(pinc_hip_d2h(tmp, vsrc, n * sizeof(double), g_pinc.stream), "pSyncToHost");

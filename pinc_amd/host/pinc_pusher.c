@@ -340,7 +340,8 @@ static int push_all(Population *pop, Grid *E, double *const *xout) {
 				                          dv->sinceSort[s] + 1 >= dv->sortMax);
 			} else {
 				sortS[s] = dv->moves % dv->sortInterval == 0;
-				countS[s] = (dv->moves + 1) % dv->sortInterval == 0;
+				/* (a sorting push never counts: sortInterval 1 recounts) */
+				countS[s] = !sortS[s] && (dv->moves + 1) % dv->sortInterval == 0;
 			}
 			sortNow |= sortS[s];
 		}
@@ -407,8 +408,9 @@ static int push_all(Population *pop, Grid *E, double *const *xout) {
 			pinc_check(pinc_hip_memset(dv->objCount + (long)s * dv->objK, 0, dv->objK * sizeof(int), g_pinc.stream),
 			           "object counts");
 		/* a species left in order by a sorting push still goes to the
-		 * alternate arrays (swapped for all species), perm = identity */
-		if (sortNow && !sortS[s]) pinc_check(pinc_hip_iota(dv->perm + pop->iStart[s], np, g_pinc.stream), "perm");
+		 * alternate arrays (swapped for all species); its perm is the
+		 * identity, recorded instead of written (pinc_unsort_vel) */
+		dv->permId[s] = !sortS[s];
 		if (sortS[s]) {
 			a.perm = dv->perm + pop->iStart[s];
 			if (!dv->cntValid[s]) {
@@ -437,6 +439,7 @@ static int push_all(Population *pop, Grid *E, double *const *xout) {
 		}
 		const int kind = sortS[s] ? PINC_PROBE_PUSH_SORT : countNext ? PINC_PROBE_PUSH_COUNT : PINC_PROBE_PUSH_PLAIN;
 		int slot = E ? pinc_probe_begin(PINC_PROBE_PUSH) : -1;
+		pinc_probe_tag(PINC_PROBE_PUSH, slot, s | (sortS[s] ? 2 : countNext ? 1 : 0) << 8);
 		int slotK = E ? pinc_probe_begin(kind) : -1;
 		pinc_check(pinc_hip_push(p, s, g, &a, &nb, g_pinc.stream), "push");
 		if (ts) {
@@ -494,6 +497,18 @@ static int push_all(Population *pop, Grid *E, double *const *xout) {
 	return sortNow;
 }
 
+/* dst = the kicked velocities (component d) of species s pending in altV
+ * after a sorting push, in the current particle order */
+void pinc_unsort_vel(const Population *pop, int s, int d, double *dst) {
+	const PincDevPop *dv = pop->dev;
+	long a = pop->iStart[s], n = pop->iStop[s] - a;
+	if (n <= 0) return;
+	if (dv->permId[s])
+		pinc_check(pinc_hip_d2d(dst, dv->altV[d] + a, n * sizeof(double), g_pinc.stream), "unsort velocities");
+	else
+		pinc_check(pinc_hip_gather_perm(dv->altV[d] + a, dv->perm + a, n, dst, g_pinc.stream), "unsort velocities");
+}
+
 static void swap_pos(PincDevPop *dv, int nd, int vel) {
 	for (int d = 0; d < nd; d++) {
 		double *t = dv->p.x[d];
@@ -518,10 +533,7 @@ static void classify(Population *pop, int doMove) {
 		if (dv->pendingSorted)
 			for (int s = 0; s < pop->nSpecies; s++)
 				for (int d = 0; d < nd; d++)
-					pinc_check(pinc_hip_gather_perm(dv->altV[d] + pop->iStart[s], dv->perm + pop->iStart[s],
-					                                pop->iStop[s] - pop->iStart[s], dv->p.v[d] + pop->iStart[s],
-					                                g_pinc.stream),
-					           "unsort velocities");
+					pinc_unsort_vel(pop, s, d, dv->p.v[d] + pop->iStart[s]);
 		dv->pending = dv->pendingSorted = 0;
 		/* its object counts go with it */
 		if (dv->objCount)

@@ -292,6 +292,39 @@ def test_tiled_layout(sim_cls, name, kw, maxwell, sched):
                 assert s.count(sp) == w.count(sp)
 
 
+def test_pending_sorting_push_read_and_dropped(sim_cls):
+    """A fused puAcc whose push sorts (tiled layout, sortInterval 1) leaves
+    the move pending with the kicked velocities in slot order.  Reading the
+    particles then (pSyncToHost), and dropping the move (an extract without a
+    move), must give the state of the unfused operators: positions unmoved
+    and bit-identical, velocities kicked.  (The fused run's first sorting
+    push is preceded by a sort of the lattice-ordered population, so the two
+    runs hold the particles in different orders: compared as sets, sorted by
+    position and velocity.)"""
+    cfg = configs.config("warm", **_WARM32)
+    cfg["population"]["layout"] = "tiled"
+    cfg["population"]["sortInterval"] = "1"
+    out = {}
+    for fused in ("0", "1"):
+        cfg["population"]["fused"] = fused
+        ini = configs.write_ini(cfg)
+        with sim_cls(ini, maxwell=True, perturb=False, seed=11) as s:
+            s.init()
+            s.op("acc")
+            read = [s.particles(sp) for sp in range(2)]
+            s.op("extract")
+            out[fused] = {"read": read, "dropped": [s.particles(sp) for sp in range(2)], "em": s.emigrants()}
+    for key in ("read", "dropped"):
+        for sp in range(2):
+            (p1, v1), (p0, v0) = out["1"][key][sp], out["0"][key][sp]
+            # (by position, then velocity: particles may share a lattice site)
+            o1 = np.lexsort(np.vstack([v1.T[::-1], p1.T[::-1]]))
+            o0 = np.lexsort(np.vstack([v0.T[::-1], p0.T[::-1]]))
+            np.testing.assert_array_equal(p1[o1], p0[o0])
+            assert np.abs(v1[o1] - v0[o0]).max() <= 1e-12 * np.abs(v0).max(), (key, sp)
+    np.testing.assert_array_equal(out["1"]["em"], out["0"]["em"])
+
+
 @pytest.mark.parametrize("name,kw,maxwell", [("cold3d", {}, False),
                                              ("warm", {"true_size": (32, 32, 32), "ppc": 8, "nalloc_pc": 16}, True),
                                              ("langmuir2d", {}, False), ("langmuir1d", {}, False)])

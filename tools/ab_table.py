@@ -36,7 +36,11 @@ def main() -> int:
             print(f"{n}: no bench line")
             continue
         pk = r.get("push_kinds", {})
-        kinds = " ".join(f"{k}={v['mean_launch_ms']:.2f}ms x{v['launches']}" for k, v in pk.items())
+        kinds = " ".join(f"{k}={v['mean_launch_ms']:.2f}ms x{v['launches']}" for k, v in pk.items()
+                         if isinstance(v, dict))
+        for row in pk.get("by_species", []):
+            kinds += (f" | s{row['species']}: plain {row['plain_ms'] or 0:.2f} fresh {row['fresh_plain_ms'] or 0:.2f}"
+                      f" count {row['count_ms'] or 0:.2f} sort {row['sort_ms'] or 0:.2f}")
         print(f"{n}: value {r['value']:.4g} ms/step {r['ms_per_step']:.2f} solve {r['poisson_ms_per_step']:.2f} "
               f"push frac {r['roofline']['frac']:.3f} {kinds}")
     top = set()
