@@ -1330,7 +1330,15 @@ struct PushArgs {
 };
 // phase timestamp of the block (thread 0, s_memrealtime at 100 MHz)
 #define PUSH_TS(slot) \
-	if (a.tstamp && threadIdx.x == 0) a.tstamp[(long)chunk * 8 + (slot)] = wall_clock64()
+	if (a.tstamp && threadIdx.x == 0) a.tstamp[(long)chunk * 8 + (slot)] = tsub = wall_clock64()
+// sub-phase of the sorting push since the last PUSH_TS / PUSH_SUB, summed over
+// the blocks into diag[k] (trace mode)
+#define PUSH_SUB(k)                                                           \
+	if (a.tstamp && threadIdx.x == 0) {                                       \
+		const unsigned long long now = wall_clock64();                        \
+		atomicAdd(&a.diag[k], now - tsub);                                    \
+		tsub = now;                                                           \
+	}
 
 // same-cell groups of at least kPushGroupMin lanes (at most kPushGroups of
 // them per wave and item) are summed across the wave before the LDS add
@@ -1771,7 +1779,6 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	constexpr int kEL = KICK ? EC * ND : 1, kST = SORT ? 2 * kPushChunk : 1;
 	__shared__ __attribute__((aligned(16))) double eLs[kEL > kST ? kEL : kST];
 	double *const eL = eLs;
-	__shared__ int cntIn[SORT ? kInCellCap : 1];
 	__shared__ int cntOut[kOutCellCap];
 	__shared__ int red[3 * 3 * NW];
 	__shared__ int cbox[9];
@@ -1780,7 +1787,6 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	__shared__ int wmov[NW];
 	// sorted output staged in slot order so that each cell's run is written
 	// with consecutive lanes (one component at a time)
-	__shared__ int locStart[SORT ? kInCellCap : 1];
 	__shared__ int rlL[SORT ? kPushChunk : 1];
 	__shared__ int gdst[SORT ? kPushChunk : 1];
 	double *const stage = eLs;
@@ -1822,6 +1828,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 		al = al && !((reinterpret_cast<unsigned long>(a.xi[d]) | reinterpret_cast<unsigned long>(a.vi[d]) |
 		              reinterpret_cast<unsigned long>(a.xo[d]) | reinterpret_cast<unsigned long>(a.vo[d])) & 15);
 
+	unsigned long long tsub = 0;  // (trace mode: thread 0's last timestamp)
 	PUSH_TS(0);
 	// ---- phase A: load every item, cell box of the input positions (periodic
 	// images nearest to the cell of the block's first item)
@@ -1921,6 +1928,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	// wrapped particles) take the global path.
 	const Box eB = (KICK && !empty) ? make_box(clo, chi, cmid, 0, 1, ND, EC) : Box{{0, 0, 0}, {1, 1, 1}, 0};
 	const Box rB = !empty ? make_box(clo, chi, cmid, 1, 2, ND, RC) : Box{{0, 0, 0}, {1, 1, 1}, 0};
+	// (the sorting push's cell box: the core of its brick box ib below)
 	const Box iB = (SORT && !empty) ? make_box(clo, chi, cmid, 0, 0, ND, kInCellCap) : Box{{0, 0, 0}, {1, 1, 1}, 0};
 	// the sorting push reserves per brick from the cursor of the brick's
 	// first cell, so the counting push counts per brick (at its first key):
@@ -1930,9 +1938,8 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	const Box oB = (a.cntNext && !empty) ? make_box(clo, chi, cmid, 1, 1, ND, 16 * kOutCellCap) : Box{{0, 0, 0}, {1, 1, 1}, 0};
 	BrickBox obb = (a.cntNext && !empty) ? make_brick_box<ND>(a.tg, oB) : BrickBox{{0, 0, 0}, {1, 1, 1}, 0};
 	if (obb.vol > kOutCellCap) obb.vol = 0;
-	// sorting push: the items of the cell box iB are ranked by cell, the
-	// others inside the wide brick box ib by brick (one run of each brick per
-	// block, the brick's own items first); only items outside both take a
+	// sorting push: the items inside the wide brick box ib are ranked by
+	// brick (one run of each brick per block); only items outside it take a
 	// global slot one by one.  The brick counters live in cntOut, which a
 	// sorting push does not use (it never counts).
 	const BrickBox ib = (SORT && !empty)
@@ -1950,8 +1957,6 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	while (nCopy < PINC_PUSH_COPIES && 2 * nCopy * rStride <= RL) nCopy *= 2;
 	const int myCopy = (lane & (nCopy - 1)) * rStride;
 	for (int t = threadIdx.x; t < (PINC_PUSH_COPIES ? nCopy * rStride : rB.vol); t += kPushThreads) rhoL[t] = 0.0;
-	if (SORT)
-		for (int t = threadIdx.x; t < iB.vol; t += kPushThreads) cntIn[t] = 0;
 	for (int t = threadIdx.x; t < (SORT ? kInCellCap : obb.vol); t += kPushThreads) cntOut[t] = 0;
 	if (KICK && !(PINC_PUSH_SKIP & 2)) {
 		for (int t = threadIdx.x; t < eB.vol; t += kPushThreads) {
@@ -1977,40 +1982,38 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	}
 	__syncthreads();
 
-	int resBase = 0;      // sorting push: this thread's brick reservation
-	bool resCell = false;  // sorting push: cell threadIdx.x of iB has items
+	int resBase = 0;  // sorting push: this thread's brick reservation
 	PUSH_TS(2);
-	// ---- phase C (sorted output): rank of every item inside its input cell,
-	// and one global reservation per input cell of the block.  Per item, in
-	// LDS (the sort push is tight on VGPRs): rank in its cell << 8 | box cell,
-	// or ~global slot for an item outside the box.
+	// ---- phase C (sorted output): rank of every item inside its brick's run,
+	// and one global reservation per brick of the block.  Per item, in LDS
+	// (the sort push is tight on VGPRs): rank << 8 | brick of ib, or ~global
+	// slot for an item outside ib.  A brick's run holds its cells in the order
+	// the items reach the counter: a wave instruction's same-cell lanes stay
+	// together, so a thread's consecutive output particles mostly share a cell
+	// (round 4: ranking by cell inside each brick first cost a pass and two
+	// barriers; C4 electron sorting push 33.9 -> 32.0 ms, the plain pushes
+	// after it +1 %).
 	if (SORT) {
-		static_assert(kInCellCap <= 256 && kPushChunk <= (1 << 22), "rank/cell packing");
-		// per item: rank << 9 | cell of iB, rank << 9 | 256 | brick of ib, or
-		// ~global slot (outside both: wave-aggregated)
+		static_assert(kInCellCap <= 256 && kPushChunk <= (1 << 23), "rank/brick packing");
 		int rl[kPushItems];
 #pragma unroll
 		for (int k = 0; k < kPushItems; k++) {
-			int lc = -1, lb = -1;
 			int c[3] = {0, 0, 0};
 #pragma unroll
 			for (int d = 0; d < ND; d++) c[d] = (int)p[k][d];
 			const bool ok = (valid >> k) & 1u;
-			if (ok && iB.inside(c, ND)) lc = iB.index(c, ND);
-			else if (ok) lb = brick_inside<ND>(a.tg, ib, c);
-			// plain LDS atomics: a wave's lanes share a few cells (16-way
-			// same-address conflicts at most for sorted input), cheaper than
-			// aggregating the groups with ballots and shuffles
+			const int lb = ok ? brick_inside<ND>(a.tg, ib, c) : -1;
+			// plain LDS atomics: a wave's lanes share a few bricks (same-address
+			// conflicts), cheaper than aggregating the groups with ballots and
+			// shuffles (C4 electron sorting push 36.2 -> 33.5 ms)
 #if PINC_PUSH_AGG
-			const int rank = lds_agg_add<true>(cntIn, lc < 0 ? 0 : lc, lc >= 0);
-			const int rankB = lds_agg_add<true>(bCnt, lb < 0 ? 0 : lb, lb >= 0);
+			const int rank = lds_agg_add<true>(bCnt, lb < 0 ? 0 : lb, lb >= 0);
 #else
-			const int rank = lc >= 0 ? atomicAdd(&cntIn[lc], 1) : 0;
-			const int rankB = lb >= 0 ? atomicAdd(&bCnt[lb], 1) : 0;
+			const int rank = lb >= 0 ? atomicAdd(&bCnt[lb], 1) : 0;
 #endif
-			const bool out = ok && lc < 0 && lb < 0;
+			const bool out = ok && lb < 0;
 			const int g = agg_add(a.cursor, out ? brick_first_key<ND>(a.tg, c) : 0, out);
-			rl[k] = lc >= 0 ? (rank << 9 | lc) : lb >= 0 ? (rankB << 9 | 256 | lb) : (ok ? ~g : -1);
+			rl[k] = lb >= 0 ? (rank << 8 | lb) : (ok ? ~g : -1);
 		}
 #pragma unroll
 		for (int k = 0; k < kPushItems; k++) rlL[k * kPushThreads + threadIdx.x] = rl[k];
@@ -2022,21 +2025,10 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 			if (lane == 0 && no) atomicAdd(&a.diag[0], (unsigned long long)no);
 		}
 		__syncthreads();
+		PUSH_SUB(4);
 		static_assert(kInCellCap <= kPushThreads, "one reservation per thread");
-		// one global reservation per brick of ib: each cell of iB takes its
-		// place inside its brick's block run (LDS atomic, after the brick's
-		// own items), each brick one range of its first cell's cursor
-		int m = 0, lb = 0, bo = 0;
-		if ((int)threadIdx.x < iB.vol) {
-			m = cntIn[threadIdx.x];
-			if (m) {
-				int c[3] = {0, 0, 0};
-				iB.coords(threadIdx.x, c, ND);
-				lb = brick_inside<ND>(a.tg, ib, c);  // (ib contains iB's bricks)
-				bo = atomicAdd(&bCnt[lb], m);
-			}
-		}
-		__syncthreads();
+		// one global reservation per brick of ib, one range of its first
+		// cell's cursor
 		const int bm = (int)threadIdx.x < ib.vol ? bCnt[threadIdx.x] : 0;
 		// the global reservation's result is first needed by the stores after
 		// the kick: its round trip overlaps the kick (resBase, one VGPR)
@@ -2053,14 +2045,6 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 			for (int w = 0; w < NW; w++) t += red[w];
 			cbox[0] = t;  // items in the boxes (the box bounds are in registers by now)
 		}
-		__syncthreads();
-		// each cell of iB: block slot of its run; its brick and offset in the
-		// brick's run for the global start (after the kick)
-		if (m) {
-			cntIn[threadIdx.x] = lb << 16 | bo;
-			locStart[threadIdx.x] = bCnt[lb] + bo;
-		}
-		resCell = m != 0;
 		__syncthreads();
 	}
 
@@ -2261,7 +2245,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 		if (SORT) {
 			// flag staged by block slot (outside the box: by item position)
 			const int r = rlL[k * kPushThreads + threadIdx.x];
-			const int t = r >= 0 ? ((r & 256) ? bCnt[r & 255] : locStart[r & 255]) + (r >> 9)
+			const int t = r >= 0 ? bCnt[r & 255] + (r >> 8)
 			                     : kPushChunk + k * kPushThreads + (int)threadIdx.x;
 			stageF[t] = (unsigned char)ne;
 		}
@@ -2301,14 +2285,8 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	}
 	PUSH_TS(4);
 	if (SORT) {
-		// global start of each cell run of iB: its brick's reservation + its
-		// offset in the brick's run
+		// global start of each brick's run (the reservation made before the kick)
 		if ((int)threadIdx.x < ib.vol) bBase[threadIdx.x] = resBase;
-		__syncthreads();
-		if (resCell) {
-			const int pk = cntIn[threadIdx.x];
-			cntIn[threadIdx.x] = bBase[pk >> 16] + (pk & 0xffff);
-		}
 		__syncthreads();
 		{
 			// items in the box: block slots 0..nv-1, stored through LDS;
@@ -2322,10 +2300,9 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 				const long i = item(k);
 				const int r = rlL[k * kPushThreads + threadIdx.x];
 				if (r >= 0) {
-					const int l = r & 255, rank = r >> 9;
-					const bool br = r & 256;
-					slot[k] = (br ? bCnt[l] : locStart[l]) + rank;
-					const int o = (br ? bBase[l] : cntIn[l]) + rank;
+					const int l = r & 255, rank = r >> 8;
+					slot[k] = bCnt[l] + rank;
+					const int o = bBase[l] + rank;
 					gdst[slot[k]] = o;
 					a.perm[i] = o;
 				} else {
@@ -2342,12 +2319,14 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 				}
 			}
 			__syncthreads();
+			PUSH_SUB(5);
 			for (int t = threadIdx.x; t < nv; t += kPushThreads) {
 				const int o = gdst[t];
 				const int f = stageF[t];
 				a.flags[o] = (unsigned char)f;
 				if (f != a.center) atomicAdd(&a.chunkCount[o / PINC_CHUNK], 1);
 			}
+			PUSH_SUB(6);
 			// components c = 0 .. 2 ND - 1 (positions, then velocities), two
 			// per round: half the barriers of one at a time
 			auto comp = [&](int k, int c) -> double { return c < ND ? p[k][c] : vv[k][c - ND]; };
@@ -2383,8 +2362,9 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 #pragma unroll
 			for (int d = 0; d < ND; d++) c[d] = (int)p[k][d];
 			const int lb = mine ? brick_inside<ND>(a.tg, obb, c) : -1;
-			// (aggregated: plain atomics here cost the plain instance, which
-			// carries this code behind a runtime test, 52 spilled VGPRs)
+			// (aggregated: plain atomics here, or after the deposit, cost the
+			// plain instance, which carries this code behind a runtime test,
+			// 48-52 spilled VGPRs; aggregated after the deposit: same time)
 			lds_agg_add<false>(cntOut, lb < 0 ? 0 : lb, lb >= 0);
 			if (mine && lb < 0) atomicAdd(&a.cntNext[brick_first_key<ND>(a.tg, c)], 1);
 		}

@@ -242,7 +242,7 @@ static int cmp_double(const void *x, const void *y) {
 static void push_phase_report(const unsigned long long *dts, const unsigned long long *ddiag, int nb, int s, int sort,
                               int count) {
 	unsigned long long *t = malloc((size_t)nb * 8 * sizeof(*t));
-	unsigned long long dg[4];
+	unsigned long long dg[8];
 	pinc_check(pinc_hip_d2h(t, dts, (size_t)nb * 8 * sizeof(*t), g_pinc.stream), "push timestamps");
 	pinc_check(pinc_hip_d2h(dg, ddiag, sizeof(dg), g_pinc.stream), "push diagnostics");
 	double ph[7] = {0};
@@ -259,6 +259,11 @@ static void push_phase_report(const unsigned long long *dts, const unsigned long
 	        count ? " count" : "", (t1 - t0) * 1e-5, ph[0] / nb * 1e-2, ph[1] / nb * 1e-2, ph[2] / nb * 1e-2,
 	        ph[3] / nb * 1e-2, ph[4] / nb * 1e-2, ph[5] / nb * 1e-2, ph[6] / nb * 1e-2, (double)dg[0] / nb,
 	        (double)dg[1] / nb, (double)dg[3] / nb, (double)dg[2] / nb);
+	if (sort)
+		fprintf(stderr, "[pinc]   sort sub-phases us per block: rank loop %.2f (reservation %.2f), out-of-box and "
+		        "slot stores %.2f, flags %.2f (staged stores %.2f)\n", dg[4] / (double)nb * 1e-2,
+		        ph[2] / nb * 1e-2 - dg[4] / (double)nb * 1e-2, dg[5] / (double)nb * 1e-2, dg[6] / (double)nb * 1e-2,
+		        ph[4] / nb * 1e-2 - (dg[5] + dg[6]) / (double)nb * 1e-2);
 	/* per XCD (the push deals chunks [x q + min(x, r), ...) to XCD x): span
 	 * from its first block's start to its last block's end, and the mean
 	 * number of its blocks between their first and last timestamp */
@@ -432,8 +437,8 @@ static int push_all(Population *pop, Grid *E, double *const *xout) {
 			/* 8 timestamps per push block (pinc_hip_push_chunk particles), then
 			 * the diagnostic counters */
 			const long nbk = np / pinc_hip_push_chunk() + 1;
-			pinc_check(pinc_hip_malloc((void **)&ts, (nbk * 8 + 4) * sizeof(*ts)), "push timestamps");
-			pinc_check(pinc_hip_memset(ts + nbk * 8, 0, 4 * sizeof(*ts), g_pinc.stream), "push diagnostics");
+			pinc_check(pinc_hip_malloc((void **)&ts, (nbk * 8 + 8) * sizeof(*ts)), "push timestamps");
+			pinc_check(pinc_hip_memset(ts + nbk * 8, 0, 8 * sizeof(*ts), g_pinc.stream), "push diagnostics");
 			a.tstamp = ts;
 			a.diag = ts + nbk * 8;
 		}

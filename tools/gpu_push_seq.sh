@@ -18,5 +18,5 @@ for V in "${libs[@]}"; do
   python3 tools/trace_summary.py $O/prof_$n 24 > $O/${n}_seq.txt && rm -rf $O/prof_$n
   python3 -c "
 import json; r=json.load(open('$O/$n.json'))
-print('$n value %.4g ms/step %.2f solve %.2f push %.2f' % (r['value'], r['ms_per_step'], r['poisson_ms_per_step'], r['push_deposit_ms_per_step']), {k: round(v['mean_launch_ms'], 2) for k, v in r['push_kinds'].items()})"
+print('$n value %.4g ms/step %.2f solve %.2f push %.2f' % (r['value'], r['ms_per_step'], r['poisson_ms_per_step'], r['push_deposit_ms_per_step']), {k: round(v['mean_launch_ms'], 2) for k, v in r['push_kinds'].items() if isinstance(v, dict)})"
 done
