@@ -1389,6 +1389,11 @@ constexpr int kPushGroupMin = PINC_PUSH_GROUP_MIN;
 constexpr int kRhoLds = PINC_PUSH_COPIES ? PINC_PUSH_RHO_LDS : 1024;
 
 constexpr int kPushGroups = PINC_PUSH_GROUPS;
+// 1: the sorting push stages its output through LDS in block-slot order;
+// 0: every item is stored straight to its slot
+#ifndef PINC_PUSH_SORT_STAGE
+#define PINC_PUSH_SORT_STAGE 0
+#endif
 // 1: the sorting push ranks its items with wave-aggregated LDS atomics
 // (lds_agg_add, round 3); 0: plain LDS atomics (measured at C4: electron
 // sorting push 36.2 -> 33.5 ms)
@@ -1498,10 +1503,11 @@ __device__ __forceinline__ void node_pair(const Geo32 &G, int d, int j, int &o0,
 		o0 = d ? mul24(j, G.stride[d]) : j;
 		o1 = o0 + G.stride[d];
 	} else {
-		// wrap_pad of j and j+1 (padded coordinates 0..T+1)
+		// wrap_pad of j and j+1 (padded coordinates 0..T+1; a periodic image
+		// of the block's boxes may lie one period either side, -T < j < 2T)
 		int s0 = j - 1, s1 = j;
 		s0 = s0 < 0 ? s0 + G.T[d] : (s0 >= G.T[d] ? s0 - G.T[d] : s0);
-		s1 = s1 >= G.T[d] ? s1 - G.T[d] : s1;
+		s1 = s1 < 0 ? s1 + G.T[d] : (s1 >= G.T[d] ? s1 - G.T[d] : s1);
 		o0 = d ? mul24(s0, G.stride[d]) : s0;
 		o1 = d ? mul24(s1, G.stride[d]) : s1;
 	}
@@ -1541,8 +1547,8 @@ __device__ __forceinline__ Images make_images(const Geo32 &G, int wrapMask, cons
 
 // LDS capacities of the push: E nodes (pre-move cells + 1), charge nodes
 // (post-move cells + 1), input cells and output cells of the sort counters
-// (the sorting push, whose LDS also holds the rank and staging arrays, keeps
-// the smaller boxes).  The unsorted push's boxes take a chunk that straddles
+// (the sorting push, whose LDS also holds the rank array -- and with
+// PINC_PUSH_SORT_STAGE the staging arrays -- keeps the smaller charge box).  The unsorted push's boxes take a chunk that straddles
 // two tiles (8 x 4 x 4 cells) after a step of motion ((10 x 6 x 6 cells):
 // 539 E nodes, 1053 charge nodes); with 384 and 1024 such chunks -- a
 // quarter of them -- gathered E and added charge through global memory.
@@ -1552,7 +1558,7 @@ constexpr int kRhoBoxCap = 1024;
 #endif
 constexpr int kEBoxCapPlain = PINC_PUSH_EBOX;
 #ifndef PINC_PUSH_SORT_EBOX
-#define PINC_PUSH_SORT_EBOX 704
+#define PINC_PUSH_SORT_EBOX (PINC_PUSH_SORT_STAGE ? 704 : PINC_PUSH_EBOX)
 #endif
 constexpr int kEBoxCapSort = PINC_PUSH_SORT_EBOX;
 constexpr int kInCellCap = 256;
@@ -1772,11 +1778,10 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	// corner) and E_z at eL[2 cap + t], else value-major
 	constexpr int EC = SORT ? kEBoxCapSort : kEBoxCapPlain;  // E box capacity (nodes)
 	constexpr int RC = SORT ? kRhoBoxCap : RL;              // charge box capacity (nodes)
-	// the sorting push stages its sorted output in the same LDS once the
-	// kick has read E (a barrier separates the last E read from the first
-	// staged write)
-	// (the sorted output is staged two components at a time)
-	constexpr int kEL = KICK ? EC * ND : 1, kST = SORT ? 2 * kPushChunk : 1;
+	// PINC_PUSH_SORT_STAGE: the sorting push stages its sorted output in the
+	// same LDS once the kick has read E (a barrier separates the last E read
+	// from the first staged write), two components at a time
+	constexpr int kEL = KICK ? EC * ND : 1, kST = (SORT && PINC_PUSH_SORT_STAGE) ? 2 * kPushChunk : 1;
 	__shared__ __attribute__((aligned(16))) double eLs[kEL > kST ? kEL : kST];
 	double *const eL = eLs;
 	__shared__ int cntOut[kOutCellCap];
@@ -1788,9 +1793,9 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	// sorted output staged in slot order so that each cell's run is written
 	// with consecutive lanes (one component at a time)
 	__shared__ int rlL[SORT ? kPushChunk : 1];
-	__shared__ int gdst[SORT ? kPushChunk : 1];
+	__shared__ int gdst[(SORT && PINC_PUSH_SORT_STAGE) ? kPushChunk : 1];
 	double *const stage = eLs;
-	__shared__ unsigned char stageF[SORT ? 2 * kPushChunk : 1];
+	__shared__ unsigned char stageF[SORT ? (PINC_PUSH_SORT_STAGE ? 2 : 1) * kPushChunk : 1];
 	const Geo32 G = make_geo32(a.g);
 	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 	// chunk of this block.  PINC_PUSH_XCD: consecutive chunks (the same cell
@@ -2033,6 +2038,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 		// the global reservation's result is first needed by the stores after
 		// the kick: its round trip overlaps the kick (resBase, one VGPR)
 		if (bm) resBase = atomicAdd(&a.cursor[brick_key<ND>(a.tg, ib, threadIdx.x)], bm);
+#if PINC_PUSH_SORT_STAGE
 		// block slot of each brick's run: exclusive scan of the brick counts
 		const int inc = wave_incl_scan(bm);
 		if (lane == 63) red[wv] = inc;
@@ -2046,6 +2052,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 			cbox[0] = t;  // items in the boxes (the box bounds are in registers by now)
 		}
 		__syncthreads();
+#endif
 	}
 
 	PUSH_TS(3);
@@ -2243,11 +2250,15 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 			}
 		}
 		if (SORT) {
+#if PINC_PUSH_SORT_STAGE
 			// flag staged by block slot (outside the box: by item position)
 			const int r = rlL[k * kPushThreads + threadIdx.x];
 			const int t = r >= 0 ? bCnt[r & 255] + (r >> 8)
 			                     : kPushChunk + k * kPushThreads + (int)threadIdx.x;
 			stageF[t] = (unsigned char)ne;
+#else
+			stageF[k * kPushThreads + threadIdx.x] = (unsigned char)ne;  // by item
+#endif
 		}
 		if (!SORT) a.flags[i] = (unsigned char)ne;
 		if (ne != a.center) {
@@ -2288,6 +2299,29 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 		// global start of each brick's run (the reservation made before the kick)
 		if ((int)threadIdx.x < ib.vol) bBase[threadIdx.x] = resBase;
 		__syncthreads();
+#if !PINC_PUSH_SORT_STAGE
+		// every item straight to its slot: the lanes of a wave instruction
+		// that share a brick took consecutive ranks from its LDS counter, so
+		// their stores cover one contiguous range (coalesced like the plain
+		// push's) and no staging through LDS is needed
+#pragma unroll
+		for (int k = 0; k < kPushItems; k++) {
+			if (!((valid >> k) & 1u)) continue;
+			const long i = item(k);
+			const int r = rlL[k * kPushThreads + threadIdx.x];
+			const long o = r >= 0 ? (long)bBase[r & 255] + (r >> 8) : (long)~r;
+#pragma unroll
+			for (int d = 0; d < ND; d++) {
+				a.xo[d][o] = p[k][d];
+				a.vo[d][o] = vv[k][d];
+			}
+			const int f = stageF[k * kPushThreads + threadIdx.x];
+			a.flags[o] = (unsigned char)f;
+			a.perm[i] = (int)o;
+			if (f != a.center) atomicAdd(&a.chunkCount[o / PINC_CHUNK], 1);
+		}
+		PUSH_SUB(5);
+#else
 		{
 			// items in the box: block slots 0..nv-1, stored through LDS;
 			// the others straight to their global slot
@@ -2351,6 +2385,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 				}
 			}
 		}
+#endif
 	}
 	PUSH_TS(5);
 	if (a.cntNext) {
@@ -2439,6 +2474,14 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 		}
 		cic_weights<ND, V3D>(dec, comp, w);
 		literal_ghost_weights<ND>(a.g, j, w);
+		// the cell's periodic image nearest the block's reference cell (the
+		// boxes' coordinates): a particle that wrapped deposits into the LDS
+		// box at its image nodes, which the flush maps to the same storage
+		// (x, y wrapped; slab ghost planes when the slab dimension wraps,
+		// folded by the halo add as every ghost deposit) instead of adding
+		// its eight weights to memory
+#pragma unroll
+		for (int d = 0; d < ND; d++) j[d] = img(d, j[d]);
 		return kk;
 	};
 	// one wave pass: lanes sharing a cell (up to kPushGroups groups of at
