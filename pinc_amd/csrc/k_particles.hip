@@ -1389,11 +1389,6 @@ constexpr int kPushGroupMin = PINC_PUSH_GROUP_MIN;
 constexpr int kRhoLds = PINC_PUSH_COPIES ? PINC_PUSH_RHO_LDS : 1024;
 
 constexpr int kPushGroups = PINC_PUSH_GROUPS;
-// 1: the sorting push stages its output through LDS in block-slot order;
-// 0: every item is stored straight to its slot
-#ifndef PINC_PUSH_SORT_STAGE
-#define PINC_PUSH_SORT_STAGE 0
-#endif
 // 1: the sorting push ranks its items with wave-aggregated LDS atomics
 // (lds_agg_add, round 3); 0: plain LDS atomics (measured at C4: electron
 // sorting push 36.2 -> 33.5 ms)
@@ -1547,8 +1542,8 @@ __device__ __forceinline__ Images make_images(const Geo32 &G, int wrapMask, cons
 
 // LDS capacities of the push: E nodes (pre-move cells + 1), charge nodes
 // (post-move cells + 1), input cells and output cells of the sort counters
-// (the sorting push, whose LDS also holds the rank array -- and with
-// PINC_PUSH_SORT_STAGE the staging arrays -- keeps the smaller charge box).  The unsorted push's boxes take a chunk that straddles
+// (the sorting push, whose LDS also holds the rank array, keeps the smaller
+// charge box).  The unsorted push's boxes take a chunk that straddles
 // two tiles (8 x 4 x 4 cells) after a step of motion ((10 x 6 x 6 cells):
 // 539 E nodes, 1053 charge nodes); with 384 and 1024 such chunks -- a
 // quarter of them -- gathered E and added charge through global memory.
@@ -1558,7 +1553,7 @@ constexpr int kRhoBoxCap = 1024;
 #endif
 constexpr int kEBoxCapPlain = PINC_PUSH_EBOX;
 #ifndef PINC_PUSH_SORT_EBOX
-#define PINC_PUSH_SORT_EBOX (PINC_PUSH_SORT_STAGE ? 704 : PINC_PUSH_EBOX)
+#define PINC_PUSH_SORT_EBOX PINC_PUSH_EBOX
 #endif
 constexpr int kEBoxCapSort = PINC_PUSH_SORT_EBOX;
 constexpr int kInCellCap = 256;
@@ -1778,11 +1773,8 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	// corner) and E_z at eL[2 cap + t], else value-major
 	constexpr int EC = SORT ? kEBoxCapSort : kEBoxCapPlain;  // E box capacity (nodes)
 	constexpr int RC = SORT ? kRhoBoxCap : RL;              // charge box capacity (nodes)
-	// PINC_PUSH_SORT_STAGE: the sorting push stages its sorted output in the
-	// same LDS once the kick has read E (a barrier separates the last E read
-	// from the first staged write), two components at a time
-	constexpr int kEL = KICK ? EC * ND : 1, kST = (SORT && PINC_PUSH_SORT_STAGE) ? 2 * kPushChunk : 1;
-	__shared__ __attribute__((aligned(16))) double eLs[kEL > kST ? kEL : kST];
+	constexpr int kEL = KICK ? EC * ND : 1;
+	__shared__ __attribute__((aligned(16))) double eLs[kEL];
 	double *const eL = eLs;
 	__shared__ int cntOut[kOutCellCap];
 	__shared__ int red[3 * 3 * NW];
@@ -1790,12 +1782,9 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	__shared__ double kered[NW];
 	__shared__ int wcnt[NW];
 	__shared__ int wmov[NW];
-	// sorted output staged in slot order so that each cell's run is written
-	// with consecutive lanes (one component at a time)
+	// sorting push, per item: its rank code (phase C) and its flag (phase D)
 	__shared__ int rlL[SORT ? kPushChunk : 1];
-	__shared__ int gdst[(SORT && PINC_PUSH_SORT_STAGE) ? kPushChunk : 1];
-	double *const stage = eLs;
-	__shared__ unsigned char stageF[SORT ? (PINC_PUSH_SORT_STAGE ? 2 : 1) * kPushChunk : 1];
+	__shared__ unsigned char stageF[SORT ? kPushChunk : 1];
 	const Geo32 G = make_geo32(a.g);
 	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 	// chunk of this block.  PINC_PUSH_XCD: consecutive chunks (the same cell
@@ -2038,21 +2027,6 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 		// the global reservation's result is first needed by the stores after
 		// the kick: its round trip overlaps the kick (resBase, one VGPR)
 		if (bm) resBase = atomicAdd(&a.cursor[brick_key<ND>(a.tg, ib, threadIdx.x)], bm);
-#if PINC_PUSH_SORT_STAGE
-		// block slot of each brick's run: exclusive scan of the brick counts
-		const int inc = wave_incl_scan(bm);
-		if (lane == 63) red[wv] = inc;
-		__syncthreads();
-		int off = 0;
-		for (int w = 0; w < wv; w++) off += red[w];
-		if ((int)threadIdx.x < ib.vol) bCnt[threadIdx.x] = off + inc - bm;
-		if (threadIdx.x == 0) {
-			int t = 0;
-			for (int w = 0; w < NW; w++) t += red[w];
-			cbox[0] = t;  // items in the boxes (the box bounds are in registers by now)
-		}
-		__syncthreads();
-#endif
 	}
 
 	PUSH_TS(3);
@@ -2250,15 +2224,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 			}
 		}
 		if (SORT) {
-#if PINC_PUSH_SORT_STAGE
-			// flag staged by block slot (outside the box: by item position)
-			const int r = rlL[k * kPushThreads + threadIdx.x];
-			const int t = r >= 0 ? bCnt[r & 255] + (r >> 8)
-			                     : kPushChunk + k * kPushThreads + (int)threadIdx.x;
-			stageF[t] = (unsigned char)ne;
-#else
 			stageF[k * kPushThreads + threadIdx.x] = (unsigned char)ne;  // by item
-#endif
 		}
 		if (!SORT) a.flags[i] = (unsigned char)ne;
 		if (ne != a.center) {
@@ -2299,7 +2265,6 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 		// global start of each brick's run (the reservation made before the kick)
 		if ((int)threadIdx.x < ib.vol) bBase[threadIdx.x] = resBase;
 		__syncthreads();
-#if !PINC_PUSH_SORT_STAGE
 		// every item straight to its slot: the lanes of a wave instruction
 		// that share a brick took consecutive ranks from its LDS counter, so
 		// their stores cover one contiguous range (coalesced like the plain
@@ -2320,72 +2285,6 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 			a.perm[i] = (int)o;
 			if (f != a.center) atomicAdd(&a.chunkCount[o / PINC_CHUNK], 1);
 		}
-		PUSH_SUB(5);
-#else
-		{
-			// items in the box: block slots 0..nv-1, stored through LDS;
-			// the others straight to their global slot
-			const int nv = __builtin_amdgcn_readfirstlane(cbox[0]);
-			int slot[kPushItems];
-#pragma unroll
-			for (int k = 0; k < kPushItems; k++) {
-				slot[k] = -1;
-				if (!((valid >> k) & 1u)) continue;
-				const long i = item(k);
-				const int r = rlL[k * kPushThreads + threadIdx.x];
-				if (r >= 0) {
-					const int l = r & 255, rank = r >> 8;
-					slot[k] = bCnt[l] + rank;
-					const int o = bBase[l] + rank;
-					gdst[slot[k]] = o;
-					a.perm[i] = o;
-				} else {
-					const long o = ~r;
-#pragma unroll
-					for (int d = 0; d < ND; d++) {
-						a.xo[d][o] = p[k][d];
-						a.vo[d][o] = vv[k][d];
-					}
-					const int f = stageF[kPushChunk + k * kPushThreads + threadIdx.x];
-					a.flags[o] = (unsigned char)f;
-					a.perm[i] = (int)o;
-					if (f != a.center) atomicAdd(&a.chunkCount[o / PINC_CHUNK], 1);
-				}
-			}
-			__syncthreads();
-			PUSH_SUB(5);
-			for (int t = threadIdx.x; t < nv; t += kPushThreads) {
-				const int o = gdst[t];
-				const int f = stageF[t];
-				a.flags[o] = (unsigned char)f;
-				if (f != a.center) atomicAdd(&a.chunkCount[o / PINC_CHUNK], 1);
-			}
-			PUSH_SUB(6);
-			// components c = 0 .. 2 ND - 1 (positions, then velocities), two
-			// per round: half the barriers of one at a time
-			auto comp = [&](int k, int c) -> double { return c < ND ? p[k][c] : vv[k][c - ND]; };
-			auto dst = [&](int c) -> double * { return c < ND ? a.xo[c] : a.vo[c - ND]; };
-#pragma unroll
-			for (int c = 0; c < 2 * ND; c += 2) {
-				// (the first round's writes follow the barrier after the kick's
-				// last E read and the slot assignment above)
-				if (c) __syncthreads();
-#pragma unroll
-				for (int k = 0; k < kPushItems; k++)
-					if (slot[k] >= 0) {
-						stage[slot[k]] = comp(k, c);
-						stage[kPushChunk + slot[k]] = comp(k, c + 1);
-					}
-				__syncthreads();
-				double *const o0 = dst(c), *const o1 = dst(c + 1);
-				for (int t = threadIdx.x; t < nv; t += kPushThreads) {
-					const int g = gdst[t];
-					__builtin_nontemporal_store(stage[t], o0 + g);
-					__builtin_nontemporal_store(stage[kPushChunk + t], o1 + g);
-				}
-			}
-		}
-#endif
 	}
 	PUSH_TS(5);
 	if (a.cntNext) {

@@ -260,10 +260,8 @@ static void push_phase_report(const unsigned long long *dts, const unsigned long
 	        ph[3] / nb * 1e-2, ph[4] / nb * 1e-2, ph[5] / nb * 1e-2, ph[6] / nb * 1e-2, (double)dg[0] / nb,
 	        (double)dg[1] / nb, (double)dg[3] / nb, (double)dg[2] / nb);
 	if (sort)
-		fprintf(stderr, "[pinc]   sort sub-phases us per block: rank loop %.2f (reservation %.2f), out-of-box and "
-		        "slot stores %.2f, flags %.2f (staged stores %.2f)\n", dg[4] / (double)nb * 1e-2,
-		        ph[2] / nb * 1e-2 - dg[4] / (double)nb * 1e-2, dg[5] / (double)nb * 1e-2, dg[6] / (double)nb * 1e-2,
-		        ph[4] / nb * 1e-2 - (dg[5] + dg[6]) / (double)nb * 1e-2);
+		fprintf(stderr, "[pinc]   sort sub-phases us per block: rank loop %.2f, reservation %.2f\n",
+		        dg[4] / (double)nb * 1e-2, ph[2] / nb * 1e-2 - dg[4] / (double)nb * 1e-2);
 	/* per XCD (the push deals chunks [x q + min(x, r), ...) to XCD x): span
 	 * from its first block's start to its last block's end, and the mean
 	 * number of its blocks between their first and last timestamp */
