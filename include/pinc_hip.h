@@ -111,9 +111,10 @@ int pinc_hip_move_classify(pinc_pop_t pop, int s, int doMove, const double *thr,
  *     cursor[key(x_i)]++ (cursor = exclusive scan of the key counts of the
  *     current positions, pinc_hip_count_keys + pinc_hip_scan_keys), its
  *     moved state to xout/vout at that slot (must not alias pop), flags at
- *     that slot, perm[i] = slot; chunkCount counts emigrants per
- *     destination chunk; the keys of the moved particles that
- *     stay are counted into cntNext (zeroed by the caller). */
+ *     that slot, perm[i] = slot if perm is set; chunkCount counts
+ *     emigrants per destination chunk.  Otherwise (cursor == NULL) the keys
+ *     of the moved particles that stay are counted into cntNext if set
+ *     (zeroed by the caller); a sorting push does not count. */
 typedef struct {
 	double *xout[3];
 	double *vout[3];

@@ -1318,7 +1318,7 @@ struct PushArgs {
 	TileGeo tg;
 	int *cursor;
 	int *cntNext;
-	int *perm;           // perm[i] = destination of particle i
+	int *perm;           // perm[i] = destination of particle i (nullable)
 	unsigned long long *moved;  // += particles that stay but changed cell (nullable)
 	unsigned long long *spread;  // += the block's input cell-box volume (nullable)
 	unsigned long long *tstamp;  // 8 phase timestamps per block (diagnostics, nullable)
@@ -1403,8 +1403,14 @@ constexpr int kPushGroups = PINC_PUSH_GROUPS;
 #ifndef PINC_PUSH_WPE
 #define PINC_PUSH_WPE 4
 #endif
+// 2 (default): pieces of PINC_PUSH_XCD_PIECE chunks round-robin over the
+// XCDs (C4: step 55.39 -> 55.07 ms; the contiguous eighths of 1 left the XCD
+// holding the top z tiles 1.2 ms behind the others on the electrons)
 #ifndef PINC_PUSH_XCD
-#define PINC_PUSH_XCD 1
+#define PINC_PUSH_XCD 2
+#endif
+#ifndef PINC_PUSH_XCD_PIECE
+#define PINC_PUSH_XCD_PIECE 64
 #endif
 #ifndef PINC_PUSH_THREADS
 #define PINC_PUSH_THREADS 256
@@ -1793,7 +1799,20 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	// workgroup dispatch), so block b runs on XCD b % 8; the map is a
 	// bijection for any grid size and only a placement hint, never needed
 	// for correctness.
-#if PINC_PUSH_XCD
+#if PINC_PUSH_XCD == 2
+	// pieces of PINC_PUSH_XCD_PIECE consecutive chunks dealt round-robin over
+	// the XCDs (the tail beyond whole rounds in order): every XCD gets pieces
+	// from every part of the array, e.g. both z faces' tiles, where wrapped
+	// particles make blocks slower
+	const unsigned chunk = [] {
+		constexpr unsigned P = PINC_PUSH_XCD_PIECE;
+		const unsigned nb = gridDim.x, b = blockIdx.x;
+		const unsigned F = nb / (8u * P) * (8u * P);
+		if (b >= F) return b;
+		const unsigned x = b & 7u, y = b >> 3;
+		return ((y / P) * 8u + x) * P + (y % P);
+	}();
+#elif PINC_PUSH_XCD
 	const unsigned chunk = [] {
 		const unsigned nb = gridDim.x, x = blockIdx.x & 7u, y = blockIdx.x >> 3;
 		const unsigned q = nb >> 3, r = nb & 7u;
@@ -2282,7 +2301,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 			}
 			const int f = stageF[k * kPushThreads + threadIdx.x];
 			a.flags[o] = (unsigned char)f;
-			a.perm[i] = (int)o;
+			if (a.perm) a.perm[i] = (int)o;
 			if (f != a.center) atomicAdd(&a.chunkCount[o / PINC_CHUNK], 1);
 		}
 	}
@@ -3010,7 +3029,6 @@ extern "C" int pinc_hip_push(pinc_pop_t pop, int s, pinc_geom_t g, const pinc_pu
 	int nd = pop.nd;
 	if (nd != g.nd) return set_error(hipErrorInvalidValue, "push: population and grid dimensions differ");
 	const bool sort = args->cursor != nullptr;
-	if (sort && (args->perm == nullptr)) return set_error(hipErrorInvalidValue, "push: sorted output needs perm");
 	if (sort && n > 2147483647L) return set_error(hipErrorInvalidValue, "push: species too large for int slots");
 	long nodes = 1;
 	for (int d = 0; d < nd; d++) nodes *= (d == nd - 1) ? (long)g.nloc + 2 : (long)g.T[d];

@@ -101,8 +101,8 @@ struct PincDevPop {
 	int *keyWork[PINC_MAX_SPECIES];     /* scan scratch */
 	int cntValid[PINC_MAX_SPECIES];
 	int everSorted;                     /* input already in cell order once */
-	int *perm;                          /* slot of each particle after a sorted push */
-	int permId[PINC_MAX_SPECIES];       /* ... identity for species s (left in order: perm not written) */
+	int permId[PINC_MAX_SPECIES];       /* species s left in order by the pending sorting push */
+	Grid *pendingE;                     /* E of the pending push's kick (pinc_pending_vel) */
 	/* adaptive sort schedule (population:sortFraction > 0): a species is
 	 * sorted once the fraction of its particles that left their cell since
 	 * its last sort would pass sortFraction, at most sortMax pushes apart */
@@ -249,7 +249,7 @@ void pinc_pop_flush_host(const Population *pop);
 /* the weight a deposit without the literal factor misses for the second fold
  * of main.c:232 (pinc_pusher.c) */
 /* kicked velocities pending after a sorting push, in the current order */
-void pinc_unsort_vel(const Population *pop, int s, int d, double *dst);
+void pinc_pending_vel(const Population *pop, int s, double *const *dst);
 void pinc_literal_second_fold(const Population *pop, Grid *rho, int order);
 
 /* helpers shared by the host translation units */

@@ -101,7 +101,6 @@ Population *pAlloc(const dictionary *ini) {
 	dv->sorted = dv->tiled && dv->fused &&
 	             (iniHas(ini, "population:sortInPush") ? iniGetInt(ini, "population:sortInPush") : 1);
 	if (dv->sorted) {
-		pinc_check(pinc_hip_malloc((void **)&dv->perm, cap * sizeof(int)), "pAlloc perm");
 		dv->sortFraction = iniHas(ini, "population:sortFraction") ? iniGetDouble(ini, "population:sortFraction") : 0.0;
 		dv->sortMax = iniHas(ini, "population:sortMax") ? iniGetInt(ini, "population:sortMax") : 32;
 		if (dv->sortFraction < 0 || dv->sortMax < 1) msg(ERROR, "population:sortFraction/sortMax out of range");
@@ -227,7 +226,6 @@ void pFree(Population *p) {
 			pinc_hip_free(dv->keyCur[s]);
 			pinc_hip_free(dv->keyWork[s]);
 		}
-		pinc_hip_free(dv->perm);
 		pinc_hip_free(dv->movedCnt);
 		pinc_hip_free(dv->spreadCnt);
 		for (int s = 0; s < PINC_MAX_SPECIES; s++) pinc_hip_free(dv->sortWork[s]);
@@ -407,18 +405,17 @@ void pSyncToHost(Population *p) {
 		if (n <= 0) continue;
 		double *tmp = malloc(n * sizeof(double));
 		double *dtmp = NULL;
-		/* a sorted fused push is pending: the kicked velocities sit in altV in
-		 * slot order; read them back in the current order through perm */
-		if (dv->pending && dv->pendingSorted)
-			pinc_check(pinc_hip_malloc((void **)&dtmp, n * sizeof(double)), "pSyncToHost tmp");
+		/* a sorted fused push is pending: the kicked velocities in the current
+		 * order come from pinc_pending_vel */
+		if (dv->pending && dv->pendingSorted) {
+			pinc_check(pinc_hip_malloc((void **)&dtmp, nd * n * sizeof(double)), "pSyncToHost tmp");
+			double *dst[3] = {dtmp, dtmp + n, dtmp + 2 * n};
+			pinc_pending_vel(p, s, dst);
+		}
 		for (int d = 0; d < nd; d++) {
 			pinc_check(pinc_hip_d2h(tmp, dv->p.x[d] + a, n * sizeof(double), g_pinc.stream), "pSyncToHost");
 			for (long i = 0; i < n; i++) p->pos[(a + i) * nd + d] = tmp[i];
-			const double *vsrc = dv->p.v[d] + a;
-			if (dtmp) {
-				pinc_unsort_vel(p, s, d, dtmp);
-				vsrc = dtmp;
-			}
+			const double *vsrc = dtmp ? dtmp + d * n : dv->p.v[d] + a;
 			pinc_check(pinc_hip_d2h(tmp, vsrc, n * sizeof(double), g_pinc.stream), "pSyncToHost");
 			for (long i = 0; i < n; i++) p->vel[(a + i) * nd + d] = tmp[i];
 		}

@@ -411,11 +411,9 @@ static int push_all(Population *pop, Grid *E, double *const *xout) {
 			pinc_check(pinc_hip_memset(dv->objCount + (long)s * dv->objK, 0, dv->objK * sizeof(int), g_pinc.stream),
 			           "object counts");
 		/* a species left in order by a sorting push still goes to the
-		 * alternate arrays (swapped for all species); its perm is the
-		 * identity, recorded instead of written (pinc_unsort_vel) */
+		 * alternate arrays (swapped for all species) */
 		dv->permId[s] = !sortS[s];
 		if (sortS[s]) {
-			a.perm = dv->perm + pop->iStart[s];
 			if (!dv->cntValid[s]) {
 				pinc_check(pinc_hip_memset(dv->keyCnt[s], 0, (dv->nKeys + 1) * sizeof(int), g_pinc.stream), "keys");
 				pinc_check(pinc_hip_count_keys(p, s, 0, g, dv->tileWidth, dv->keyCnt[s], g_pinc.stream), "count keys");
@@ -500,16 +498,34 @@ static int push_all(Population *pop, Grid *E, double *const *xout) {
 	return sortNow;
 }
 
-/* dst = the kicked velocities (component d) of species s pending in altV
- * after a sorting push, in the current particle order */
-void pinc_unsort_vel(const Population *pop, int s, int d, double *dst) {
+/* dst[d] = the kicked velocities of species s pending after a sorting push,
+ * in the current particle order (n per component, device).  A species the
+ * push left in order has them in altV.  A sorted one gets the kick again:
+ * from its unkicked velocities (p.v, which a sorting push only reads), with
+ * the push's E and k_accel, whose arithmetic is the fused kick's
+ * (puInterp3D1's expression order, no contraction, E read as stored), so
+ * the velocities are bit-identical.  This replaces a permutation that every
+ * sorting push wrote (4 B per particle) for this rare path (a read or an
+ * extract between puAcc and puMove). */
+void pinc_pending_vel(const Population *pop, int s, double *const *dst) {
 	const PincDevPop *dv = pop->dev;
 	long a = pop->iStart[s], n = pop->iStop[s] - a;
+	int nd = pop->nDims;
 	if (n <= 0) return;
-	if (dv->permId[s])
-		pinc_check(pinc_hip_d2d(dst, dv->altV[d] + a, n * sizeof(double), g_pinc.stream), "unsort velocities");
-	else
-		pinc_check(pinc_hip_gather_perm(dv->altV[d] + a, dv->perm + a, n, dst, g_pinc.stream), "unsort velocities");
+	for (int d = 0; d < nd; d++) {
+		const double *src = (dv->permId[s] ? dv->altV[d] : dv->p.v[d]) + a;
+		if (dst[d] != src)
+			pinc_check(pinc_hip_d2d(dst[d], src, n * sizeof(double), g_pinc.stream), "pending velocities");
+	}
+	if (dv->permId[s]) return;
+	if (!dv->pendingE) msg(ERROR, "pending sorted push without its E");
+	PincDevGrid *eg = dv->pendingE->dev;
+	pinc_check(pinc_hip_field_chain(eg->d, eg->scaled, eg->n, dv->qm, dv->mq, 1.0, s, g_pinc.stream), "E chain");
+	pinc_pop_t p = pinc_devpop(pop);
+	/* (species s only is touched: indices iStart[s] .. iStop[s] - 1) */
+	for (int d = 0; d < nd; d++) p.v[d] = dst[d] - a;
+	int nb = 0;
+	pinc_check(pinc_hip_accelerate(p, s, eg->geom, eg->scaled, dv->kePartial, &nb, g_pinc.stream), "pending kick");
 }
 
 static void swap_pos(PincDevPop *dv, int nd, int vel) {
@@ -534,9 +550,11 @@ static void classify(Population *pop, int doMove) {
 		/* flags recomputed for the current positions: drop the pending move
 		 * (a sorted one first puts the kicked velocities back in order) */
 		if (dv->pendingSorted)
-			for (int s = 0; s < pop->nSpecies; s++)
-				for (int d = 0; d < nd; d++)
-					pinc_unsort_vel(pop, s, d, dv->p.v[d] + pop->iStart[s]);
+			for (int s = 0; s < pop->nSpecies; s++) {
+				double *dst[3];
+				for (int d = 0; d < 3; d++) dst[d] = d < nd ? dv->p.v[d] + pop->iStart[s] : NULL;
+				pinc_pending_vel(pop, s, dst);
+			}
 		dv->pending = dv->pendingSorted = 0;
 		/* its object counts go with it */
 		if (dv->objCount)
@@ -882,6 +900,7 @@ static void acc(Population *pop, Grid *E, int ke) {
 		dv->pending = 0;
 		dv->pendingSorted = push_all(pop, E, dv->altX);
 		dv->pending = 1;
+		dv->pendingE = E;
 		dv->flagsValid = 0;
 		if (ke) {
 			double sums[PINC_MAX_SPECIES];

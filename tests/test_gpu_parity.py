@@ -297,7 +297,8 @@ def test_pending_sorting_push_read_and_dropped(sim_cls):
     the move pending with the kicked velocities in slot order.  Reading the
     particles then (pSyncToHost), and dropping the move (an extract without a
     move), must give the state of the unfused operators: positions unmoved
-    and bit-identical, velocities kicked.  (The fused run's first sorting
+    and bit-identical, velocities kicked -- and bit-identical to those the
+    push commits at the next move.  (The fused run's first sorting
     push is preceded by a sort of the lattice-ordered population, so the two
     runs hold the particles in different orders: compared as sets, sorted by
     position and velocity.)"""
@@ -323,6 +324,18 @@ def test_pending_sorting_push_read_and_dropped(sim_cls):
             np.testing.assert_array_equal(p1[o1], p0[o0])
             assert np.abs(v1[o1] - v0[o0]).max() <= 1e-12 * np.abs(v0).max(), (key, sp)
     np.testing.assert_array_equal(out["1"]["em"], out["0"]["em"])
+    # the read while the sorted move is pending re-applies the kick
+    # (pinc_pending_vel): bit-identical to the velocities the push committed
+    cfg["population"]["fused"] = "1"
+    with sim_cls(configs.write_ini(cfg), maxwell=True, perturb=False, seed=11) as s:
+        s.init()
+        s.op("acc")
+        pending = [s.particles(sp)[1] for sp in range(2)]
+        s.op("move")
+        moved = [s.particles(sp)[1] for sp in range(2)]
+    for sp in range(2):
+        a, b = pending[sp], moved[sp]
+        np.testing.assert_array_equal(a[np.lexsort(a.T[::-1])], b[np.lexsort(b.T[::-1])])
 
 
 @pytest.mark.parametrize("name,kw,maxwell", [("cold3d", {}, False),
