@@ -174,11 +174,13 @@ def test_c4_full_size_invariants(built):
 
 
 def test_c5_full_size_invariants(built):
-    """256^3 with the sphere of radius 8 cells (bench --workload c5, the
-    capacitance matrix by translation to keep the set-up short: the same
-    run to solver tolerance, tests/test_gpu_objects.py), 4 steps: charge
-    that left the plasma is on the object."""
-    r = _full_size_run("c5", 4, {"objects": {"capacitance": "green"}})
+    """256^3 with the sphere of radius 8 cells, the bench's flags (bench
+    --workload c5: the capacitance matrix from one solve per surface node,
+    as the reference's oComputeCapacitanceMatrix, ~15 s of set-up; the
+    spectral second guess; the fused collection), 4 steps: charge that left
+    the plasma is on the object (the full-size run had used
+    the translation shortcut)."""
+    r = _full_size_run("c5", 4)
     n, q = np.array(r["n"], dtype=float), np.asarray(r["q"])
     plasma = n @ q[: n.shape[1]]
     total = plasma + np.array(r["collected"]) - r["collected"][0]
