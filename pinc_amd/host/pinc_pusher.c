@@ -240,7 +240,7 @@ static int cmp_double(const void *x, const void *y) {
 /* PINC_TRACE_SORT=2: mean per-block time of each push phase (s_memrealtime,
  * 100 MHz) and the kernel's span */
 static void push_phase_report(const unsigned long long *dts, const unsigned long long *ddiag, int nb, int s, int sort,
-                              int count) {
+                              int count, double *const *xout, long i0, long np) {
 	unsigned long long *t = malloc((size_t)nb * 8 * sizeof(*t));
 	unsigned long long dg[8];
 	pinc_check(pinc_hip_d2h(t, dts, (size_t)nb * 8 * sizeof(*t), g_pinc.stream), "push timestamps");
@@ -284,6 +284,45 @@ static void push_phase_report(const unsigned long long *dts, const unsigned long
 		double *lv = malloc((size_t)nb * sizeof(*lv));
 		for (int b = 0; b < nb; b++) lv[b] = (double)(t[b * 8 + 7] - t[b * 8]) * 1e-2;
 		qsort(lv, nb, sizeof(*lv), cmp_double);
+		/* the slowest blocks: chunk (position in the species, in chunks),
+		 * lifetime, start relative to the launch's first block */
+		{
+			int top[5] = {-1, -1, -1, -1, -1};
+			for (int b = 0; b < nb; b++) {
+				const unsigned long long l = t[b * 8 + 7] - t[b * 8];
+				for (int k = 0; k < 5; k++) {
+					if (top[k] < 0 || l > t[top[k] * 8 + 7] - t[top[k] * 8]) {
+						for (int m = 4; m > k; m--) top[m] = top[m - 1];
+						top[k] = b;
+						break;
+					}
+				}
+			}
+			fprintf(stderr, "[pinc]   slowest blocks (chunk of %d: us, start us):", nb);
+			for (int k = 0; k < 5 && top[k] >= 0; k++)
+				fprintf(stderr, " %d: %.1f, %.1f;", top[k], (t[top[k] * 8 + 7] - t[top[k] * 8]) * 1e-2,
+				        (t[top[k] * 8] - t0) * 1e-2);
+			fprintf(stderr, "\n");
+			/* their particles' cells after the push (unsorted push: same order) */
+			const long chunk = pinc_hip_push_chunk();
+			double *buf = malloc(chunk * sizeof(double));
+			for (int k = 0; k < 5 && top[k] >= 0 && !sort; k++) {
+				long b0 = (long)top[k] * chunk, n = b0 + chunk <= np ? chunk : np - b0;
+				fprintf(stderr, "[pinc]     chunk %d cells:", top[k]);
+				for (int d = 0; d < 3 && xout[d]; d++) {
+					pinc_check(pinc_hip_d2h(buf, xout[d] + i0 + b0, n * sizeof(double), g_pinc.stream), "trace read");
+					int lo = 1 << 30, hi = -(1 << 30);
+					for (long i = 0; i < n; i++) {
+						int c = (int)buf[i];
+						lo = c < lo ? c : lo;
+						hi = c > hi ? c : hi;
+					}
+					fprintf(stderr, " d%d %d..%d", d, lo, hi);
+				}
+				fprintf(stderr, "\n");
+			}
+			free(buf);
+		}
 		fprintf(stderr, "[pinc]   block us p10 %.1f p50 %.1f p90 %.1f p99 %.1f max %.1f\n", lv[nb / 10], lv[nb / 2],
 		        lv[nb * 9 / 10], lv[nb * 99 / 100], lv[nb - 1]);
 		/* phases of the blocks above p90 and below p50 */
@@ -444,7 +483,7 @@ static int push_all(Population *pop, Grid *E, double *const *xout) {
 		int slotK = E ? pinc_probe_begin(kind) : -1;
 		pinc_check(pinc_hip_push(p, s, g, &a, &nb, g_pinc.stream), "push");
 		if (ts) {
-			push_phase_report(ts, a.diag, nb, s, sortS[s], countNext);
+			push_phase_report(ts, a.diag, nb, s, sortS[s], countNext, a.xout, pop->iStart[s], np);
 			pinc_hip_free(ts);
 		}
 		/* pos R+W, vel R+W (32 B per dim per particle) + E R (8 B per value
