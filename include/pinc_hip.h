@@ -111,10 +111,10 @@ int pinc_hip_move_classify(pinc_pop_t pop, int s, int doMove, const double *thr,
  *     cursor[key(x_i)]++ (cursor = exclusive scan of the key counts of the
  *     current positions, pinc_hip_count_keys + pinc_hip_scan_keys), its
  *     moved state to xout/vout at that slot (must not alias pop), flags at
- *     that slot, perm[i] = slot if perm is set; chunkCount counts
- *     emigrants per destination chunk.  Otherwise (cursor == NULL) the keys
- *     of the moved particles that stay are counted into cntNext if set
- *     (zeroed by the caller); a sorting push does not count. */
+ *     that slot; chunkCount counts emigrants per destination chunk.
+ *     Otherwise (cursor == NULL) the keys of the moved particles that stay
+ *     are counted into cntNext if set (zeroed by the caller); a sorting
+ *     push does not count. */
 typedef struct {
 	double *xout[3];
 	double *vout[3];
@@ -131,7 +131,6 @@ typedef struct {
 	int tileWidth;
 	int *cursor;
 	int *cntNext;
-	int *perm;
 	unsigned long long *moved; /* if set: += particles that stay and changed cell */
 	unsigned long long *spread; /* if set: += each block's input cell-box volume (cells spanned by its
 	                             * items, periodic images nearest its first item) */
@@ -158,7 +157,6 @@ int pinc_hip_count_keys(pinc_pop_t pop, int s, long first, pinc_geom_t g, int ti
 /* exclusive scan of nKeys counts (offsets[nKeys] = total); work holds
  * 2*ceil(nKeys/4096)+1 ints */
 int pinc_hip_scan_keys(const int *counts, long nKeys, int *offsets, int *work, void *stream);
-/* dst[i] = src[perm[i]] (velocities of a sorted push in the old order) */
 /* puBoris3D1KE (pusher.c:433-483; rotation parameters pusher.c:485-505) with
  * the reference's indexing defect corrected: per particle a half kick from
  * Es (E as rescaled for species s), v' = v + v x T, v += v' x S (addCross
@@ -166,9 +164,6 @@ int pinc_hip_scan_keys(const int *counts, long nKeys, int *offsets, int *work, v
  * three components each.  3-D only. */
 int pinc_hip_boris(pinc_pop_t pop, int s, pinc_geom_t g, const double *Es, const double *T, const double *S,
                    double *kePartial, int *nBlocks, void *stream);
-int pinc_hip_gather_perm(const double *src, const int *perm, long n, double *dst, void *stream);
-/* perm[i] = i (a species left in order by a push that sorted another one) */
-int pinc_hip_iota(int *perm, long n, void *stream);
 /* rho = the reference's per-species chain (gZero; gMul(1/q_s); add species
  * s; gMul(q_s); pusher.c:512-572) applied to per-species sums acc[s], over
  * n slab elements */

@@ -1318,7 +1318,6 @@ struct PushArgs {
 	TileGeo tg;
 	int *cursor;
 	int *cntNext;
-	int *perm;           // perm[i] = destination of particle i (nullable)
 	unsigned long long *moved;  // += particles that stay but changed cell (nullable)
 	unsigned long long *spread;  // += the block's input cell-box volume (nullable)
 	unsigned long long *tstamp;  // 8 phase timestamps per block (diagnostics, nullable)
@@ -1389,12 +1388,6 @@ constexpr int kPushGroupMin = PINC_PUSH_GROUP_MIN;
 constexpr int kRhoLds = PINC_PUSH_COPIES ? PINC_PUSH_RHO_LDS : 1024;
 
 constexpr int kPushGroups = PINC_PUSH_GROUPS;
-// 1: the sorting push ranks its items with wave-aggregated LDS atomics
-// (lds_agg_add, round 3); 0: plain LDS atomics (measured at C4: electron
-// sorting push 36.2 -> 33.5 ms)
-#ifndef PINC_PUSH_AGG
-#define PINC_PUSH_AGG 0
-#endif
 // 8 waves x 4 particles per thread per PINC_CHUNK block: fewer live VGPRs
 // (px) than 4 waves x 8, so more waves per SIMD hide the gather latency
 #ifndef PINC_PUSH_ITEMS
@@ -2019,11 +2012,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 			// plain LDS atomics: a wave's lanes share a few bricks (same-address
 			// conflicts), cheaper than aggregating the groups with ballots and
 			// shuffles (C4 electron sorting push 36.2 -> 33.5 ms)
-#if PINC_PUSH_AGG
-			const int rank = lds_agg_add<true>(bCnt, lb < 0 ? 0 : lb, lb >= 0);
-#else
 			const int rank = lb >= 0 ? atomicAdd(&bCnt[lb], 1) : 0;
-#endif
 			const bool out = ok && lb < 0;
 			const int g = agg_add(a.cursor, out ? brick_first_key<ND>(a.tg, c) : 0, out);
 			rl[k] = lb >= 0 ? (rank << 8 | lb) : (ok ? ~g : -1);
@@ -2301,7 +2290,6 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 			}
 			const int f = stageF[k * kPushThreads + threadIdx.x];
 			a.flags[o] = (unsigned char)f;
-			if (a.perm) a.perm[i] = (int)o;
 			if (f != a.center) atomicAdd(&a.chunkCount[o / PINC_CHUNK], 1);
 		}
 	}
@@ -3060,7 +3048,6 @@ extern "C" int pinc_hip_push(pinc_pop_t pop, int s, pinc_geom_t g, const pinc_pu
 	a.tg = make_tile_geo(g, args->tileWidth > 0 ? args->tileWidth : 1, &nKeys);
 	a.cursor = args->cursor;
 	a.cntNext = args->cntNext;
-	a.perm = args->perm;
 	a.moved = args->moved;
 	a.spread = args->spread;
 	a.tstamp = args->tstamp;
@@ -3136,32 +3123,6 @@ extern "C" int pinc_hip_scan_keys(const int *counts, long nKeys, int *offsets, i
 	return check_launch("scan_keys");
 }
 
-__global__ void k_gather_perm(const double *__restrict__ src, const int *__restrict__ perm, long n,
-                              double *__restrict__ dst) {
-	for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
-		dst[i] = src[perm[i]];
-}
-
-extern "C" int pinc_hip_gather_perm(const double *src, const int *perm, long n, double *dst, void *stream) {
-	if (n <= 0) return 0;
-	long nb = ceil_div(n, (long)kThreads);
-	if (nb > 65536) nb = 65536;
-	hipLaunchKernelGGL(k_gather_perm, dim3((unsigned)nb), dim3(kThreads), 0, (hipStream_t)stream, src, perm, n, dst);
-	return check_launch("gather_perm");
-}
-
-__global__ void k_iota(int *__restrict__ perm, long n) {
-	for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
-		perm[i] = (int)i;
-}
-
-extern "C" int pinc_hip_iota(int *perm, long n, void *stream) {
-	if (n <= 0) return 0;
-	long nb = ceil_div(n, (long)kThreads);
-	if (nb > 65536) nb = 65536;
-	hipLaunchKernelGGL(k_iota, dim3((unsigned)nb), dim3(kThreads), 0, (hipStream_t)stream, perm, n);
-	return check_launch("iota");
-}
 
 extern "C" int pinc_hip_rho_combine(double *rho, const double *const *acc, const double *charge, int ns, long n,
                                     void *stream) {
