@@ -325,10 +325,20 @@ def main() -> int:
         out = os.fdopen(os.dup(1), "w")
         os.dup2(2, 1)
 
-    import torch
+    # PINC_TORCH_STACK=0 (one rank): no torch in the process, so the
+    # libraries run on /opt/rocm's HIP runtime and rocFFT, as the C driver does
+    torch_stack = os.environ.get("PINC_TORCH_STACK", "1") != "0"
+    if not torch_stack and world > 1:
+        raise SystemExit("PINC_TORCH_STACK=0 runs one rank (torch.distributed is the control plane)")
     if args.host_transport:
         local = 0
-    torch.cuda.set_device(local)
+    if torch_stack:
+        import torch
+        torch.cuda.set_device(local)
+
+    def device_sync():
+        if torch_stack:
+            torch.cuda.synchronize()
     dist = None
     if world > 1:
         # control plane only (barriers, the communicator id, max-over-ranks
@@ -408,14 +418,14 @@ def main() -> int:
         _lib.comm_stats_start(1 << 15)
 
     barrier()
-    torch.cuda.synchronize()
+    device_sync()
     sim.sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
         sim.step()
         log(f"timed step {i} done at {time.perf_counter() - t0:.2f} s")
     sim.sync()
-    torch.cuda.synchronize()
+    device_sync()
     barrier()
     dt = time.perf_counter() - t0
 
