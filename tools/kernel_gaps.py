@@ -62,9 +62,15 @@ def main():
         g = sum(w[1] for w in ws) / len(ws) / 1e6
         n = sum(w[2] for w in ws) / len(ws)
         print(f"solve windows {len(ws)}: kernels {k:.3f} ms + gaps {g:.3f} ms per window ({n:.0f} launches)")
-    pushes = [i for i, r in enumerate(rows) if short(r[0]).startswith("k_push")]
     # a step starts at the first push after a field kernel
-    steps = [i for i in pushes if any(short(rows[j][0]).startswith("k_efield") for j in range(max(0, i - 12), i))]
+    steps, sawField = [], False
+    for i, r in enumerate(rows):
+        n = short(r[0])
+        if n.startswith("k_efield"):
+            sawField = True
+        elif n.startswith("k_push") and sawField:
+            steps.append(i)
+            sawField = False
     if len(steps) > 3:
         spans = [(rows[b][1] - rows[a][1]) / 1e6 for a, b in zip(steps[1:], steps[2:])]
         idle = [sum(gaps[a + 1:b + 1]) / 1e6 for a, b in zip(steps[1:], steps[2:])]
