@@ -367,8 +367,10 @@ void gNeutralizeGrid(Grid *grid, const MpiInfo *mpiInfo) {
 	pinc_check(pinc_hip_sub_dev(dv->d, dv->n, PINC_SLOT(2), g_pinc.stream), "neutralize sub");
 }
 
-/* 0.5 * sum over this rank's true nodes of rho*phi (grid.c:1276-1294) */
-void gPotEnergy(const Grid *rho, const Grid *phi, Population *pop) {
+/* 0.5 * sum over this rank's true nodes of rho*phi (grid.c:1276-1294):
+ * the sum into PINC_SLOT(3), read by gPotEnergy (or by the step loop
+ * together with the error word, pinc_regular.c) */
+void pinc_pot_energy_launch(const Grid *rho, const Grid *phi) {
 	const PincDevGrid *r = rho->dev, *p = phi->dev;
 	long ps = r->planeSize;
 	long n = ps * r->geom.nloc;
@@ -379,6 +381,10 @@ void gPotEnergy(const Grid *rho, const Grid *phi, Population *pop) {
 		pv = p->global ? p->global : p->d + ps;
 	}
 	pinc_check(pinc_hip_dot(rv, pv, n, g_pinc.dScratch, PINC_SLOT(3), g_pinc.stream), "potential energy");
+}
+
+void gPotEnergy(const Grid *rho, const Grid *phi, Population *pop) {
+	pinc_pot_energy_launch(rho, phi);
 	double e = 0;
 	pinc_check(pinc_hip_d2h(&e, PINC_SLOT(3), sizeof(double), g_pinc.stream), "potential energy");
 	pop->potEnergy[pop->nSpecies] = 0.5 * e;

@@ -114,7 +114,10 @@ struct PincDevPop {
 	 * size in the first push after the last sort (a drifting beam changes
 	 * cell without spreading); sortMax still bounds the interval */
 	double sortSpread;
-	unsigned long long *spreadCnt;      /* device, per species, this push */
+	unsigned long long *spreadCnt;      /* device, per species, this push (after movedCnt, then the
+	                                     * kinetic-energy sums as doubles: one block, one read) */
+	double keSums[PINC_MAX_SPECIES];    /* host: this push's v^2 sums, read with the counters */
+	int keSumsValid;
 	double spreadBase[PINC_MAX_SPECIES], spreadLast[PINC_MAX_SPECIES];
 	double movedFrac[PINC_MAX_SPECIES], lastRate[PINC_MAX_SPECIES];
 	int sinceSort[PINC_MAX_SPECIES], sortNext[PINC_MAX_SPECIES];
@@ -249,6 +252,7 @@ void pinc_pop_flush_host(const Population *pop);
 /* the weight a deposit without the literal factor misses for the second fold
  * of main.c:232 (pinc_pusher.c) */
 /* kicked velocities pending after a sorting push, in the current order */
+void pinc_pot_energy_launch(const Grid *rho, const Grid *phi);
 void pinc_pending_vel(const Population *pop, int s, double *const *dst);
 void pinc_literal_second_fold(const Population *pop, Grid *rho, int order);
 

@@ -107,10 +107,11 @@ Population *pAlloc(const dictionary *ini) {
 		dv->sortSpread = iniHas(ini, "population:sortSpread") ? iniGetDouble(ini, "population:sortSpread") : 0.0;
 		if (dv->sortSpread < 0) msg(ERROR, "population:sortSpread out of range");
 		if (dv->sortFraction > 0) {
-			pinc_check(pinc_hip_malloc((void **)&dv->movedCnt, PINC_MAX_SPECIES * sizeof(unsigned long long)),
+			/* moved and spread counters and the kinetic-energy sums in one
+			 * block: one read per push */
+			pinc_check(pinc_hip_malloc((void **)&dv->movedCnt, 3 * PINC_MAX_SPECIES * sizeof(unsigned long long)),
 			           "pAlloc moved");
-			pinc_check(pinc_hip_malloc((void **)&dv->spreadCnt, PINC_MAX_SPECIES * sizeof(unsigned long long)),
-			           "pAlloc spread");
+			dv->spreadCnt = dv->movedCnt + PINC_MAX_SPECIES;
 			for (int s = 0; s < PINC_MAX_SPECIES; s++) dv->sortNext[s] = 1;
 		}
 	}
@@ -227,7 +228,6 @@ void pFree(Population *p) {
 			pinc_hip_free(dv->keyWork[s]);
 		}
 		pinc_hip_free(dv->movedCnt);
-		pinc_hip_free(dv->spreadCnt);
 		for (int s = 0; s < PINC_MAX_SPECIES; s++) pinc_hip_free(dv->sortWork[s]);
 		pinc_hip_free(dv->chunkCount);
 		pinc_hip_free(dv->ws[0].chunkOffset);

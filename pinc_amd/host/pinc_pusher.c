@@ -369,6 +369,7 @@ static int push_all(Population *pop, Grid *E, double *const *xout) {
 	}
 	int sortNow = 0, sortS[PINC_MAX_SPECIES] = {0}, countS[PINC_MAX_SPECIES] = {0};
 	int adaptive = dv->sorted && dv->sortFraction > 0;
+	dv->keSumsValid = 0;
 	if (dv->sorted) {
 		ensure_keys(pop);
 		for (int s = 0; s < pop->nSpecies; s++) {
@@ -396,10 +397,9 @@ static int push_all(Population *pop, Grid *E, double *const *xout) {
 	}
 	int nd = pop->nDims;
 	if (adaptive) {
-		pinc_check(pinc_hip_memset(dv->movedCnt, 0, PINC_MAX_SPECIES * sizeof(unsigned long long), g_pinc.stream),
+		/* (spreadCnt follows movedCnt in one block, pinc_pop.c) */
+		pinc_check(pinc_hip_memset(dv->movedCnt, 0, 2 * PINC_MAX_SPECIES * sizeof(unsigned long long), g_pinc.stream),
 		           "moved counts");
-		pinc_check(pinc_hip_memset(dv->spreadCnt, 0, PINC_MAX_SPECIES * sizeof(unsigned long long), g_pinc.stream),
-		           "spread counts");
 	}
 	for (int s = 0; s < pop->nSpecies; s++) {
 		int countNext = countS[s];
@@ -496,8 +496,9 @@ static int push_all(Population *pop, Grid *E, double *const *xout) {
 		if (E) {
 			/* two-stage (block partials of the partials): deterministic and
 			 * fast for a million partials */
-			if (nb > 0) pinc_check(pinc_hip_sum(dv->kePartial, nb, g_pinc.dScratch, PINC_SLOT(16 + s), g_pinc.stream), "ke");
-			else pinc_check(pinc_hip_memset(PINC_SLOT(16 + s), 0, sizeof(double), g_pinc.stream), "ke");
+			double *keOut = adaptive ? (double *)(dv->spreadCnt + PINC_MAX_SPECIES) + s : PINC_SLOT(16 + s);
+			if (nb > 0) pinc_check(pinc_hip_sum(dv->kePartial, nb, g_pinc.dScratch, keOut, g_pinc.stream), "ke");
+			else pinc_check(pinc_hip_memset(keOut, 0, sizeof(double), g_pinc.stream), "ke");
 		}
 		if (countNext) {
 			int *t = dv->keyCnt[s];
@@ -509,9 +510,13 @@ static int push_all(Population *pop, Grid *E, double *const *xout) {
 		}
 	}
 	if (adaptive) {
-		unsigned long long mv[PINC_MAX_SPECIES], sp[PINC_MAX_SPECIES];
-		pinc_check(pinc_hip_d2h(mv, dv->movedCnt, pop->nSpecies * sizeof(mv[0]), g_pinc.stream), "moved readback");
-		pinc_check(pinc_hip_d2h(sp, dv->spreadCnt, pop->nSpecies * sizeof(sp[0]), g_pinc.stream), "spread readback");
+		unsigned long long cnt[3 * PINC_MAX_SPECIES];
+		pinc_check(pinc_hip_d2h(cnt, dv->movedCnt, sizeof(cnt), g_pinc.stream), "moved, spread and energy readback");
+		const unsigned long long *mv = cnt, *sp = cnt + PINC_MAX_SPECIES;
+		if (E) {
+			memcpy(dv->keSums, cnt + 2 * PINC_MAX_SPECIES, sizeof(dv->keSums));
+			dv->keSumsValid = 1;
+		}
 		for (int s = 0; s < pop->nSpecies; s++) {
 			long np = pop->iStop[s] - pop->iStart[s];
 			double rate = np > 0 ? (double)mv[s] / (double)np : 0.0;
@@ -943,7 +948,10 @@ static void acc(Population *pop, Grid *E, int ke) {
 		dv->flagsValid = 0;
 		if (ke) {
 			double sums[PINC_MAX_SPECIES];
-			pinc_check(pinc_hip_d2h(sums, PINC_SLOT(16), pop->nSpecies * sizeof(double), g_pinc.stream), "ke readback");
+			if (dv->keSumsValid) /* read with the sort counters (push_all) */
+				memcpy(sums, dv->keSums, sizeof(sums));
+			else
+				pinc_check(pinc_hip_d2h(sums, PINC_SLOT(16), pop->nSpecies * sizeof(double), g_pinc.stream), "ke readback");
 			for (int s = 0; s < pop->nSpecies; s++) pop->kinEnergy[s] = sums[s] * (0.5 * pop->mass[s]);
 		}
 		pinc_phase_end(6);

@@ -59,11 +59,15 @@ struct PincSim {
 
 static int g_simActive = 0;
 
+static void report_errors(int err) {
+	if (err & 1) msg(ERROR, "Particle travels too fast (population:maxVel exceeded, population.c:342-365)");
+	if (err & 2) msg(ERROR, "Particle is out of bounds after migration (population.c:316-340)");
+}
+
 static void check_errors(void) {
 	int err = 0;
 	pinc_check(pinc_hip_d2h(&err, g_pinc.dErr, sizeof(int), g_pinc.stream), "assert word");
-	if (err & 1) msg(ERROR, "Particle travels too fast (population:maxVel exceeded, population.c:342-365)");
-	if (err & 2) msg(ERROR, "Particle is out of bounds after migration (population.c:316-340)");
+	report_errors(err);
 }
 
 static PincSim *sim_build(dictionary *ini, const PincSimOpts *opts) {
@@ -207,9 +211,16 @@ static void sim_step(PincSim *S) {
 	S->acc(pop, S->E);
 	pinc_phase_begin(7);
 	pSumKinEnergy(pop);
-	gPotEnergy(S->rho, S->phi, pop);
+	/* gPotEnergy and the error word in one read (PINC_SLOT(3..4)) */
+	pinc_pot_energy_launch(S->rho, S->phi);
+	pinc_check(pinc_hip_d2d(PINC_SLOT(4), g_pinc.dErr, sizeof(int), g_pinc.stream), "assert word");
+	double r[2];
+	pinc_check(pinc_hip_d2h(r, PINC_SLOT(3), sizeof(r), g_pinc.stream), "potential energy");
+	pop->potEnergy[pop->nSpecies] = 0.5 * r[0];
 	pinc_phase_end(7);
-	check_errors();
+	int err = 0;
+	memcpy(&err, &r[1], sizeof(err));
+	report_errors(err);
 	S->steps++;
 }
 
