@@ -20,7 +20,7 @@ from pinc_amd import configs
 from test_oracle_golden import ke_peak_omega
 
 pytestmark = pytest.mark.gpu
-GOLD = json.loads((Path(__file__).parent / "golden" / "reference_outputs.json").read_text())["runs"]
+GOLD = json.loads((Path(__file__).parent / "golden" / "reference_outputs.json").read_text())["standin_build_runs"]
 
 
 @pytest.fixture(scope="module")

@@ -13,7 +13,7 @@ import pytest
 import orc
 from pinc_amd import configs
 
-GOLD = json.loads((Path(__file__).parent / "golden" / "reference_outputs.json").read_text())["runs"]
+GOLD = json.loads((Path(__file__).parent / "golden" / "reference_outputs.json").read_text())["standin_build_runs"]
 
 
 def ke_peak_omega(ke, dt):
