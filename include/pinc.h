@@ -34,33 +34,53 @@ typedef enum { TOHALO = 0, FROMHALO = 1 } opDirection;       /* grid.h:22-25 */
 typedef struct PincDevPop PincDevPop;
 typedef struct PincDevGrid PincDevGrid;
 
+/* The structs below have the reference's fields in the reference's order,
+ * types and offsets (x86-64 LP64; tests/test_core_layout.py checks every
+ * offsetof against tests/golden/core_layout.json, extracted from core.h).
+ * Each gains its device twin as a field appended AFTER the reference's
+ * last one, so code compiled against core.h reads every reference field at
+ * the offset it expects.  hid_t is HDF5 >= 1.10's int64_t (the library
+ * loads HDF5 at run time); MPI_Request * is an opaque pointer slot.  Fields
+ * the hot path does not use are kept NULL/0 (marked "unused"). */
+typedef long long pinc_hid_t;        /* hid_t (HDF5 >= 1.10: int64_t) */
+
 /* core.h:72-86 */
 typedef struct {
 	double *pos;         /* host mirror (AoS, nDims per particle)        */
 	double *vel;
 	long *iStart;        /* nSpecies+1 */
 	long *iStop;         /* nSpecies   */
+	long *objVicinity;   /* unused (NULL): object.c keeps its own lists  */
+	long *collisions;    /* unused (NULL)                                 */
 	double *charge;      /* normalised, nSpecies */
 	double *mass;
 	double *kinEnergy;   /* nSpecies+1 */
 	double *potEnergy;   /* nSpecies+1 */
 	int nSpecies;
 	int nDims;
-	PincDevPop *dev;     /* device twin */
-	long long h5;        /* .pop.h5 file (hid_t; rank 0 only, pOpenH5) */
+	pinc_hid_t h5;       /* .pop.h5 file (rank 0 only, pOpenH5) */
+	PincDevPop *dev;     /* device twin (appended) */
 } Population;
 
-/* core.h:112-138 (MPI request/handle fields replaced by the RCCL context) */
+/* core.h:112-138 */
 typedef struct {
 	int mpiRank, mpiSize, nDims;
 	int *subdomain, *nSubdomains, *nSubdomainsProd, *offset;
 	double *posToSubdomain;
 	int nSpecies, nNeighbors, neighborhoodCenter;
+	long **migrants;        /* unused (NULL; DEPRECATED in the reference) */
+	long **migrantsDummy;   /* unused (NULL) */
 	long *nEmigrants;       /* nNeighbors*nSpecies */
 	long *nEmigrantsAlloc;  /* nNeighbors */
 	long *nImmigrants;      /* nNeighbors*nSpecies */
+	long nImmigrantsAlloc;  /* immigrant records the device buffer holds */
+	double **emigrants;     /* unused (NULL): emigrants stay on the device */
+	double **emigrantsDummy;/* unused (NULL) */
+	double *immigrants;     /* unused (NULL) */
 	double *thresholds;     /* 2*nDims (+ nDims upper bounds for the assert) */
-	void *comm;             /* RCCL communicator (NULL with one rank) */
+	void *send;             /* MPI_Request *: unused (NULL) */
+	void *recv;             /* MPI_Request *: unused (NULL) */
+	void *comm;             /* RCCL communicator, NULL with one rank (appended) */
 } MpiInfo;
 
 /* core.h:261-277 */
@@ -70,9 +90,14 @@ typedef struct {
 	int *size, *trueSize;
 	long *sizeProd;
 	int *nGhostLayers;
+	double *sendSlice;   /* unused (NULL): halos move on the device */
+	double *recvSlice;   /* unused (NULL) */
+	double *bndSlice;    /* unused (NULL): periodic boundaries only */
+	pinc_hid_t h5;       /* .grid.h5 file (rank 0 only, gOpenH5) */
+	pinc_hid_t h5MemSpace;  /* unused (0): set per write */
+	pinc_hid_t h5FileSpace; /* unused (0) */
 	bndType *bnd;
-	PincDevGrid *dev;    /* device twin */
-	long long h5;        /* .grid.h5 file (hid_t; rank 0 only, gOpenH5) */
+	PincDevGrid *dev;    /* device twin (appended) */
 } Grid;
 
 /* core.h:392-417 */
@@ -115,12 +140,12 @@ funPtr selectInner(const dictionary *ini, const char *key, const char *list, ...
 #endif
 
 /* --------------------------------------------------------------- aux -- */
-/* Timer (core.h:419-436, aux.c:48-85): wall time in nanoseconds; tStop waits
+/* Timer (core.h:439-442, aux.c:48-85): wall time in nanoseconds; tStop waits
  * for the device work queued so far, so a span measures what the reference's
  * blocking loop measured */
 typedef struct {
-	long long start;
-	long long total;
+	unsigned long long total;  /* total time */
+	unsigned long long start;  /* previous start time */
 } Timer;
 Timer *tAlloc();        /* main.c:192 passes the rank; unused, as in aux.c */
 void tFree(Timer *t);

@@ -1880,7 +1880,17 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	int cref[3] = {0, 0, 0};
 #pragma unroll
 	for (int d = 0; d < ND; d++) cref[d] = __builtin_amdgcn_readfirstlane((int)xref[d]);
-	const Images img = make_images(G, a.wrapMask, cref, ND);
+	// main.c's double fold (literal loop): a deposit on a slab ghost plane
+	// counts twice and literal_ghost_weights adds that weight at the cell's
+	// own planes, so the slab dimension keeps its unmapped cells there (an
+	// image would move weight between ghost plane 0 and true plane T, which
+	// one fold treats alike and two do not)
+#ifndef PINC_LITERAL_SLAB_IMAGES
+	const int imgMask = a.g.literal ? (a.wrapMask & ~(1 << G.slab)) : a.wrapMask;
+#else
+	const int imgMask = a.wrapMask;  // (variant build: the round-4 mapping, for the regression test)
+#endif
+	const Images img = make_images(G, imgMask, cref, ND);
 #pragma unroll
 	for (int k = 0; k < kPushItems; k += 2) {
 #pragma unroll

@@ -80,6 +80,7 @@ struct PincObj {
 	/* main.c's order (oAlloc, oOpenH5, oReadH5): the tables are built when
 	 * oReadH5 reads the mask named by oOpenH5 */
 	int pending;
+	int optional;        /* objects:optional = 1 / PINC_OBJ_OPTIONAL=1: no mask file = no objects */
 	pinc_geom_t geom;
 	char *h5path;
 };
@@ -602,6 +603,8 @@ Object *oAlloc(const dictionary *ini) {
 	if (o) return o;
 	o = calloc(1, sizeof(*o));
 	o->pending = 1;
+	o->optional = (iniHas(ini, "objects:optional") && iniGetInt(ini, "objects:optional")) ||
+	              (getenv("PINC_OBJ_OPTIONAL") && atoi(getenv("PINC_OBJ_OPTIONAL")));
 	o->geom = g;
 	o->green = capacitance_green(ini);
 	o->haveCap = 1; /* nothing to solve until a mask arrives */
@@ -628,8 +631,10 @@ void oOpenH5(const dictionary *ini, Object *obj, const MpiInfo *mpiInfo, const U
 
 /* object.c:727-756: read /Object, then oFillLookupTables and
  * oFindObjectSurfaceNodes.  An object built from the ini (extensions) keeps
- * its tables.  No file at the oOpenH5 path: a run without objects (the
- * reference would read an absent dataset). */
+ * its tables.  No file at the oOpenH5 path ends the run, as in the
+ * reference (its H5Dopen fails); a run without objects must opt in with
+ * objects:optional = 1 or PINC_OBJ_OPTIONAL=1 (a mistyped
+ * files:output must not run silently without the objects). */
 void oReadH5(Object *obj, const MpiInfo *mpiInfo) {
 	(void)mpiInfo;
 	if (!obj->pending) return;
@@ -637,7 +642,9 @@ void oReadH5(Object *obj, const MpiInfo *mpiInfo) {
 	if (!obj->h5path) msg(ERROR, "oReadH5 before oOpenH5");
 	FILE *f = fopen(obj->h5path, "rb");
 	if (!f) {
-		msg(WARNING, "oReadH5: no %s, the run has no objects", obj->h5path);
+		if (!obj->optional)
+			msg(ERROR, "oReadH5: no object mask %s (set objects:optional=1 to run without objects)", obj->h5path);
+		msg(WARNING, "oReadH5: no %s, the run has no objects (objects:optional)", obj->h5path);
 		return;
 	}
 	fclose(f);

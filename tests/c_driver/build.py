@@ -17,7 +17,7 @@ def build(name: str = "pinc_main") -> Path:
     src = HERE / f"{name}.c"
     exe = HERE / name
     lib = ROOT / "pinc_amd" / "lib" / "libpinc.so"
-    hdr = [ROOT / "include" / "pinc.h", ROOT / "include" / "pinc_hip.h"]
+    hdr = [ROOT / "include" / h for h in ("pinc.h", "pinc_hip.h", "core.h", "pusher.h", "multigrid.h", "spectral.h")]
     if exe.exists() and all(exe.stat().st_mtime >= p.stat().st_mtime for p in [src, lib, *hdr]):
         return exe
     subprocess.run(["gcc", "-std=c11", "-O2", "-Wall", f"-I{ROOT / 'include'}", str(src), "-o", str(exe),

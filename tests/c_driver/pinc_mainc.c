@@ -25,10 +25,10 @@
  *
  *   pinc_mainc <file.ini> [section:key=value ...]
  */
-#include <stdio.h>
-#include <stdlib.h>
-#include <sys/select.h> /* before pinc.h, which defines the select() macro */
-#include "pinc.h"
+#include "core.h"      /* main.c:10-13, the reference's header names */
+#include "pusher.h"
+#include "multigrid.h"
+#include "spectral.h"
 
 void regular(dictionary *ini);
 funPtr regular_set(dictionary *ini) {

@@ -42,13 +42,18 @@ def test_product_has_no_oracle_dependency():
 
 
 class MpiInfo(C.Structure):
+    """include/pinc.h's MpiInfo: core.h:112-138's fields in core.h's order,
+    the RCCL communicator appended."""
     _fields_ = [("mpiRank", C.c_int), ("mpiSize", C.c_int), ("nDims", C.c_int),
                 ("subdomain", C.POINTER(C.c_int)), ("nSubdomains", C.POINTER(C.c_int)),
                 ("nSubdomainsProd", C.POINTER(C.c_int)), ("offset", C.POINTER(C.c_int)),
                 ("posToSubdomain", C.POINTER(C.c_double)),
                 ("nSpecies", C.c_int), ("nNeighbors", C.c_int), ("neighborhoodCenter", C.c_int),
+                ("migrants", C.c_void_p), ("migrantsDummy", C.c_void_p),
                 ("nEmigrants", C.POINTER(C.c_long)), ("nEmigrantsAlloc", C.POINTER(C.c_long)),
-                ("nImmigrants", C.POINTER(C.c_long)), ("thresholds", C.POINTER(C.c_double)),
+                ("nImmigrants", C.POINTER(C.c_long)), ("nImmigrantsAlloc", C.c_long),
+                ("emigrants", C.c_void_p), ("emigrantsDummy", C.c_void_p), ("immigrants", C.c_void_p),
+                ("thresholds", C.POINTER(C.c_double)), ("send", C.c_void_p), ("recv", C.c_void_p),
                 ("comm", C.c_void_p)]
 
 

@@ -197,6 +197,9 @@ def _mainc_cfg(nsub=(1, 1, 1), per_rank=(16, 16, 16), ppc=8, order=1):
     cfg["population"]["nAlloc"] = f"{2 * ppc} pc"
     # a Langmuir perturbation along x, so the energies are physical
     cfg["population"]["perturbAmplitude"] = "1e-3,0,0,0,0,0"
+    # main.c always reads <files:output>test.grid.h5 (main.c:126-127); these
+    # runs have no mask file and opt in to running without objects
+    cfg["objects"] = {"optional": "1"}
     if order == 0:
         cfg["methods"]["acc"] = "puAccND0KE"
         cfg["methods"]["distr"] = "puDistrND0"
@@ -275,7 +278,12 @@ def test_mainc_loop_matches_oracle_literal(built, tmp_path, nranks, order):
     pe = sum(r[:, 1] for r in rows)
     np.testing.assert_allclose(ke, ke_o, rtol=1e-8)
     np.testing.assert_allclose(pe, pe_o, rtol=1e-8)
-    assert "TIMER: Time spent:" in outs[0][0]
+    # tMsg(t->total, ...) (main.c:276): with core.h's Timer layout (total
+    # first) the value is the run's loop time, not a clock reading
+    m = re.search(r"TIMER: Time spent:\s+([0-9.]+)(s|ms|us|ns)", outs[0][0])
+    assert m, outs[0][0][-2000:]
+    secs = float(m.group(1)) * {"s": 1.0, "ms": 1e-3, "us": 1e-6, "ns": 1e-9}[m.group(2)]
+    assert 0.0 < secs < 300.0, m.group(0)
     assert "no objects" in outs[0][1]  # oReadH5 found no <output>test.grid.h5
     hk = _history(tmp_path / "history.xy.h5", "/energy/kinetic/total")
     hp = _history(tmp_path / "history.xy.h5", "/energy/potential/total")
@@ -346,6 +354,27 @@ def test_mainc_velocity_assert_ends_run(built, tmp_path):
         os.unlink(ini)
     assert r.returncode != 0
     assert "travels too fast" in r.stderr
+
+
+@pytest.mark.gpu
+def test_mainc_missing_object_mask_ends_run(built, tmp_path):
+    """main.c reads its object mask unconditionally (main.c:126-127,
+    object.c:727-756); without the file the reference's H5Dopen fails, so a
+    mistyped files:output ends the run here too unless the ini opts in with
+    objects:optional = 1."""
+    import build as cbuild
+    from pinc_amd import configs
+    exe = cbuild.build("pinc_mainc")
+    cfg = _mainc_cfg()
+    del cfg["objects"]
+    ini = configs.write_ini(cfg)
+    try:
+        r = subprocess.run([str(exe), ini, "time:nTimeSteps=1", f"files:output={tmp_path}/"], capture_output=True,
+                           text=True, timeout=300)
+    finally:
+        os.unlink(ini)
+    assert r.returncode != 0
+    assert "no object mask" in r.stderr
 
 
 @pytest.mark.gpu

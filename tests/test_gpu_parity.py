@@ -390,3 +390,38 @@ def test_literal_mainc_energy_history(sim_cls, name, fused):
             ke, pe, _ = s.energy()
             assert abs(ke - ke_o[n]) <= 1e-8 * abs(ke_o[n]), (n, ke, ke_o[n])
             assert abs(pe - pe_o[n]) <= 1e-8 * abs(pe_o[n]), (n, pe, pe_o[n])
+
+
+@pytest.mark.parametrize("sort_interval", ["8", "1000000"], ids=["sorting", "no_sort"])
+def test_literal_loop_tiled_one_rank_crossing_z(sim_cls, sort_interval):
+    """the literal loop (rho folded twice, main.c:226,232) on one
+    rank in the tiled layout, where the slab dimension wraps in place, with a
+    warm plasma whose particles cross the z boundary.  The fused push must
+    leave slab-ghost deposits on their own planes (a periodic image would
+    move weight between ghost plane 0 and true plane T, which the double
+    fold counts differently).  rho after every step against the checker's
+    literal loop to 1e-12 of one species' charge scale, energies to 1e-8."""
+    cfg = configs.config("warm", true_size=(16, 16, 16), ppc=16, nalloc_pc=24, vth=0.15, levels=3)
+    cfg["population"].update({"layout": "tiled", "sortInterval": sort_interval})
+    ini = configs.write_ini(cfg)
+    steps = 6
+    w = orc.World(ini, [], True)
+    w.init(False, True, 11)
+    w.init_fields()
+    with sim_cls(ini, literal=True, maxwell=True, perturb=False, seed=11) as s:
+        s.init()
+        q, _ = s.species()
+        for n in range(steps):
+            s.step()
+            w.step()
+            r, ro = s.grid(0), w.grid(0)
+            scale = abs(q[0]) * 16 * 8
+            assert np.abs(r[1:-1, 1:-1, 1:-1] - ro[1:-1, 1:-1, 1:-1]).max() <= 1e-12 * scale, n
+            ke, pe, _ = s.energy()
+            ke_o, pe_o = w.energy()
+            assert abs(ke - ke_o) <= 1e-8 * abs(ke_o), (n, ke, ke_o)
+            assert abs(pe - pe_o) <= 1e-8 * abs(pe_o), (n, pe, pe_o)
+        # electrons sit in the half cells at both z ends (they wrap there)
+        zs = s.particles(0)[0][:, 2]
+        assert np.sum(zs < 1.5) > 0 and np.sum(zs > 16.5) > 0
+    w.close()
