@@ -275,6 +275,10 @@ int pinc_hip_accelerate_ngp(pinc_pop_t pop, int s, pinc_geom_t g, const double *
 int pinc_hip_vel_assert(pinc_pop_t pop, int s, double maxVel, int *errFlag, void *stream);
 /* particles per workgroup of pinc_hip_push (a build constant) */
 long pinc_hip_push_chunk(void);
+/* xcd[c] = the XCD (block index mod 8) whose block processes push chunk c,
+ * for a launch of nBlocks blocks (the push's chunk placement; trace
+ * diagnostics) */
+int pinc_hip_push_xcd_of_chunks(long nBlocks, int *xcd);
 
 /* puAcc3D1KE / puAccND1KE (pusher.c:178-265) with puInterp3D1/ND1
  * (pusher.c:1089-1162), gathering from Es (pinc_hip_field_chain).

@@ -1408,6 +1408,15 @@ constexpr int kPushGroups = PINC_PUSH_GROUPS;
 #ifndef PINC_PUSH_THREADS
 #define PINC_PUSH_THREADS 256
 #endif
+// 1: per-item periodic images only in blocks that straddle a boundary (k_push)
+#ifndef PINC_PUSH_IMG_GATE
+#define PINC_PUSH_IMG_GATE 1
+#endif
+// 1: the cell-change statistic from the pre-move cell, the frame test only
+// for particles that leave the centre (k_push)
+#ifndef PINC_PUSH_LEAN
+#define PINC_PUSH_LEAN 1
+#endif
 constexpr int kPushThreads = PINC_PUSH_THREADS;
 constexpr int kPushItems = PINC_PUSH_ITEMS;  // particles per thread, in lane-contiguous pairs
 constexpr int kPushChunk = kPushThreads * kPushItems;  // particles per block (PINC_CHUNK / 2 by default)
@@ -1759,6 +1768,34 @@ __device__ __forceinline__ int brick_key(const TileGeo &tg, const BrickBox &bb, 
 
 typedef double dvec2 __attribute__((ext_vector_type(2)));
 
+// chunk of push block b of nb.  PINC_PUSH_XCD: consecutive chunks (the same
+// cell tiles after a sort: shared E nodes and rho atomics) on one XCD's L2.
+// Blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md,
+// workgroup dispatch), so block b runs on XCD b % 8; the map is a bijection
+// for any grid size and only a placement hint, never needed for
+// correctness.  (Host and device: the push trace attributes chunks to XCDs
+// with it, pinc_hip_push_xcd_of_chunk.)
+__host__ __device__ __forceinline__ unsigned push_chunk_of(unsigned nb, unsigned b) {
+#if PINC_PUSH_XCD == 2
+	// pieces of PINC_PUSH_XCD_PIECE consecutive chunks dealt round-robin over
+	// the XCDs (the tail beyond whole rounds in order): every XCD gets pieces
+	// from every part of the array, e.g. both z faces' tiles, where wrapped
+	// particles make blocks slower
+	constexpr unsigned P = PINC_PUSH_XCD_PIECE;
+	const unsigned F = nb / (8u * P) * (8u * P);
+	if (b >= F) return b;
+	const unsigned x = b & 7u, y = b >> 3;
+	return ((y / P) * 8u + x) * P + (y % P);
+#elif PINC_PUSH_XCD
+	const unsigned x = b & 7u, y = b >> 3;
+	const unsigned q = nb >> 3, r = nb & 7u;
+	return x * q + (x < r ? x : r) + y;
+#else
+	(void)nb;
+	return b;
+#endif
+}
+
 // OBJ: the object test of the fused collection (separate instances, so the
 // plain push carries none of its code)
 template <int ND, bool V3D, bool KICK, bool SORT, bool OBJ = false>
@@ -1786,34 +1823,8 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	__shared__ unsigned char stageF[SORT ? kPushChunk : 1];
 	const Geo32 G = make_geo32(a.g);
 	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-	// chunk of this block.  PINC_PUSH_XCD: consecutive chunks (the same cell
-	// tiles after a sort: shared E nodes and rho atomics) on one XCD's L2.
-	// Blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md,
-	// workgroup dispatch), so block b runs on XCD b % 8; the map is a
-	// bijection for any grid size and only a placement hint, never needed
-	// for correctness.
-#if PINC_PUSH_XCD == 2
-	// pieces of PINC_PUSH_XCD_PIECE consecutive chunks dealt round-robin over
-	// the XCDs (the tail beyond whole rounds in order): every XCD gets pieces
-	// from every part of the array, e.g. both z faces' tiles, where wrapped
-	// particles make blocks slower
-	const unsigned chunk = [] {
-		constexpr unsigned P = PINC_PUSH_XCD_PIECE;
-		const unsigned nb = gridDim.x, b = blockIdx.x;
-		const unsigned F = nb / (8u * P) * (8u * P);
-		if (b >= F) return b;
-		const unsigned x = b & 7u, y = b >> 3;
-		return ((y / P) * 8u + x) * P + (y % P);
-	}();
-#elif PINC_PUSH_XCD
-	const unsigned chunk = [] {
-		const unsigned nb = gridDim.x, x = blockIdx.x & 7u, y = blockIdx.x >> 3;
-		const unsigned q = nb >> 3, r = nb & 7u;
-		return x * q + min(x, r) + y;
-	}();
-#else
-	const unsigned chunk = blockIdx.x;
-#endif
+	// chunk of this block (push_chunk_of: XCD-aware placement)
+	const unsigned chunk = push_chunk_of(gridDim.x, blockIdx.x);
 	const long base = (long)chunk * kPushChunk;
 	// item k of a thread: particles in lane-contiguous pairs (16-B loads and
 	// stores, 1 KiB per wave instruction), pair k/2 of the thread
@@ -1847,7 +1858,6 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	}
 	double p[kPushItems][ND], vv[kPushItems][ND];
 	unsigned valid = 0;
-	int lo[3] = {INT32_MAX, INT32_MAX, INT32_MAX}, hi[3] = {INT32_MIN, INT32_MIN, INT32_MIN}, sm[3] = {0, 0, 0};
 	static_assert(kPushItems % 2 == 0, "items come in pairs");
 #pragma unroll
 	for (int k = 0; k < kPushItems; k += 2) {
@@ -1891,44 +1901,73 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	const int imgMask = a.wrapMask;  // (variant build: the round-4 mapping, for the regression test)
 #endif
 	const Images img = make_images(G, imgMask, cref, ND);
+	// cell range (and sum) of the block's items, in raw cells or in the
+	// images nearest the reference cell
+	auto cell_box = [&](bool withImg) {
+		int lo[3] = {INT32_MAX, INT32_MAX, INT32_MAX}, hi[3] = {INT32_MIN, INT32_MIN, INT32_MIN}, sm[3] = {0, 0, 0};
 #pragma unroll
-	for (int k = 0; k < kPushItems; k += 2) {
+		for (int k = 0; k < kPushItems; k += 2) {
 #pragma unroll
-		for (int d = 0; d < ND; d++) {
+			for (int d = 0; d < ND; d++) {
 #pragma unroll
-			for (int h = 0; h < 2; h++) {
-				if ((valid >> (k + h)) & 1u) {
-					const int c = img(d, (int)p[k + h][d]);
-					lo[d] = min(lo[d], c);
-					hi[d] = max(hi[d], c);
-					sm[d] += c;
+				for (int h = 0; h < 2; h++) {
+					if ((valid >> (k + h)) & 1u) {
+						const int c = withImg ? img(d, (int)p[k + h][d]) : (int)p[k + h][d];
+						lo[d] = min(lo[d], c);
+						hi[d] = max(hi[d], c);
+						sm[d] += c;
+					}
 				}
 			}
 		}
-	}
+#pragma unroll
+		for (int d = 0; d < ND; d++) {
+			int x = wave_min_i(lo[d]), y = wave_max_i(hi[d]), z = wave_sum(sm[d]);
+			if (lane == 0) {
+				red[(3 * d) * NW + wv] = x;
+				red[(3 * d + 1) * NW + wv] = y;
+				red[(3 * d + 2) * NW + wv] = z;
+			}
+		}
+		__syncthreads();
+		if (threadIdx.x < ND) {
+			int d = threadIdx.x, x = INT32_MAX, y = INT32_MIN, z = 0;
+			for (int w = 0; w < NW; w++) {
+				x = min(x, red[(3 * d) * NW + w]);
+				y = max(y, red[(3 * d + 1) * NW + w]);
+				z += red[(3 * d + 2) * NW + w];
+			}
+			const int nv = (int)min((long)kPushChunk, a.n - base);
+			cbox[d] = x;
+			cbox[3 + d] = y;
+			cbox[6 + d] = nv > 0 ? z / nv : 0;
+		}
+		__syncthreads();
+	};
+#if PINC_PUSH_IMG_GATE
+	// The images differ from the raw cells only for a block whose items
+	// straddle a periodic boundary: with every raw cell within T/2 - 2 of the
+	// reference cell, the pre-move cells and the post-move cells of the
+	// particles that stay in place (one cell of motion) all lie strictly
+	// between the images' bounds, so img() is the identity there.  Such
+	// blocks (nearly all) skip the per-item image arithmetic in the box, the
+	// kick and the deposit; a particle that wrapped in place lands outside
+	// the charge box and adds its weights through memory (the same nodes, a
+	// different summation order).  The others take the raw box first, then
+	// the images' box.
+	cell_box(false);
+	bool useImg = false;
 #pragma unroll
 	for (int d = 0; d < ND; d++) {
-		int x = wave_min_i(lo[d]), y = wave_max_i(hi[d]), z = wave_sum(sm[d]);
-		if (lane == 0) {
-			red[(3 * d) * NW + wv] = x;
-			red[(3 * d + 1) * NW + wv] = y;
-			red[(3 * d + 2) * NW + wv] = z;
-		}
+		const int x = __builtin_amdgcn_readfirstlane(cbox[d]), y = __builtin_amdgcn_readfirstlane(cbox[3 + d]);
+		useImg |= x <= y && (img.lo[d] != INT32_MIN || img.hi[d] != INT32_MAX) &&
+		          (cref[d] - x > G.T[d] / 2 - 2 || y - cref[d] > G.T[d] / 2 - 2);
 	}
-	__syncthreads();
-	if (threadIdx.x < ND) {
-		int d = threadIdx.x, x = INT32_MAX, y = INT32_MIN, z = 0;
-		for (int w = 0; w < NW; w++) {
-			x = min(x, red[(3 * d) * NW + w]);
-			y = max(y, red[(3 * d + 1) * NW + w]);
-			z += red[(3 * d + 2) * NW + w];
-		}
-		const int nv = (int)min((long)kPushChunk, a.n - base);
-		cbox[d] = x;
-		cbox[3 + d] = y;
-		cbox[6 + d] = nv > 0 ? z / nv : 0;
-	}
-	__syncthreads();
+	if (useImg) cell_box(true);
+#else
+	const bool useImg = true;
+	cell_box(true);
+#endif
 	int clo[3] = {0, 0, 0}, chi[3] = {0, 0, 0}, cmid[3] = {0, 0, 0};
 #pragma unroll
 	for (int d = 0; d < ND; d++) {
@@ -2064,6 +2103,11 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	double ke = 0.0;
 	int cnt = 0, bad = 0;
 	unsigned dep = 0;
+#if PINC_PUSH_LEAN
+	bool thrInFrame = true;
+#pragma unroll
+	for (int d = 0; d < ND; d++) thrInFrame &= a.thr.lo[d] >= 0.0 && a.thr.up[d] <= a.thr.hi[d];
+#endif
 #pragma unroll
 	for (int k = 0; k < kPushItems; k++) {
 		if (!((valid >> k) & 1u)) continue;
@@ -2074,9 +2118,13 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 #pragma unroll
 			for (int d = 0; d < ND; d++) {
 				j[d] = (int)p[k][d];
-				jc[d] = img(d, j[d]);
+				jc[d] = j[d];
 				dec[d] = p[k][d] - j[d];
 				comp[d] = 1 - dec[d];
+			}
+			if (useImg) {
+#pragma unroll
+				for (int d = 0; d < ND; d++) jc[d] = img(d, j[d]);
 			}
 			// all 2^ND corners in the staged box: one unsigned compare per
 			// dimension, evaluated without short-circuit branches
@@ -2199,16 +2247,50 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 		}
 		// drift + pVelAssertMax (population.c:342-365)
 		int chg = 0;
+#if PINC_PUSH_LEAN
+		int c0[3] = {0, 0, 0};  // pre-move cell (the statistic below)
+#pragma unroll
+		for (int d = 0; d < ND; d++) c0[d] = (int)p[k][d];
+#endif
 #pragma unroll
 		for (int d = 0; d < ND; d++) {
 			bad |= (vv[k][d] > a.maxVel);
 			p[k][d] += vv[k][d];
 			// cell changed (statistic for the sort schedule; recomputed, not kept)
+#if PINC_PUSH_LEAN
+			chg |= (int)p[k][d] != c0[d];
+#else
 			chg |= (int)p[k][d] != (int)(p[k][d] - vv[k][d]);
+#endif
 		}
 		// neighbour digit per dimension, as k_move_classify
 		int ne = 0;
 		bool outside = false;
+#if PINC_PUSH_LEAN
+		int digs[3] = {1, 1, 1};
+		bool leaves = false;
+#pragma unroll
+		for (int d = 0; d < ND; d++) {
+			digs[d] = 1 - (p[k][d] < a.thr.lo[d]) + (p[k][d] >= a.thr.up[d]);
+			leaves |= digs[d] != 1;
+		}
+		// a particle inside [lo, up) in every dimension is inside the frame
+		// when 0 <= lo and up <= hi (thrInFrame): the frame test and the
+		// in-place wrap only for the few that cross a threshold
+		if (leaves || !thrInFrame) {
+#pragma unroll
+			for (int d = 0; d < ND; d++) {
+				const double q = p[k][d] - (double)(digs[d] - 1) * (a.thr.hi[d] - 1.0);
+				outside |= (q < 0.0 || q > a.thr.hi[d]);
+				if ((a.wrapMask >> d) & 1) {
+					if (digs[d] != 1) p[k][d] = p[k][d] + (double)((1 - digs[d]) * a.thr.T[d]);
+					digs[d] = 1;
+				}
+			}
+		}
+#pragma unroll
+		for (int d = ND - 1; d >= 0; d--) ne = ne * 3 + digs[d];
+#else
 #pragma unroll
 		for (int d = ND - 1; d >= 0; d--) {
 			int dig = 1 - (p[k][d] < a.thr.lo[d]) + (p[k][d] >= a.thr.up[d]);
@@ -2220,6 +2302,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 			}
 			ne = ne * 3 + dig;
 		}
+#endif
 		// pPosAssertInLocalFrame fails for this particle (the host stops the
 		// run with msg(ERROR) before the next deposit): route it to the
 		// emigrant path so that nothing indexes the grid with it
@@ -2396,8 +2479,10 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 		// (x, y wrapped; slab ghost planes when the slab dimension wraps,
 		// folded by the halo add as every ghost deposit) instead of adding
 		// its eight weights to memory
+		if (useImg) {
 #pragma unroll
-		for (int d = 0; d < ND; d++) j[d] = img(d, j[d]);
+			for (int d = 0; d < ND; d++) j[d] = img(d, j[d]);
+		}
 		return kk;
 	};
 	// one wave pass: lanes sharing a cell (up to kPushGroups groups of at
@@ -2645,6 +2730,11 @@ __global__ __launch_bounds__(kThreads) void k_vel_assert(const double *__restric
 
 // =========================================================== C ABI ========
 extern "C" long pinc_hip_push_chunk(void) { return kPushChunk; }
+
+extern "C" int pinc_hip_push_xcd_of_chunks(long nBlocks, int *xcd) {
+	for (long b = 0; b < nBlocks; b++) xcd[push_chunk_of((unsigned)nBlocks, (unsigned)b)] = (int)(b & 7);
+	return 0;
+}
 
 extern "C" int pinc_hip_deposit_ngp(pinc_pop_t pop, int s, pinc_geom_t g, double *rho, void *stream) {
 	long n = pop.iStop[s] - pop.iStart[s];

@@ -239,6 +239,12 @@ static int sock_exchange(void *user, int nOps, const int *sendPeer, const void *
 		if (recvBytes[i] > 0) x[nx++] = (Xfer){recvPeer[i], (char *)recvbuf[i], recvBytes[i], 0};
 	}
 	struct pollfd *q = calloc((size_t)g_nPeer * 2 + 1, sizeof(*q));
+	/* a peer that stays connected but makes no progress for PINC_COMM_TIMEOUT
+	 * seconds (default 300, as the RCCL watchdog; 0 = wait forever) fails the
+	 * exchange instead of hanging every rank */
+	const double stallMax = getenv("PINC_COMM_TIMEOUT") ? atof(getenv("PINC_COMM_TIMEOUT")) : 300.0;
+	struct timespec t0;
+	clock_gettime(CLOCK_MONOTONIC, &t0);
 	for (;;) {
 		/* the first unfinished send and receive of each peer */
 		int nq = 0, busy = 0;
@@ -255,13 +261,26 @@ static int sock_exchange(void *user, int nOps, const int *sendPeer, const void *
 			nq++;
 		}
 		if (!busy) break;
-		if (poll(q, nq, 1000) < 0 && errno != EINTR) {
+		int ready = poll(q, nq, 1000);
+		if (ready < 0 && errno != EINTR) {
+			free(q);
+			free(x);
+			return 1;
+		}
+		struct timespec t1;
+		clock_gettime(CLOCK_MONOTONIC, &t1);
+		if (ready > 0) t0 = t1;
+		else if (stallMax > 0 && (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec) > stallMax) {
+			fprintf(stderr, "[pinc] rank %d: host transport exchange made no progress for %.0f s (PINC_COMM_TIMEOUT)\n",
+			        me, stallMax);
 			free(q);
 			free(x);
 			return 1;
 		}
 		for (int j = 0; j < nq; j++) {
-			if (q[j].revents & (POLLERR | POLLNVAL)) {
+			/* a hang-up with sends still pending can never complete them */
+			if ((q[j].revents & (POLLERR | POLLNVAL)) ||
+			    ((q[j].revents & POLLHUP) && (q[j].events & POLLOUT) && !(q[j].revents & POLLOUT))) {
 				free(q);
 				free(x);
 				return 1;

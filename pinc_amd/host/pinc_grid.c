@@ -92,6 +92,15 @@ void gFreeMpi(MpiInfo *m) {
 	free(m);
 }
 
+static PincDevGrid *g_live;          /* allocated grids (pinc_grid_live) */
+static unsigned long long g_serial;
+
+int pinc_grid_live(const Grid *g, unsigned long long serial) {
+	for (const PincDevGrid *d = g_live; d; d = d->liveNext)
+		if (d->serial == serial) return g->dev == d;
+	return 0;
+}
+
 Grid *gAlloc(const dictionary *ini, int nValues) {
 	pinc_geom_t geo = pinc_geom_current();
 	int nd = iniGetInt(ini, "grid:nDims");
@@ -139,6 +148,9 @@ Grid *gAlloc(const dictionary *ini, int nValues) {
 		pinc_check(pinc_hip_malloc((void **)&dv->recv[0], dv->planeSize * nValues * sizeof(double)), "halo buf");
 		pinc_check(pinc_hip_malloc((void **)&dv->recv[1], dv->planeSize * nValues * sizeof(double)), "halo buf");
 	}
+	dv->serial = ++g_serial;
+	dv->liveNext = g_live;
+	g_live = dv;
 	g->dev = dv;
 	return g;
 }
@@ -146,6 +158,11 @@ Grid *gAlloc(const dictionary *ini, int nValues) {
 void gFree(Grid *g) {
 	if (!g) return;
 	if (g->dev) {
+		for (PincDevGrid **l = &g_live; *l; l = &(*l)->liveNext)
+			if (*l == g->dev) {
+				*l = g->dev->liveNext;
+				break;
+			}
 		pinc_hip_free(g->dev->d);
 		if (g->dev->ownsGlobal) pinc_hip_free(g->dev->global);
 		pinc_hip_free(g->dev->recv[0]);
@@ -277,6 +294,7 @@ void gHaloOp(funPtr sliceOp, Grid *grid, const MpiInfo *mpiInfo, opDirection dir
 		/* main.c:232's second fold of one deposit (main.c:226 was the first) */
 		if (dv->depPop && dv->folds == 1 && !geo.literal) pinc_literal_second_fold(dv->depPop, grid, dv->depOrder);
 		dv->folds++;
+		pinc_grid_touch(grid);
 		if (g_pinc.nranks == 1) {
 			pinc_check(pinc_hip_fold_self(dv->d, geo, g_pinc.stream), "fold");
 		} else {
@@ -291,6 +309,7 @@ void gHaloOp(funPtr sliceOp, Grid *grid, const MpiInfo *mpiInfo, opDirection dir
 	}
 	if (sliceOp == (funPtr)setSlice && dir == TOHALO) {
 		if (dv->ghostsValid) return;
+		pinc_grid_touch(grid);
 		if (dv->global) {
 			pinc_check(pinc_hip_slab_from_global(dv->d, dv->global, geo, dv->nValues, g_pinc.stream),
 			           "slab from global");
@@ -314,6 +333,7 @@ void gHaloOp(funPtr sliceOp, Grid *grid, const MpiInfo *mpiInfo, opDirection dir
 }
 
 void gFinDiff1st(const Grid *scalar, Grid *field) {
+	pinc_grid_touch(field);
 	if (scalar->dev->ext) {
 		/* sharded multigrid: the extended slab holds planes off-hz .. of the
 		 * potential, every plane E reads exact (pinc_mg.c) */
@@ -339,16 +359,19 @@ void gFinDiff1st(const Grid *scalar, Grid *field) {
 }
 
 void gMul(Grid *grid, double num) {
+	pinc_grid_touch(grid);
 	pinc_check(pinc_hip_scale(grid->dev->d, grid->dev->n, num, g_pinc.stream), "gMul");
 }
 
 void gZero(Grid *grid) {
+	pinc_grid_touch(grid);
 	pinc_check(pinc_hip_zero(grid->dev->d, grid->dev->n, g_pinc.stream), "gZero");
 	grid->dev->ghostsValid = 0;
 	grid->dev->depPop = NULL;
 }
 
 void gAddTo(Grid *result, Grid *addition) {
+	pinc_grid_touch(result);
 	pinc_check(pinc_hip_add(result->dev->d, addition->dev->d, result->dev->n, g_pinc.stream), "gAddTo");
 }
 
@@ -441,6 +464,7 @@ void gSyncToHost(Grid *grid) {
 
 void gSyncToDevice(Grid *grid) {
 	PincDevGrid *dv = grid->dev;
+	pinc_grid_touch(grid);
 	if (!grid->val) msg(ERROR, "gSyncToDevice without host values");
 	int rank = grid->rank, nd = rank - 1, nv = dv->nValues;
 	double *tmp = malloc(dv->n * sizeof(double));

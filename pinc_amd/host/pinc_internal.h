@@ -103,6 +103,7 @@ struct PincDevPop {
 	int everSorted;                     /* input already in cell order once */
 	int permId[PINC_MAX_SPECIES];       /* species s left in order by the pending sorting push */
 	Grid *pendingE;                     /* E of the pending push's kick (pinc_pending_vel) */
+	unsigned long long pendingESerial, pendingEGen; /* ... its serial and write count then */
 	/* adaptive sort schedule (population:sortFraction > 0): a species is
 	 * sorted once the fraction of its particles that left their cell since
 	 * its last sort would pass sortFraction, at most sortMax pushes apart */
@@ -163,7 +164,16 @@ struct PincDevGrid {
 	const Population *depPop;
 	int depOrder, folds;
 	double *lit;
+	/* writes of d since gAlloc, and a process-unique id with the list of live
+	 * grids: a pending sorting push checks that its E is the one it kicked
+	 * with (pinc_pending_vel) */
+	unsigned long long gen, serial;
+	PincDevGrid *liveNext;
 };
+/* d was (or is about to be) rewritten */
+static inline void pinc_grid_touch(Grid *g) { g->dev->gen++; }
+/* the grid is allocated and is the one with this serial */
+int pinc_grid_live(const Grid *g, unsigned long long serial);
 
 /* immersed objects (pinc_obj.c; object.c, config C5) */
 PincObj *pinc_obj_create(const dictionary *ini, const Grid *rho);

@@ -262,17 +262,18 @@ static void push_phase_report(const unsigned long long *dts, const unsigned long
 	if (sort)
 		fprintf(stderr, "[pinc]   sort sub-phases us per block: rank loop %.2f, reservation %.2f\n",
 		        dg[4] / (double)nb * 1e-2, ph[2] / nb * 1e-2 - dg[4] / (double)nb * 1e-2);
-	/* per XCD (the push deals chunks [x q + min(x, r), ...) to XCD x): span
-	 * from its first block's start to its last block's end, and the mean
-	 * number of its blocks between their first and last timestamp */
+	/* per XCD (chunk c runs on XCD xcd[c], the push's own placement map):
+	 * span from its first block's start to its last block's end, and the
+	 * mean number of its blocks between their first and last timestamp */
 	if (g_pinc.traceSort > 2) {
-		const int q = nb / 8, r = nb % 8;
+		int *xcd = malloc((size_t)nb * sizeof(int));
+		pinc_check(pinc_hip_push_xcd_of_chunks(nb, xcd), "push xcd map");
 		fprintf(stderr, "[pinc]   xcd span ms / blocks in flight:");
 		for (int x = 0; x < 8; x++) {
-			const int c0 = x * q + (x < r ? x : r), c1 = c0 + q + (x < r);
 			unsigned long long a0 = ~0ull, a1 = 0;
 			double life = 0;
-			for (int b = c0; b < c1; b++) {
+			for (int b = 0; b < nb; b++) {
+				if (xcd[b] != x) continue;
 				if (t[b * 8] < a0) a0 = t[b * 8];
 				if (t[b * 8 + 7] > a1) a1 = t[b * 8 + 7];
 				life += (double)(t[b * 8 + 7] - t[b * 8]);
@@ -280,6 +281,7 @@ static void push_phase_report(const unsigned long long *dts, const unsigned long
 			fprintf(stderr, " %.2f/%.0f", (a1 - a0) * 1e-5, a1 > a0 ? life / (double)(a1 - a0) : 0.0);
 		}
 		fprintf(stderr, "\n");
+		free(xcd);
 		/* block lifetime percentiles (first to last timestamp) */
 		double *lv = malloc((size_t)nb * sizeof(*lv));
 		for (int b = 0; b < nb; b++) lv[b] = (double)(t[b * 8 + 7] - t[b * 8]) * 1e-2;
@@ -563,6 +565,9 @@ void pinc_pending_vel(const Population *pop, int s, double *const *dst) {
 	}
 	if (dv->permId[s]) return;
 	if (!dv->pendingE) msg(ERROR, "pending sorted push without its E");
+	if (!pinc_grid_live(dv->pendingE, dv->pendingESerial) || dv->pendingE->dev->gen != dv->pendingEGen)
+		msg(ERROR, "E was changed or freed between puAcc and a read of the pending sorting push's velocities "
+		           "(read or extract the population before writing E)");
 	PincDevGrid *eg = dv->pendingE->dev;
 	pinc_check(pinc_hip_field_chain(eg->d, eg->scaled, eg->n, dv->qm, dv->mq, 1.0, s, g_pinc.stream), "E chain");
 	pinc_pop_t p = pinc_devpop(pop);
@@ -945,6 +950,8 @@ static void acc(Population *pop, Grid *E, int ke) {
 		dv->pendingSorted = push_all(pop, E, dv->altX);
 		dv->pending = 1;
 		dv->pendingE = E;
+		dv->pendingESerial = E->dev->serial;
+		dv->pendingEGen = E->dev->gen;
 		dv->flagsValid = 0;
 		if (ke) {
 			double sums[PINC_MAX_SPECIES];

@@ -148,3 +148,16 @@ def test_bench_config_sort_spread():
     gated = configs.bench_config("c4ts", 32, 4, sort_spread=2.0)
     assert gated["population"]["sortSpread"] == "2.0"
     assert "sortSpread" not in configs.bench_config("c4", 32, 4, layout="reference")["population"]
+
+
+@pytest.mark.parametrize("nb", [1, 7, 512, 513, 1048576, 1048576 + 300])
+def test_push_chunk_placement_is_a_bijection(lib, nb):
+    """The push's chunk -> XCD placement (push_chunk_of, shared by the kernel
+    and the trace's per-XCD attribution): every chunk is taken by
+    exactly one block and each XCD gets its share (host function, no GPU)."""
+    xcd = np.full(nb, -1, dtype=np.int32)
+    lib.HIP.pinc_hip_push_xcd_of_chunks.argtypes = [C.c_long, C.c_void_p]
+    assert lib.HIP.pinc_hip_push_xcd_of_chunks(nb, xcd.ctypes.data) == 0
+    assert xcd.min() >= 0 and xcd.max() <= 7
+    counts = np.bincount(xcd, minlength=8)
+    assert counts.max() - counts.min() <= 1, counts
