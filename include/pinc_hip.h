@@ -77,6 +77,14 @@ int pinc_hip_memset(void *ptr, int value, unsigned long bytes, void *stream);
 int pinc_hip_h2d(void *dst, const void *src, unsigned long bytes, void *stream);
 int pinc_hip_d2h(void *dst, const void *src, unsigned long bytes, void *stream);
 int pinc_hip_d2d(void *dst, const void *src, unsigned long bytes, void *stream);
+/* asynchronous device-to-host copy (dst: pinned memory from
+ * pinc_hip_host_alloc), complete once an event recorded after it is
+ * (pinc_hip_event_sync): the host keeps enqueueing work meanwhile (the
+ * multigrid's per-cycle norm, pinc_mg.c) */
+int pinc_hip_d2h_async(void *dst, const void *src, unsigned long bytes, void *stream);
+int pinc_hip_host_alloc(void **ptr, unsigned long bytes);
+int pinc_hip_host_free(void *ptr);
+int pinc_hip_event_sync(void *ev);
 /* events for per-phase device timing (replaces Timer, aux.c:48-85) */
 int pinc_hip_event_create(void **ev);
 int pinc_hip_event_destroy(void *ev);

@@ -153,6 +153,29 @@ extern "C" int pinc_hip_d2h(void *dst, const void *src, unsigned long bytes, voi
 	return 0;
 }
 
+extern "C" int pinc_hip_d2h_async(void *dst, const void *src, unsigned long bytes, void *stream) {
+	if (!bytes) return 0;
+	HIPCALL(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, (hipStream_t)stream), "d2h async");
+	return 0;
+}
+
+extern "C" int pinc_hip_host_alloc(void **ptr, unsigned long bytes) {
+	if (bytes == 0) bytes = 16;
+	HIPCALL(hipHostMalloc(ptr, bytes, hipHostMallocDefault), "hipHostMalloc");
+	return 0;
+}
+
+extern "C" int pinc_hip_host_free(void *ptr) {
+	if (!ptr) return 0;
+	HIPCALL(hipHostFree(ptr), "hipHostFree");
+	return 0;
+}
+
+extern "C" int pinc_hip_event_sync(void *ev) {
+	HIPCALL(hipEventSynchronize((hipEvent_t)ev), "hipEventSynchronize");
+	return 0;
+}
+
 extern "C" int pinc_hip_d2d(void *dst, const void *src, unsigned long bytes, void *stream) {
 	if (!bytes) return 0;
 	HIPCALL(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream), "d2d");

@@ -158,6 +158,7 @@ Grid *gAlloc(const dictionary *ini, int nValues) {
 void gFree(Grid *g) {
 	if (!g) return;
 	if (g->dev) {
+		pinc_grid_touch(g); /* a pending sorting push that kicked with it lets go first */
 		for (PincDevGrid **l = &g_live; *l; l = &(*l)->liveNext)
 			if (*l == g->dev) {
 				*l = g->dev->liveNext;

@@ -102,6 +102,8 @@ struct PincDevPop {
 	int cntValid[PINC_MAX_SPECIES];
 	int everSorted;                     /* input already in cell order once */
 	int permId[PINC_MAX_SPECIES];       /* species s left in order by the pending sorting push */
+	int vKicked[PINC_MAX_SPECIES];      /* p.v of species s holds the pending push's kicked velocities
+	                                       (materialised before its E was written, pinc_grid_touch) */
 	Grid *pendingE;                     /* E of the pending push's kick (pinc_pending_vel) */
 	unsigned long long pendingESerial, pendingEGen; /* ... its serial and write count then */
 	/* adaptive sort schedule (population:sortFraction > 0): a species is
@@ -170,8 +172,12 @@ struct PincDevGrid {
 	unsigned long long gen, serial;
 	PincDevGrid *liveNext;
 };
-/* d was (or is about to be) rewritten */
-static inline void pinc_grid_touch(Grid *g) { g->dev->gen++; }
+/* d is about to be rewritten: a pending sorting push that kicked with this
+ * grid first materialises its kicked velocities (pinc_pusher.c) */
+void pinc_grid_touch(Grid *g);
+/* populations whose pending sorting push may need its E (pinc_pusher.c) */
+void pinc_pending_register(Population *pop);
+void pinc_pending_unregister(Population *pop);
 /* the grid is allocated and is the one with this serial */
 int pinc_grid_live(const Grid *g, unsigned long long serial);
 
@@ -241,6 +247,18 @@ struct MultigridSolver {
 	int z0;                        /* global plane of extended plane 0 */
 	double *rho1Slab;              /* this rank's level-1 planes before the all-gather */
 	pinc_lvl_t L1s;
+	/* the per-cycle norm read without idling the GPU (mgSolve): the norm
+	 * goes to pinned memory asynchronously and, while the host waits for
+	 * it, the next cycle's first double sweep (phi -> res, which leaves phi
+	 * untouched) is already queued; preDone tells that cycle's pre-smoothing
+	 * the sweep is done.  Only when the last solve of this role needed more
+	 * cycles than have run (lastCycles), so a converged solve rarely leaves a
+	 * sweep unused.  (multigrid:speculate, default 1; native, replicated, no
+	 * graph.) */
+	int speculate, preDone;
+	long lastCycles[4];
+	double *hostNorm;
+	void *normEvent;
 };
 
 /* collectives over RCCL or the host transport (pinc_comm.c) */

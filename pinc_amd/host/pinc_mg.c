@@ -222,6 +222,14 @@ MultigridSolver *mgAllocSolver(const dictionary *ini, Grid *rho, Grid *phi) {
 		} else if (strcmp(v, "response")) msg(ERROR, "objects:secondGuess = %s (spectral | response)", v);
 		free(v);
 	}
+	/* (PINC_MG_SPECULATE=0 overrides the ini: A/B runs of the bench) */
+	S->speculate = S->native && !S->shard && !S->useGraph && S->nLevels > 1 &&
+	               (!iniHas(ini, "multigrid:speculate") || iniGetInt(ini, "multigrid:speculate")) &&
+	               !(getenv("PINC_MG_SPECULATE") && !atoi(getenv("PINC_MG_SPECULATE")));
+	if (S->speculate) {
+		pinc_check(pinc_hip_host_alloc((void **)&S->hostNorm, sizeof(double)), "mg norm");
+		pinc_check(pinc_hip_event_create(&S->normEvent), "mg norm");
+	}
 	if (S->native && S->nLevels >= 2 && iniHas(ini, "multigrid:spectralCoarse") &&
 	    iniGetInt(ini, "multigrid:spectralCoarse")) {
 		pinc_check(pinc_hip_fft_create(&S->fftCoarse, S->L[1].nd, S->L[1].T, g_pinc.stream), "mg spectral coarse");
@@ -262,6 +270,8 @@ void mgFreeSolver(MultigridSolver *S) {
 	pinc_hip_fft_destroy(S->fft);
 	pinc_hip_fft_slab_destroy(S->fftSlab);
 	pinc_hip_fft_destroy(S->fftCoarse);
+	pinc_hip_host_free(S->hostNorm);
+	if (S->normEvent) pinc_hip_event_destroy(S->normEvent);
 	free(S->hist);
 	for (int q = 0; q < S->nLevels; q++) {
 		if (q > 0 || S->shard) {
@@ -438,6 +448,13 @@ static void smooth_native(MultigridSolver *S, int q, int nIter, int nd3) {
 	/* two iterations per launch (pinc_hip_gs_sweep2x) in pairs, so that the
 	 * ping-pong ends in phi */
 	int fused2 = fused && L.T[0] % 32 == 0 && L.T[1] % 8 == 0;
+	if (q == 0 && S->preDone) {
+		/* the first double sweep ran while the host read the last cycle's
+		 * norm (mgSolve), and its ping-pong swap is applied */
+		if (!(fused2 && !S->shard && nIter >= 2)) msg(ERROR, "mg: a speculative sweep the smoothing cannot use");
+		S->preDone = 0;
+		k = 2;
+	}
 	if (fused2 && !(q == 0 && S->shard)) {
 		/* one launch per two iterations, phi[q] -> res[q], then the pointers
 		 * swap (round 4: a smoothing of 10 is five double sweeps instead of
@@ -478,6 +495,15 @@ static void smooth_native(MultigridSolver *S, int q, int nIter, int nd3) {
 			           "gs pass");
 		}
 	}
+}
+
+/* level 0's pre-smoothing opens with one pinc_hip_gs_sweep2x phi -> res
+ * (smooth_native's fused2 branch): the sweep mgSolve may queue ahead */
+static int first_sweep_is_double(const MultigridSolver *S) {
+	const pinc_lvl_t L = S->L[0];
+	if (!S->native || S->shard || S->nPre < 2 || !S->pre3d) return 0;
+	int fused = L.nd == 3 && L.T[0] % 16 == 0 && L.T[1] % 16 == 0 && L.T[2] % 16 == 0 && S->N[0] >= S->fusedMin;
+	return fused && L.T[0] % 32 == 0 && L.T[1] % 8 == 0;
 }
 
 /* the iterate back into phi[q]'s own buffer after a swapped smoothing */
@@ -648,7 +674,26 @@ void mgSolve(MultigridSolver *S, Grid *rho, Grid *phi, const MpiInfo *mpiInfo) {
 				pinc_check(pinc_hip_reduce(g_pinc.dScratch, nb, 1.0, PINC_SLOT(TMP_SLOT + 1), g_pinc.stream), "norm");
 			}
 			double sum = 0;
-			pinc_check(pinc_hip_d2h(&sum, PINC_SLOT(TMP_SLOT + 1), sizeof(double), g_pinc.stream), "norm");
+			int spec = 0;
+			if (S->speculate) {
+				/* the norm to pinned memory; while the host waits for it, the
+				 * next cycle's first double sweep (phi -> res: phi untouched)
+				 * runs if the last solve of this role needed another cycle */
+				pinc_check(pinc_hip_d2h_async(S->hostNorm, PINC_SLOT(TMP_SLOT + 1), sizeof(double), g_pinc.stream),
+				           "norm");
+				pinc_check(pinc_hip_event_record(S->normEvent, g_pinc.stream), "norm");
+				spec = first_sweep_is_double(S) && c + 1 < S->lastCycles[role & 3] && !S->swapped[0];
+				if (spec) {
+					int gslot = pinc_probe_begin(PINC_PROBE_GS);
+					pinc_check(pinc_hip_gs_sweep2x(S->phi[0], S->res[0], S->rho[0], S->L[0], g_pinc.stream),
+					           "gs sweep2x (ahead)");
+					pinc_probe_end(PINC_PROBE_GS, gslot, 24.0 * S->N[0]);
+				}
+				pinc_check(pinc_hip_event_sync(S->normEvent), "norm");
+				sum = *S->hostNorm;
+			} else {
+				pinc_check(pinc_hip_d2h(&sum, PINC_SLOT(TMP_SLOT + 1), sizeof(double), g_pinc.stream), "norm");
+			}
 			barRes = sqrt(sum / S->Ng0);
 			if (S->histN < S->histCap) S->hist[S->histN] = barRes;
 			S->histN++;
@@ -667,7 +712,18 @@ void mgSolve(MultigridSolver *S, Grid *rho, Grid *phi, const MpiInfo *mpiInfo) {
 				        g_pinc.rank, c, barRes);
 				break;
 			}
+			if (spec && barRes > 1.E-10) {
+				/* another cycle: its first double sweep is done (the
+				 * smoothing's ping-pong swap now) */
+				double *t = S->phi[0];
+				S->phi[0] = S->res[0];
+				S->res[0] = t;
+				S->swapped[0] ^= 1;
+				S->preDone = 1;
+			}
 		}
+		S->preDone = 0;
+		S->lastCycles[role & 3] = c;
 		if (S->native) neutralize_level(S, 0, S->phi[0]);
 	} else {
 		for (int c = 0; c < S->mgCycles; c++) {

@@ -208,6 +208,7 @@ void pPosAssertInLocalFrame(const Population *pop, const Grid *grid) {
 void pFree(Population *p) {
 	if (!p) return;
 	PincDevPop *dv = p->dev;
+	pinc_pending_unregister(p);
 	if (dv) {
 		/* main.c:297-298 frees the population before the objects */
 		if (dv->objOwner) pinc_obj_forget_pop(dv->objOwner);

@@ -563,11 +563,11 @@ void pinc_pending_vel(const Population *pop, int s, double *const *dst) {
 		if (dst[d] != src)
 			pinc_check(pinc_hip_d2d(dst[d], src, n * sizeof(double), g_pinc.stream), "pending velocities");
 	}
-	if (dv->permId[s]) return;
+	if (dv->permId[s] || dv->vKicked[s]) return;
 	if (!dv->pendingE) msg(ERROR, "pending sorted push without its E");
 	if (!pinc_grid_live(dv->pendingE, dv->pendingESerial) || dv->pendingE->dev->gen != dv->pendingEGen)
-		msg(ERROR, "E was changed or freed between puAcc and a read of the pending sorting push's velocities "
-		           "(read or extract the population before writing E)");
+		msg(ERROR, "internal: E was changed or freed between puAcc and a re-kick of the pending sorting push "
+		           "(pinc_grid_touch missed a write)");
 	PincDevGrid *eg = dv->pendingE->dev;
 	pinc_check(pinc_hip_field_chain(eg->d, eg->scaled, eg->n, dv->qm, dv->mq, 1.0, s, g_pinc.stream), "E chain");
 	pinc_pop_t p = pinc_devpop(pop);
@@ -575,6 +575,47 @@ void pinc_pending_vel(const Population *pop, int s, double *const *dst) {
 	for (int d = 0; d < nd; d++) p.v[d] = dst[d] - a;
 	int nb = 0;
 	pinc_check(pinc_hip_accelerate(p, s, eg->geom, eg->scaled, dv->kePartial, &nb, g_pinc.stream), "pending kick");
+}
+
+/* The populations with a pending fused push (main.c has one).  Before a
+ * grid is written, a pending sorting push that kicked with it re-applies its
+ * kick to the unkicked velocities in place (p.v, in the current order), so
+ * that a later read or a dropped move does not need that E any more: main.c's
+ * initial half step rescales E right after puAcc (gMul(E, 2), main.c:183-185),
+ * and a read of the population after it must see the half kick. */
+static Population *g_pendPop[8];
+
+void pinc_pending_register(Population *pop) {
+	for (int i = 0; i < 8; i++)
+		if (g_pendPop[i] == pop) return;
+	for (int i = 0; i < 8; i++)
+		if (!g_pendPop[i]) {
+			g_pendPop[i] = pop;
+			return;
+		}
+	msg(ERROR, "more than 8 populations with pending pushes");
+}
+
+void pinc_pending_unregister(Population *pop) {
+	for (int i = 0; i < 8; i++)
+		if (g_pendPop[i] == pop) g_pendPop[i] = NULL;
+}
+
+void pinc_grid_touch(Grid *g) {
+	for (int i = 0; i < 8; i++) {
+		Population *pop = g_pendPop[i];
+		if (!pop) continue;
+		PincDevPop *dv = pop->dev;
+		if (!dv->pending || !dv->pendingSorted || dv->pendingE != g) continue;
+		for (int s = 0; s < pop->nSpecies; s++) {
+			if (dv->permId[s] || dv->vKicked[s]) continue;
+			double *dst[3] = {NULL, NULL, NULL};
+			for (int d = 0; d < pop->nDims; d++) dst[d] = dv->p.v[d] + pop->iStart[s];
+			pinc_pending_vel(pop, s, dst);
+			dv->vKicked[s] = 1;
+		}
+	}
+	g->dev->gen++;
 }
 
 static void swap_pos(PincDevPop *dv, int nd, int vel) {
@@ -948,6 +989,8 @@ static void acc(Population *pop, Grid *E, int ke) {
 		if (!dv->sorted) maybe_sort(pop);
 		dv->pending = 0;
 		dv->pendingSorted = push_all(pop, E, dv->altX);
+		for (int s = 0; s < PINC_MAX_SPECIES; s++) dv->vKicked[s] = 0;
+		pinc_pending_register(pop);
 		dv->pending = 1;
 		dv->pendingE = E;
 		dv->pendingESerial = E->dev->serial;

@@ -51,26 +51,6 @@ def single(kind: str, layout: str, fused: int) -> int:
     return 0
 
 
-def stale_e() -> int:
-    """A fused puAcc whose push sorts leaves the kicked velocities to be
-    re-derived from its E (pinc_pending_vel).  Writing E before reading the
-    population must stop with msg(ERROR) instead of returning velocities
-    kicked by the new E."""
-    from pinc_amd import Sim, configs
-    cfg = _cfg("tiled", 1)
-    cfg["population"]["sortInterval"] = "1"
-    ini = configs.write_ini(cfg)
-    with Sim(ini) as s:
-        s.init()
-        s.op("acc")
-        E = s.grid(2)
-        s.set_grid(2, E * 2.0)
-        s.particles(0)
-    os.unlink(ini)
-    print("REACHED-END", flush=True)
-    return 0
-
-
 def overflow() -> int:
     """Two z-slabs; population:nAlloc equals the initial count, so a rank has
     no room for a single net immigrant.  Every species-0 particle of rank 1
@@ -103,14 +83,12 @@ def overflow() -> int:
 
 def main() -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("kind", choices=["maxvel", "frame", "overflow", "stale_e"])
+    ap.add_argument("kind", choices=["maxvel", "frame", "overflow"])
     ap.add_argument("--layout", default="reference")
     ap.add_argument("--fused", type=int, default=1)
     a = ap.parse_args()
     if a.kind == "overflow":
         return overflow()
-    if a.kind == "stale_e":
-        return stale_e()
     return single(a.kind, a.layout, a.fused)
 
 

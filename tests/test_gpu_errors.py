@@ -48,16 +48,6 @@ def test_particle_outside_local_frame_stops_run(built, layout, fused):
     assert "ERROR" in r.stderr and "out of bounds" in r.stderr, r.stderr[-800:]
 
 
-@pytest.mark.gpu
-def test_pending_sorting_push_with_changed_e_stops_run(built):
-    """pinc_pending_vel re-applies a sorting push's kick from its E: an E
-    written between puAcc and the read is detected (write count and identity
-    of the grid) and stops the run."""
-    r = _run(["stale_e"])
-    assert r.returncode != 0 and "REACHED-END" not in r.stdout, (r.stdout[-800:], r.stderr[-800:])
-    assert "ERROR" in r.stderr and "E was changed or freed" in r.stderr, r.stderr[-800:]
-
-
 def _port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))

@@ -203,3 +203,38 @@ def test_extrapolated_guess_matches_oracle(layout, coarse):
     finally:
         for f in (ini_plain, ini_o, ini_g):
             os.unlink(f)
+
+
+def test_speculative_first_sweep_is_bit_identical():
+    """multigrid:speculate (default on): while the host reads a cycle's
+    norm, the next cycle's first double sweep (phi -> res) already runs when
+    the last solve of the same role needed more cycles.  A sequence of solves
+    whose cycle counts go up and down (so some sweeps ahead are used and some
+    dropped) gives bit-identical potentials and residual histories to the
+    synchronous loop."""
+    from pinc_amd import configs
+    from pinc_amd.sim import Sim
+    rhos = [mg_history.make_rho(128, seed, amp) for seed, amp in
+            [(1, 1.0), (1, 1.0), (2, 1.0), (3, 1e-3), (4, 10.0), (4, 10.0), (5, 1.0)]]
+    out = {}
+    for spec in ("0", "1"):
+        cfg = configs.config("warm", true_size=(128, 128, 128), ppc=1, nalloc_pc=2, levels=5)
+        cfg["multigrid"].update({"native": "1", "extrapolate": "1", "spectralCoarse": "1", "speculate": spec})
+        ini = configs.write_ini(cfg)
+        try:
+            with Sim(ini, perturb=False) as s:
+                s.mg_limit(0, 100)
+                hist, phis = [], []
+                for r in rhos:
+                    s.set_grid(0, r)
+                    s.op("solve")
+                    hist.append(s.mg_history().tolist())
+                    phis.append(s.grid(1)[1:-1, 1:-1, 1:-1].copy())
+        finally:
+            os.unlink(ini)
+        out[spec] = (hist, phis)
+    counts = [len(h) for h in out["1"][0]]
+    assert len(set(counts)) > 1, counts           # the counts vary
+    assert out["0"][0] == out["1"][0]
+    for a, b in zip(out["0"][1], out["1"][1]):
+        assert np.array_equal(a, b)

@@ -292,6 +292,38 @@ def test_tiled_layout(sim_cls, name, kw, maxwell, sched):
                 assert s.count(sp) == w.count(sp)
 
 
+@pytest.mark.parametrize("then", ["read", "drop"])
+def test_pending_sorting_push_survives_an_e_write(sim_cls, then):
+    """a sorting puAcc leaves the move pending and re-derives the
+    kicked velocities from its E on demand.  main.c rescales E right after
+    the initial half-step puAcc (gMul(E, 2.0)); any such write of E first
+    materialises the pending kick (pinc_grid_touch), so reading the
+    population afterwards, or dropping the move, gives the velocities of the
+    E the push kicked with -- bit-identical to a run without the write
+    (tools/debug/pending_e.py compares both with the unfused operators)."""
+    cfg = configs.config("warm", **_WARM32)
+    cfg["population"].update({"layout": "tiled", "sortInterval": "1", "fused": "1"})
+    ini = configs.write_ini(cfg)
+    out = []
+    for write in (False, True):
+        with sim_cls(ini, maxwell=True, perturb=False, seed=11) as s:
+            s.init()
+            s.op("acc")
+            if write:
+                s.set_grid(2, s.grid(2) * 2.0)
+            if then == "drop":
+                s.op("extract")
+            out.append([s.particles(sp) for sp in range(2)])
+    # (as sets, by position then velocity: the sorting pushes of the two runs
+    # order particles sharing a lattice site arbitrarily)
+    for sp in range(2):
+        (p0, v0), (p1, v1) = out[0][sp], out[1][sp]
+        o0 = np.lexsort(np.vstack([v0.T[::-1], p0.T[::-1]]))
+        o1 = np.lexsort(np.vstack([v1.T[::-1], p1.T[::-1]]))
+        np.testing.assert_array_equal(p0[o0], p1[o1])
+        np.testing.assert_array_equal(v0[o0], v1[o1])
+
+
 def test_pending_sorting_push_read_and_dropped(sim_cls):
     """A fused puAcc whose push sorts (tiled layout, sortInterval 1) leaves
     the move pending with the kicked velocities in slot order.  Reading the
