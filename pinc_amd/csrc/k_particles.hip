@@ -380,6 +380,40 @@ constexpr int kDepItems = 16;
 constexpr int kDepChunk = kThreads * kDepItems;
 constexpr int kDepCap = 4096;  // LDS nodes per workgroup (32 KiB)
 
+// Integer wave reductions with DPP (row shifts 1, 2, 4, 8, then the row
+// broadcasts of lanes 15 and 31): six VALU instructions with DPP operands and
+// one readlane, the total uniform.  (The shfl_xor butterflies they replace
+// cost six ds_bpermute round trips through the LDS unit each: in the push,
+// where nine reductions per block ran that way, a third of its LDS
+// instructions.)  Every lane of the wave must be active.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ int dpp_i(int old, int v) {
+	return __builtin_amdgcn_update_dpp(old, v, CTRL, ROWS, 0xf, false);
+}
+template <typename Op>
+__device__ __forceinline__ int wave_reduce_i(int v, int id, Op op) {
+	v = op(v, dpp_i<0x111, 0xf>(id, v));  // row_shr:1
+	v = op(v, dpp_i<0x112, 0xf>(id, v));  // row_shr:2
+	v = op(v, dpp_i<0x114, 0xf>(id, v));  // row_shr:4
+	v = op(v, dpp_i<0x118, 0xf>(id, v));  // row_shr:8 (lane 15 of a row: its total)
+	v = op(v, dpp_i<0x142, 0xa>(id, v));  // row_bcast:15 into rows 1, 3
+	v = op(v, dpp_i<0x143, 0xc>(id, v));  // row_bcast:31 into rows 2, 3
+	return __builtin_amdgcn_readlane(v, 63);
+}
+#ifndef PINC_DPP_REDUCE
+#define PINC_DPP_REDUCE 1
+#endif
+#if PINC_DPP_REDUCE
+__device__ __forceinline__ int wave_min_i(int v) {
+	return wave_reduce_i(v, INT32_MAX, [](int a, int b) { return min(a, b); });
+}
+__device__ __forceinline__ int wave_max_i(int v) {
+	return wave_reduce_i(v, INT32_MIN, [](int a, int b) { return max(a, b); });
+}
+__device__ __forceinline__ int wave_sum_i(int v) {
+	return wave_reduce_i(v, 0, [](int a, int b) { return a + b; });
+}
+#else
 __device__ __forceinline__ int wave_min_i(int v) {
 #pragma unroll
 	for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
@@ -390,6 +424,8 @@ __device__ __forceinline__ int wave_max_i(int v) {
 	for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
 	return v;
 }
+__device__ __forceinline__ int wave_sum_i(int v) { return wave_sum(v); }
+#endif
 
 template <int ND, bool V3D>
 __device__ __forceinline__ void cic_weights(const double *dec, const double *comp, double *w) {
@@ -1591,6 +1627,41 @@ struct Box {
 		}
 	}
 };
+// Box coordinates of linear index l < vol without integer division: the
+// block-uniform reciprocals of the extents (box_rcp) and one float multiply
+// per dimension.  (l + 0.5) / n lies at least 0.5 / n from an integer and
+// the float product errs by less than 2^-12 for l < 2^11 (the boxes hold at
+// most 2048 nodes, extents <= 2 kBoxReach + 4), so the quotient is exact.
+struct BoxRcp {
+	float r[3];
+};
+__device__ __forceinline__ BoxRcp box_rcp(const Box &b) {
+	BoxRcp q;
+#pragma unroll
+	for (int d = 0; d < 3; d++) q.r[d] = 1.0f / (float)b.n[d];
+	return q;
+}
+#ifndef PINC_PUSH_FASTDIV
+#define PINC_PUSH_FASTDIV 1
+#endif
+__device__ __forceinline__ void box_coords(const Box &b, const BoxRcp &q, int l, int *c, int nd) {
+#if !PINC_PUSH_FASTDIV
+	(void)q;
+	b.coords(l, c, nd);
+	return;
+#endif
+#pragma unroll
+	for (int d = 0; d < 3; d++) {
+		if (d >= nd) break;
+		if (d == nd - 1) {
+			c[d] = b.lo[d] + l;
+			break;
+		}
+		const int qd = (int)(((float)l + 0.5f) * q.r[d]);
+		c[d] = b.lo[d] + (l - qd * b.n[d]);
+		l = qd;
+	}
+}
 // Box of the cells clo..chi grown by grow_lo/grow_hi, trimmed to at most cap
 // entries: each dimension first to kBoxReach cells either side of the mean
 // cell mid, then the widest one cell at a time from its side farther from mid
@@ -1922,7 +1993,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 		}
 #pragma unroll
 		for (int d = 0; d < ND; d++) {
-			int x = wave_min_i(lo[d]), y = wave_max_i(hi[d]), z = wave_sum(sm[d]);
+			int x = wave_min_i(lo[d]), y = wave_max_i(hi[d]), z = wave_sum_i(sm[d]);
 			if (lane == 0) {
 				red[(3 * d) * NW + wv] = x;
 				red[(3 * d + 1) * NW + wv] = y;
@@ -2014,9 +2085,10 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	for (int t = threadIdx.x; t < (PINC_PUSH_COPIES ? nCopy * rStride : rB.vol); t += kPushThreads) rhoL[t] = 0.0;
 	for (int t = threadIdx.x; t < (SORT ? kInCellCap : obb.vol); t += kPushThreads) cntOut[t] = 0;
 	if (KICK && !(PINC_PUSH_SKIP & 2)) {
+		const BoxRcp eq = box_rcp(eB);
 		for (int t = threadIdx.x; t < eB.vol; t += kPushThreads) {
 			int c[3] = {0, 0, 0};
-			eB.coords(t, c, ND);
+			box_coords(eB, eq, t, c, ND);
 			int off = 0;
 #pragma unroll
 			for (int d = 0; d < ND; d++) {
@@ -2072,7 +2144,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 			int no = 0;
 #pragma unroll
 			for (int k = 0; k < kPushItems; k++) no += rl[k] < 0 && ((valid >> k) & 1u);
-			no = wave_sum(no);
+			no = wave_sum_i(no);
 			if (lane == 0 && no) atomicAdd(&a.diag[0], (unsigned long long)no);
 		}
 		__syncthreads();
@@ -2405,11 +2477,11 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	}
 	if (bad) atomicOr(a.err, bad);
 	if (!SORT) {
-		int wc = wave_sum(cnt);
+		int wc = wave_sum_i(cnt);
 		if (lane == 0) wcnt[wv] = wc;
 	}
 	if (a.moved) {
-		int wm = wave_sum(__popc(dep >> 16));
+		int wm = wave_sum_i(__popc(dep >> 16));
 		if (lane == 0) wmov[wv] = wm;
 	}
 
@@ -2606,13 +2678,14 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 		atomicAdd(a.spread, v);
 	}
 	// flush: one global atomic per touched node / output cell
+	const BoxRcp rq = box_rcp(rB);
 	for (int t = threadIdx.x; t < ((PINC_PUSH_SKIP & 4) ? 0 : rB.vol); t += kPushThreads) {
 		double v = rhoL[t];
 		if (PINC_PUSH_COPIES)
 			for (int c = 1; c < nCopy; c++) v += rhoL[c * rStride + t];
 		if (v == 0.0) continue;
 		int c[3] = {0, 0, 0};
-		rB.coords(t, c, ND);
+		box_coords(rB, rq, t, c, ND);
 		int off = 0;
 #pragma unroll
 		for (int d = 0; d < ND; d++) {
