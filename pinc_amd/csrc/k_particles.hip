@@ -14,6 +14,7 @@
 // All arithmetic is fp64 in the reference's association order; the library
 // is compiled with -ffp-contract=off so no multiply-add is fused.
 #include "common.h"
+#include <type_traits>
 
 using namespace pinc;
 
@@ -403,6 +404,26 @@ __device__ __forceinline__ int wave_reduce_i(int v, int id, Op op) {
 #ifndef PINC_DPP_REDUCE
 #define PINC_DPP_REDUCE 1
 #endif
+// fp64 wave sum, the same DPP pattern on the two halves of each partner
+// value (a fixed tree: deterministic); the total in every lane's return
+__device__ __forceinline__ double wave_sum_d(double v) {
+	auto step = [](double x, auto ctrl) -> double {
+		constexpr int C = decltype(ctrl)::value >> 4, R = decltype(ctrl)::value & 15;
+		const unsigned long long u = __double_as_longlong(x);
+		const unsigned lo = __builtin_amdgcn_update_dpp(0u, (unsigned)u, C, R, 0xf, false);
+		const unsigned hi = __builtin_amdgcn_update_dpp(0u, (unsigned)(u >> 32), C, R, 0xf, false);
+		return x + __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+	};
+	v = step(v, std::integral_constant<int, (0x111 << 4) | 0xf>{});
+	v = step(v, std::integral_constant<int, (0x112 << 4) | 0xf>{});
+	v = step(v, std::integral_constant<int, (0x114 << 4) | 0xf>{});
+	v = step(v, std::integral_constant<int, (0x118 << 4) | 0xf>{});
+	v = step(v, std::integral_constant<int, (0x142 << 4) | 0xa>{});
+	v = step(v, std::integral_constant<int, (0x143 << 4) | 0xc>{});
+	const unsigned long long u = __double_as_longlong(v);
+	const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, 63), hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), 63);
+	return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
 #if PINC_DPP_REDUCE
 __device__ __forceinline__ int wave_min_i(int v) {
 	return wave_reduce_i(v, INT32_MAX, [](int a, int b) { return min(a, b); });
@@ -2180,6 +2201,30 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 #pragma unroll
 	for (int d = 0; d < ND; d++) thrInFrame &= a.thr.lo[d] >= 0.0 && a.thr.up[d] <= a.thr.hi[d];
 #endif
+	// positions (and velocities if kicked or moved) of items k, k + 1
+	const bool wvel = KICK || a.vo[0] != a.vi[0];
+	auto store_pair = [&](int k) {
+		const long i = item(k);
+		const bool ok0 = (valid >> k) & 1u, ok1 = (valid >> (k + 1)) & 1u;
+#pragma unroll
+		for (int d = 0; d < ND; d++) {
+			if (ok1 && al) {
+#if PINC_PUSH_CONSEC || !PINC_PUSH_NT
+				*reinterpret_cast<dvec2 *>(a.xo[d] + i) = dvec2{p[k][d], p[k + 1][d]};
+				if (wvel) *reinterpret_cast<dvec2 *>(a.vo[d] + i) = dvec2{vv[k][d], vv[k + 1][d]};
+#else
+				__builtin_nontemporal_store(dvec2{p[k][d], p[k + 1][d]}, reinterpret_cast<dvec2 *>(a.xo[d] + i));
+				if (wvel)
+					__builtin_nontemporal_store(dvec2{vv[k][d], vv[k + 1][d]}, reinterpret_cast<dvec2 *>(a.vo[d] + i));
+#endif
+			} else {
+				if (ok0) a.xo[d][i] = p[k][d];
+				if (ok0 && wvel) a.vo[d][i] = vv[k][d];
+				if (ok1) a.xo[d][i + 1] = p[k + 1][d];
+				if (ok1 && wvel) a.vo[d][i + 1] = vv[k + 1][d];
+			}
+		}
+	};
 #pragma unroll
 	for (int k = 0; k < kPushItems; k++) {
 		if (!((valid >> k) & 1u)) continue;
@@ -2406,32 +2451,12 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 			dep |= (1u | (unsigned)chg << 16) << k;  // bits 16+: changed cell
 		}
 	}
+	// (all pairs after the last kick: storing each pair right after its
+	// kick, to free its velocity registers, measured 20.6 -> 26.2 ms per
+	// plain push at C4, profiles/r05j_push_early_store_ab.txt)
 	if (!SORT) {
-		// positions (and velocities if kicked or moved) in pairs
-		const bool wv = KICK || a.vo[0] != a.vi[0];
 #pragma unroll
-		for (int k = 0; k < kPushItems; k += 2) {
-			const long i = item(k);
-			const bool ok0 = (valid >> k) & 1u, ok1 = (valid >> (k + 1)) & 1u;
-#pragma unroll
-			for (int d = 0; d < ND; d++) {
-				if (ok1 && al) {
-#if PINC_PUSH_CONSEC || !PINC_PUSH_NT
-					*reinterpret_cast<dvec2 *>(a.xo[d] + i) = dvec2{p[k][d], p[k + 1][d]};
-					if (wv) *reinterpret_cast<dvec2 *>(a.vo[d] + i) = dvec2{vv[k][d], vv[k + 1][d]};
-#else
-					__builtin_nontemporal_store(dvec2{p[k][d], p[k + 1][d]}, reinterpret_cast<dvec2 *>(a.xo[d] + i));
-					if (wv)
-						__builtin_nontemporal_store(dvec2{vv[k][d], vv[k + 1][d]}, reinterpret_cast<dvec2 *>(a.vo[d] + i));
-#endif
-				} else {
-					if (ok0) a.xo[d][i] = p[k][d];
-					if (ok0 && wv) a.vo[d][i] = vv[k][d];
-					if (ok1) a.xo[d][i + 1] = p[k + 1][d];
-					if (ok1 && wv) a.vo[d][i + 1] = vv[k + 1][d];
-				}
-			}
-		}
+		for (int k = 0; k < kPushItems; k += 2) store_pair(k);
 	}
 	PUSH_TS(4);
 	if (SORT) {
@@ -2657,10 +2682,24 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	}
 
 	if (KICK) {
+#if PINC_DPP_REDUCE
+		// per-wave sums with DPP (no LDS shuffles); the block barrier below
+		// publishes them
+		const double w = wave_sum_d(ke);
+		if (lane == 0) kered[wv] = w;
+#else
 		double t = block_sum(ke, kered);
 		if (threadIdx.x == 0) a.kePartial[chunk] = t;
+#endif
 	}
 	__syncthreads();
+#if PINC_DPP_REDUCE
+	if (KICK && threadIdx.x == 0) {
+		double t = 0.0;
+		for (int w = 0; w < NW; w++) t += kered[w];
+		a.kePartial[chunk] = t;
+	}
+#endif
 	if (!SORT && threadIdx.x == 0) {
 		int t = 0;
 		for (int w = 0; w < NW; w++) t += wcnt[w];
