@@ -36,6 +36,17 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+# the measured copy ceiling of the push's own streams (six SoA arrays, each a
+# separate allocation, one block per 1024-particle chunk, nontemporal):
+# profiles/r05e_copy_ceiling.json (tools/copy_probe2.hip)
+COPY_CEILING = ROOT / "profiles" / "r05e_copy_ceiling.json"
+
+
+def _copy_ceiling_gbs() -> float | None:
+    try:
+        return 1000.0 * json.loads(COPY_CEILING.read_text())["push_streams_ceiling_TBs"]
+    except (OSError, ValueError, KeyError, TypeError):
+        return None
 METRIC = "particle-updates/sec + Poisson-solve ms/step, 256³ grid 64 ppc, 1/2/4/8 MI355X"
 # kernel names as rocprofv3 --kernel-trace reports them (3-D instantiations)
 ROCPROF_NAMES = {
@@ -487,9 +498,6 @@ def main() -> int:
                       "est_ms_per_step": p["mean_ms"] * p["launches"] / args.steps}
     dom = max(kernels, key=lambda k: kernels[k]["est_ms_per_step"])
     dk = kernels[dom]
-    # push+deposit against SURVEY.md 8(d): 144 B per particle-update (3-D)
-    # 144 B per 3-D particle-update (96 B in 2-D) + 32 B per cell
-    pd_bytes = (96.0 if c2 else 144.0) * n_local + 32.0 * S ** nd / world
     if "push_plain" in sub:
         for k in ("push_count", "push_sort"):
             if k in sub:
@@ -500,7 +508,6 @@ def main() -> int:
     # configuration key of the PMC traffic profiles (tools/pmc_summary.py)
     traffic_key = {"workload": args.workload, "grid": [S] * nd, "ppc_per_species": args.ppc, "n_gpus": world,
                    "layout": args.layout}
-    pd_gbs = pd_bytes / (push_ms * 1e-3) / 1e9 if push_ms > 0 else 0.0
 
     result = {
         "metric": METRIC,
@@ -578,9 +585,6 @@ def main() -> int:
             "samples": dk["samples"],
             "launches": dk["launches"],
         },
-        "push_deposit_roofline": {"bytes_per_step": pd_bytes, "achieved": pd_gbs, "peak": HBM_PEAK_GBS,
-                                  "unit": "GB/s", "frac": pd_gbs / HBM_PEAK_GBS,
-                                  "basis": "144 B per particle-update + 32 B per cell (SURVEY.md 8(d))"},
         "kernels": kernels,
         "push_kinds": sub,
         "cpu_baseline": None,
@@ -591,6 +595,13 @@ def main() -> int:
     result["config"]["traffic_key"] = traffic_key
     result["config"]["runtime_stack"] = _lib.runtime_stack()
     tr = _pmc_traffic(dk["rocprof_name"].rstrip("*").rstrip(" ,").split("*")[0], traffic_key)
+    cc = _copy_ceiling_gbs()
+    if cc and dom == "push":
+        # the same achieved rate against what a pure copy of the push's own
+        # streams reaches on this chip (a measured ceiling, not a spec)
+        result["roofline"]["copy_ceiling"] = cc
+        result["roofline"]["frac_of_copy_ceiling"] = dk["achieved_GBs"] / cc
+        result["roofline"]["copy_ceiling_source"] = str(COPY_CEILING.relative_to(ROOT))
     if tr is not None:
         result["roofline"]["traffic"] = tr["bytes_per_launch"]
         result["roofline"]["traffic_source"] = tr["source"]
