@@ -156,6 +156,8 @@ typedef struct {
 	int *objCount;
 	int objLo[3], objHi[3];   /* bounding box (padded node coordinates, inclusive)
 	                             of the nodes with an id: only cells there are looked up */
+	unsigned long long *emigTotal; /* if set: += the particles flagged to leave (every flag but the
+	                                  centre: emigrants, collected, outside the frame) */
 } pinc_push_t;
 int pinc_hip_push(pinc_pop_t pop, int s, pinc_geom_t g, const pinc_push_t *args, int *nBlocks, void *stream);
 /* number of sort keys (cells incl. the wrap layer) of the tiled layout */

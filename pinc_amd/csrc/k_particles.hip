@@ -1383,6 +1383,7 @@ struct PushArgs {
 	long objSy, objSz, objN;
 	int *objCount;
 	int objLo[3], objExt[3];     // bounding box of the object nodes: lower corner, extent - 1
+	unsigned long long *emigTotal;  // += particles flagged to leave (nullable)
 };
 // phase timestamp of the block (thread 0, s_memrealtime at 100 MHz)
 #define PUSH_TS(slot) \
@@ -2446,7 +2447,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 		}
 		if (!SORT) a.flags[i] = (unsigned char)ne;
 		if (ne != a.center) {
-			if (!SORT) cnt++;
+			cnt++;
 		} else {
 			dep |= (1u | (unsigned)chg << 16) << k;  // bits 16+: changed cell
 		}
@@ -2501,7 +2502,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 		}
 	}
 	if (bad) atomicOr(a.err, bad);
-	if (!SORT) {
+	if (!SORT || a.emigTotal) {
 		int wc = wave_sum_i(cnt);
 		if (lane == 0) wcnt[wv] = wc;
 	}
@@ -2700,10 +2701,11 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 		a.kePartial[chunk] = t;
 	}
 #endif
-	if (!SORT && threadIdx.x == 0) {
+	if ((!SORT || a.emigTotal) && threadIdx.x == 0) {
 		int t = 0;
 		for (int w = 0; w < NW; w++) t += wcnt[w];
-		if (t) atomicAdd(&a.chunkCount[base / PINC_CHUNK], t);  // zeroed by the caller
+		if (!SORT && t) atomicAdd(&a.chunkCount[base / PINC_CHUNK], t);  // zeroed by the caller
+		if (t && a.emigTotal) atomicAdd(a.emigTotal, (unsigned long long)t);
 	}
 	if (a.moved && threadIdx.x == 0) {
 		int t = 0;
@@ -3264,6 +3266,7 @@ extern "C" int pinc_hip_push(pinc_pop_t pop, int s, pinc_geom_t g, const pinc_pu
 	a.spread = args->spread;
 	a.tstamp = args->tstamp;
 	a.diag = args->diag;
+	a.emigTotal = args->emigTotal;
 	a.objIn = args->objInside;
 	a.objSy = args->objSy;
 	a.objSz = args->objSz;

@@ -492,6 +492,7 @@ void pinc_ctx_init(void) {
 	if (g_pinc.nranks < 1) g_pinc.nranks = 1;
 	g_pinc.verbose = getenv("PINC_VERBOSE") ? atoi(getenv("PINC_VERBOSE")) : 0;
 	g_pinc.traceSort = getenv("PINC_TRACE_SORT") ? atoi(getenv("PINC_TRACE_SORT")) : 0;
+	g_pinc.extractSkip = !(getenv("PINC_EXTRACT_SKIP") && !atoi(getenv("PINC_EXTRACT_SKIP")));
 	for (int i = 0; i < 2 * PINC_NPHASES; i++) pinc_check(pinc_hip_event_create(&g_pinc.ev[i]), "event");
 	g_pinc.initialised = 1;
 }

@@ -30,6 +30,7 @@ typedef struct {
 	int thrSet;
 	int capturing; /* a stream capture is open: no event probes */
 	int traceSort; /* PINC_TRACE_SORT: print the adaptive sort schedule */
+	int extractSkip; /* PINC_EXTRACT_SKIP=0 turns off skipping extractions the push counted empty */
 	int verbose;        /* PINC_VERBOSE=n: progress every n V-cycles */
 	int timing;
 	void *ev[2*PINC_NPHASES];
@@ -102,6 +103,14 @@ struct PincDevPop {
 	int cntValid[PINC_MAX_SPECIES];
 	int everSorted;                     /* input already in cell order once */
 	int permId[PINC_MAX_SPECIES];       /* species s left in order by the pending sorting push */
+	/* particles each species' last push flagged to leave (emigrants,
+	 * collected, outside the frame), read with the sort counters; emigValid:
+	 * the current flags are that push's, so a species with none skips the
+	 * extraction (no kernels, no host read; one rank, where the tiled push
+	 * wraps every dimension in place) */
+	unsigned long long *emigCnt;
+	unsigned long long emigLast[PINC_MAX_SPECIES];
+	int emigValid;
 	int vKicked[PINC_MAX_SPECIES];      /* p.v of species s holds the pending push's kicked velocities
 	                                       (materialised before its E was written, pinc_grid_touch) */
 	Grid *pendingE;                     /* E of the pending push's kick (pinc_pending_vel) */

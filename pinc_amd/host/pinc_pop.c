@@ -109,9 +109,10 @@ Population *pAlloc(const dictionary *ini) {
 		if (dv->sortFraction > 0) {
 			/* moved and spread counters and the kinetic-energy sums in one
 			 * block: one read per push */
-			pinc_check(pinc_hip_malloc((void **)&dv->movedCnt, 3 * PINC_MAX_SPECIES * sizeof(unsigned long long)),
+			pinc_check(pinc_hip_malloc((void **)&dv->movedCnt, 4 * PINC_MAX_SPECIES * sizeof(unsigned long long)),
 			           "pAlloc moved");
 			dv->spreadCnt = dv->movedCnt + PINC_MAX_SPECIES;
+			dv->emigCnt = dv->movedCnt + 3 * PINC_MAX_SPECIES;
 			for (int s = 0; s < PINC_MAX_SPECIES; s++) dv->sortNext[s] = 1;
 		}
 	}

@@ -400,7 +400,7 @@ static int push_all(Population *pop, Grid *E, double *const *xout) {
 	int nd = pop->nDims;
 	if (adaptive) {
 		/* (spreadCnt follows movedCnt in one block, pinc_pop.c) */
-		pinc_check(pinc_hip_memset(dv->movedCnt, 0, 2 * PINC_MAX_SPECIES * sizeof(unsigned long long), g_pinc.stream),
+		pinc_check(pinc_hip_memset(dv->movedCnt, 0, 4 * PINC_MAX_SPECIES * sizeof(unsigned long long), g_pinc.stream),
 		           "moved counts");
 	}
 	for (int s = 0; s < pop->nSpecies; s++) {
@@ -435,6 +435,7 @@ static int push_all(Population *pop, Grid *E, double *const *xout) {
 		pinc_check(pinc_hip_memset(a.chunkCount, 0, chunks * sizeof(int), g_pinc.stream), "chunk counts");
 		if (adaptive) {
 			a.moved = dv->movedCnt + s;
+			a.emigTotal = dv->emigCnt + s;
 			if (dv->sortSpread > 0 || g_pinc.traceSort) a.spread = dv->spreadCnt + s;
 		}
 		if (dv->objInside && dv->objHi[0] >= dv->objLo[0]) { /* (empty box: no object node in this slab) */
@@ -512,9 +513,11 @@ static int push_all(Population *pop, Grid *E, double *const *xout) {
 		}
 	}
 	if (adaptive) {
-		unsigned long long cnt[3 * PINC_MAX_SPECIES];
+		unsigned long long cnt[4 * PINC_MAX_SPECIES];
 		pinc_check(pinc_hip_d2h(cnt, dv->movedCnt, sizeof(cnt), g_pinc.stream), "moved, spread and energy readback");
 		const unsigned long long *mv = cnt, *sp = cnt + PINC_MAX_SPECIES;
+		memcpy(dv->emigLast, cnt + 3 * PINC_MAX_SPECIES, sizeof(dv->emigLast));
+		dv->emigValid = 1;
 		if (E) {
 			memcpy(dv->keSums, cnt + 2 * PINC_MAX_SPECIES, sizeof(dv->keSums));
 			dv->keSumsValid = 1;
@@ -668,6 +671,7 @@ static void classify(Population *pop, int doMove) {
 	}
 	for (int s = 0; s < PINC_MAX_SPECIES; s++) dv->cntValid[s] = 0;
 	dv->depValid = 0;
+	dv->emigValid = 0; /* (flags of this classification: not counted) */
 	int wrapMask = wrap_mask(pop);
 	pinc_pop_t p = pinc_devpop(pop);
 	for (int s = 0; s < pop->nSpecies; s++) {
@@ -693,11 +697,20 @@ void puMove(Population *pop, Object *obj) {
 static void extract(Population *pop, MpiInfo *m) {
 	pinc_pop_flush_host(pop);
 	PincDevPop *dv = pop->dev;
+	/* the flags of the last push, whose flagged counts are known */
+	const int known = g_pinc.extractSkip && dv->flagsValid && dv->emigValid;
 	if (!dv->flagsValid) classify(pop, 0);
 	pinc_phase_begin(1);
 	int ns = pop->nSpecies, nN = m->nNeighbors;
 	memset(m->nEmigrants, 0, nN * ns * sizeof(long));
 	for (int s = 0; s < ns; s++) {
+		if (known && dv->emigLast[s] == 0) {
+			/* nothing flagged to leave: the extraction would find nothing */
+			dv->nEmig[s] = 0;
+			memset(dv->neCount[s], 0, sizeof(dv->neCount[s]));
+			if (dv->depValid) dv->depEnd[s] = pop->iStop[s];
+			continue;
+		}
 		for (int attempt = 0;; attempt++) {
 			pinc_pop_t p = pinc_devpop(pop);
 			long nEmig = 0;
@@ -721,6 +734,7 @@ static void extract(Population *pop, MpiInfo *m) {
 		for (int ne = 0; ne < nN; ne++) m->nEmigrants[ne * ns + s] = dv->neCount[s][ne];
 	}
 	dv->flagsValid = 0;
+	dv->emigValid = 0;
 	if (dv->depValid) dv->depExtracted = 1;
 	pinc_phase_end(1);
 }

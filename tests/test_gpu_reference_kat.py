@@ -189,7 +189,7 @@ class PushArgs(C.Structure):
                 ("tileWidth", C.c_int), ("cursor", C.c_void_p), ("cntNext", C.c_void_p), ("moved", C.c_void_p),
                 ("spread", C.c_void_p), ("tstamp", C.c_void_p), ("diag", C.c_void_p), ("objInside", C.c_void_p),
                 ("objSy", C.c_long), ("objSz", C.c_long), ("objNodes", C.c_long), ("objCount", C.c_void_p),
-                ("objLo", C.c_int * 3), ("objHi", C.c_int * 3)]
+                ("objLo", C.c_int * 3), ("objHi", C.c_int * 3), ("emigTotal", C.c_void_p)]
 
 
 def _embedded_fractions(rho_dev: np.ndarray, T, k):
