@@ -493,7 +493,8 @@ void pinc_ctx_init(void) {
 	g_pinc.verbose = getenv("PINC_VERBOSE") ? atoi(getenv("PINC_VERBOSE")) : 0;
 	g_pinc.traceSort = getenv("PINC_TRACE_SORT") ? atoi(getenv("PINC_TRACE_SORT")) : 0;
 	g_pinc.extractSkip = !(getenv("PINC_EXTRACT_SKIP") && !atoi(getenv("PINC_EXTRACT_SKIP")));
-	for (int i = 0; i < 2 * PINC_NPHASES; i++) pinc_check(pinc_hip_event_create(&g_pinc.ev[i]), "event");
+	for (int p = 0; p < PINC_NPHASES; p++)
+		for (int i = 0; i < 2 * PINC_PHASE_RING; i++) pinc_check(pinc_hip_event_create(&g_pinc.ev[p][i]), "event");
 	g_pinc.initialised = 1;
 }
 
@@ -502,19 +503,36 @@ void pinc_ctx_require(void) {
 	pinc_boot_world();
 }
 
+/* phase timers (PincSimOpts.timing): an event pair per phase interval,
+ * summed into phaseMs only when the ring of a phase is full or the totals
+ * are read, so that timing adds no host wait to the step (an elapsed time
+ * waits for its stop event) */
 void pinc_phase_begin(int p) {
 	if (!g_pinc.timing) return;
-	pinc_check(pinc_hip_event_record(g_pinc.ev[2 * p], g_pinc.stream), "event");
+	pinc_check(pinc_hip_event_record(g_pinc.ev[p][2 * g_pinc.phaseN[p]], g_pinc.stream), "event");
 	g_pinc.phaseOpen[p] = 1;
+}
+
+static void phase_flush(int p) {
+	for (int i = 0; i < g_pinc.phaseN[p]; i++) {
+		float ms = 0;
+		pinc_check(pinc_hip_event_elapsed(&ms, g_pinc.ev[p][2 * i], g_pinc.ev[p][2 * i + 1]), "elapsed");
+		g_pinc.phaseMs[p] += ms;
+	}
+	g_pinc.phaseN[p] = 0;
 }
 
 void pinc_phase_end(int p) {
 	if (!g_pinc.timing || !g_pinc.phaseOpen[p]) return;
-	pinc_check(pinc_hip_event_record(g_pinc.ev[2 * p + 1], g_pinc.stream), "event");
-	float ms = 0;
-	pinc_check(pinc_hip_event_elapsed(&ms, g_pinc.ev[2 * p], g_pinc.ev[2 * p + 1]), "elapsed");
-	g_pinc.phaseMs[p] += ms;
+	pinc_check(pinc_hip_event_record(g_pinc.ev[p][2 * g_pinc.phaseN[p] + 1], g_pinc.stream), "event");
 	g_pinc.phaseOpen[p] = 0;
+	if (++g_pinc.phaseN[p] == PINC_PHASE_RING) phase_flush(p);
+}
+
+void pinc_phase_flush(void) {
+	if (!g_pinc.initialised) return;
+	for (int p = 0; p < PINC_NPHASES; p++)
+		if (!g_pinc.phaseOpen[p]) phase_flush(p);
 }
 
 /* ------------------------------------------------------------- probe -- */

@@ -448,6 +448,7 @@ void pCreateEnergyDatasets(long long xy, Population *pop) {
 
 /* pop->kinEnergy / potEnergy hold this rank's values; summed over ranks */
 void pWriteEnergy(long long xy, Population *pop, double x) {
+	pinc_pop_settle(pop); /* a fused puAcc3D1KE's sums */
 	char name[64];
 	int ns = pop->nSpecies;
 	xyWrite(xy, "/energy/potential/total", x, pop->potEnergy[ns], PINC_OP_SUM);

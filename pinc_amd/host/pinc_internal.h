@@ -12,6 +12,7 @@
 #include "pinc.h"
 
 #define PINC_NNE 27
+#define PINC_PHASE_RING 64
 
 typedef struct PincObj PincObj;
 
@@ -30,10 +31,16 @@ typedef struct {
 	int thrSet;
 	int capturing; /* a stream capture is open: no event probes */
 	int traceSort; /* PINC_TRACE_SORT: print the adaptive sort schedule */
+	/* launches that can set the assert word (dErr), and that count when the
+	 * word was last read: an unchanged word is not read again */
+	unsigned long errSerial, errRead;
 	int extractSkip; /* PINC_EXTRACT_SKIP=0 turns off skipping extractions the push counted empty */
 	int verbose;        /* PINC_VERBOSE=n: progress every n V-cycles */
 	int timing;
-	void *ev[2*PINC_NPHASES];
+	/* phase timers: event pairs per phase, read when the ring is full or
+	 * the totals are asked for (pinc_phase_flush), not at each phase end */
+	void *ev[PINC_NPHASES][2 * PINC_PHASE_RING];
+	int phaseN[PINC_NPHASES];
 	double phaseMs[PINC_NPHASES];
 	int phaseOpen[PINC_NPHASES];
 	/* kernel probe: HIP events around launches of one kernel, read lazily
@@ -48,6 +55,7 @@ typedef struct {
 
 /* probe hooks around a launch of kernel k with algorithmic byte count b */
 int pinc_probe_begin(int k);
+void pinc_phase_flush(void);
 void pinc_probe_end(int k, int slot, double bytes);
 void pinc_probe_tag(int k, int slot, int tag);
 
@@ -111,6 +119,14 @@ struct PincDevPop {
 	unsigned long long *emigCnt;
 	unsigned long long emigLast[PINC_MAX_SPECIES];
 	int emigValid;
+	/* the counter block (moved, spread, KE sums, emigrants) comes back
+	 * asynchronously into pinned memory (hostCnt, cntEvent) and is taken in
+	 * by pinc_pop_settle: at the next push, extraction, KE sum or energy
+	 * read, whose own host wait usually covers it (no read of its own) */
+	unsigned long long *hostCnt;
+	void *cntEvent;
+	int cntPending, cntE, keDeferred;
+	int cntSortS[PINC_MAX_SPECIES], cntCountS[PINC_MAX_SPECIES];
 	int vKicked[PINC_MAX_SPECIES];      /* p.v of species s holds the pending push's kicked velocities
 	                                       (materialised before its E was written, pinc_grid_touch) */
 	Grid *pendingE;                     /* E of the pending push's kick (pinc_pending_vel) */
@@ -186,6 +202,8 @@ struct PincDevGrid {
 void pinc_grid_touch(Grid *g);
 /* populations whose pending sorting push may need its E (pinc_pusher.c) */
 void pinc_pending_register(Population *pop);
+/* take in the last push's counter block (waits for its copy if needed) */
+void pinc_pop_settle(Population *pop);
 void pinc_pending_unregister(Population *pop);
 /* the grid is allocated and is the one with this serial */
 int pinc_grid_live(const Grid *g, unsigned long long serial);

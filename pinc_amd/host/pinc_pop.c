@@ -176,6 +176,7 @@ void pinc_pop_flush_host(const Population *pop) {
  * on, and the velocities present now are checked against it here. */
 static int assert_word(void) {
 	int err = 0;
+	g_pinc.errRead = g_pinc.errSerial;
 	pinc_check(pinc_hip_d2h(&err, g_pinc.dErr, sizeof(int), g_pinc.stream), "assert word");
 	return err;
 }
@@ -193,6 +194,7 @@ void pVelAssertMax(const Population *pop, double max) {
 			for (int d = 0; d < pop->nDims; d++) p.v[d] = dv->altV[d];
 		for (int s = 0; s < pop->nSpecies; s++)
 			pinc_check(pinc_hip_vel_assert(p, s, max, g_pinc.dErr, g_pinc.stream), "pVelAssertMax");
+		g_pinc.errSerial++;
 	}
 	if (assert_word() & 1)
 		msg(ERROR, "Particle travels too fast (population:maxVel=%g exceeded, population.c:342-365)", max);
@@ -211,6 +213,9 @@ void pFree(Population *p) {
 	PincDevPop *dv = p->dev;
 	pinc_pending_unregister(p);
 	if (dv) {
+		pinc_pop_settle(p); /* (the copy into hostCnt has landed) */
+		pinc_hip_host_free(dv->hostCnt);
+		if (dv->cntEvent) pinc_hip_event_destroy(dv->cntEvent);
 		/* main.c:297-298 frees the population before the objects */
 		if (dv->objOwner) pinc_obj_forget_pop(dv->objOwner);
 		for (int d = 0; d < p->nDims; d++) {
@@ -392,6 +397,7 @@ void pVelMaxwell(const dictionary *ini, Population *p, unsigned long long seed) 
 }
 
 void pSumKinEnergy(Population *p) {
+	pinc_pop_settle(p); /* a fused puAcc3D1KE's sums */
 	int ns = p->nSpecies;
 	p->kinEnergy[ns] = 0;
 	for (int s = 0; s < ns; s++) p->kinEnergy[ns] += p->kinEnergy[s];
@@ -430,6 +436,7 @@ void pSyncToDevice(Population *p) {
 	if (!p->pos) msg(ERROR, "pSyncToDevice without host particles");
 	int nd = p->nDims;
 	PincDevPop *dv = p->dev;
+	pinc_pop_settle(p); /* before the schedule is reset below */
 	dv->hostDirty = 0;
 	/* new particles: a pending fused move and its deposits no longer apply */
 	dv->pending = dv->pendingSorted = dv->depValid = dv->depExtracted = 0;

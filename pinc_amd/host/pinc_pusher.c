@@ -369,9 +369,11 @@ static int push_all(Population *pop, Grid *E, double *const *xout) {
 			pinc_check(pinc_hip_malloc((void **)&dv->rhoS[s], n * sizeof(double)), "species charge");
 		dv->rhoN = n;
 	}
+	pinc_pop_settle(pop); /* the schedule below reads the last push's counts */
 	int sortNow = 0, sortS[PINC_MAX_SPECIES] = {0}, countS[PINC_MAX_SPECIES] = {0};
 	int adaptive = dv->sorted && dv->sortFraction > 0;
 	dv->keSumsValid = 0;
+	g_pinc.errSerial++;
 	if (dv->sorted) {
 		ensure_keys(pop);
 		for (int s = 0; s < pop->nSpecies; s++) {
@@ -513,38 +515,61 @@ static int push_all(Population *pop, Grid *E, double *const *xout) {
 		}
 	}
 	if (adaptive) {
-		unsigned long long cnt[4 * PINC_MAX_SPECIES];
-		pinc_check(pinc_hip_d2h(cnt, dv->movedCnt, sizeof(cnt), g_pinc.stream), "moved, spread and energy readback");
-		const unsigned long long *mv = cnt, *sp = cnt + PINC_MAX_SPECIES;
-		memcpy(dv->emigLast, cnt + 3 * PINC_MAX_SPECIES, sizeof(dv->emigLast));
-		dv->emigValid = 1;
-		if (E) {
-			memcpy(dv->keSums, cnt + 2 * PINC_MAX_SPECIES, sizeof(dv->keSums));
-			dv->keSumsValid = 1;
+		if (!dv->hostCnt) {
+			pinc_check(pinc_hip_host_alloc((void **)&dv->hostCnt, 4 * PINC_MAX_SPECIES * sizeof(unsigned long long)),
+			           "counter block");
+			pinc_check(pinc_hip_event_create(&dv->cntEvent), "counter block");
 		}
-		for (int s = 0; s < pop->nSpecies; s++) {
-			long np = pop->iStop[s] - pop->iStart[s];
-			double rate = np > 0 ? (double)mv[s] / (double)np : 0.0;
-			/* mean input cell box of this push's blocks */
-			const long chunk = pinc_hip_push_chunk();
-			const double blocks = (double)((np + chunk - 1) / chunk);
-			dv->spreadLast[s] = blocks > 0 ? (double)sp[s] / blocks : 0.0;
-			if (sortS[s]) dv->spreadBase[s] = 0;
-			if (dv->sinceSort[s] == 1 && !sortS[s]) dv->spreadBase[s] = dv->spreadLast[s];
-			dv->movedFrac[s] = sortS[s] ? rate : dv->movedFrac[s] + rate;
-			dv->sinceSort[s] = sortS[s] ? 1 : dv->sinceSort[s] + 1;
-			dv->lastRate[s] = rate;
-			dv->sortNext[s] = countS[s];
-			if (g_pinc.traceSort)
-				fprintf(stderr, "[pinc] push %ld species %d: moved %.4f, displaced %.4f, cell box %.1f (x%.2f)%s%s\n",
-				        dv->moves, s, rate, dv->movedFrac[s], dv->spreadLast[s],
-				        dv->spreadBase[s] > 0 ? dv->spreadLast[s] / dv->spreadBase[s] : 0.0, sortS[s] ? ", sorted" : "",
-				        countS[s] ? ", counted" : "");
-		}
+		pinc_check(pinc_hip_d2h_async(dv->hostCnt, dv->movedCnt, 4 * PINC_MAX_SPECIES * sizeof(unsigned long long),
+		                              g_pinc.stream),
+		           "moved, spread and energy readback");
+		pinc_check(pinc_hip_event_record(dv->cntEvent, g_pinc.stream), "counter block");
+		memcpy(dv->cntSortS, sortS, sizeof(sortS));
+		memcpy(dv->cntCountS, countS, sizeof(countS));
+		dv->cntE = E != NULL;
+		dv->cntPending = 1;
 	}
 	dv->depValid = 1;
 	dv->depExtracted = 0;
 	return sortNow;
+}
+
+void pinc_pop_settle(Population *pop) {
+	PincDevPop *dv = pop->dev;
+	if (!dv || !dv->cntPending) return;
+	pinc_check(pinc_hip_event_sync(dv->cntEvent), "moved, spread and energy readback");
+	dv->cntPending = 0;
+	const unsigned long long *cnt = dv->hostCnt;
+	const unsigned long long *mv = cnt, *sp = cnt + PINC_MAX_SPECIES;
+	const int *sortS = dv->cntSortS, *countS = dv->cntCountS;
+	memcpy(dv->emigLast, cnt + 3 * PINC_MAX_SPECIES, sizeof(dv->emigLast));
+	dv->emigValid = 1;
+	if (dv->cntE) {
+		memcpy(dv->keSums, cnt + 2 * PINC_MAX_SPECIES, sizeof(dv->keSums));
+		dv->keSumsValid = 1;
+		if (dv->keDeferred)
+			for (int s = 0; s < pop->nSpecies; s++) pop->kinEnergy[s] = dv->keSums[s] * (0.5 * pop->mass[s]);
+	}
+	dv->keDeferred = 0;
+	for (int s = 0; s < pop->nSpecies; s++) {
+		long np = pop->iStop[s] - pop->iStart[s];
+		double rate = np > 0 ? (double)mv[s] / (double)np : 0.0;
+		/* mean input cell box of this push's blocks */
+		const long chunk = pinc_hip_push_chunk();
+		const double blocks = (double)((np + chunk - 1) / chunk);
+		dv->spreadLast[s] = blocks > 0 ? (double)sp[s] / blocks : 0.0;
+		if (sortS[s]) dv->spreadBase[s] = 0;
+		if (dv->sinceSort[s] == 1 && !sortS[s]) dv->spreadBase[s] = dv->spreadLast[s];
+		dv->movedFrac[s] = sortS[s] ? rate : dv->movedFrac[s] + rate;
+		dv->sinceSort[s] = sortS[s] ? 1 : dv->sinceSort[s] + 1;
+		dv->lastRate[s] = rate;
+		dv->sortNext[s] = countS[s];
+		if (g_pinc.traceSort)
+			fprintf(stderr, "[pinc] push %ld species %d: moved %.4f, displaced %.4f, cell box %.1f (x%.2f)%s%s\n",
+			        dv->moves, s, rate, dv->movedFrac[s], dv->spreadLast[s],
+			        dv->spreadBase[s] > 0 ? dv->spreadLast[s] / dv->spreadBase[s] : 0.0, sortS[s] ? ", sorted" : "",
+			        countS[s] ? ", counted" : "");
+	}
 }
 
 /* dst[d] = the kicked velocities of species s pending after a sorting push,
@@ -636,6 +661,7 @@ static void swap_pos(PincDevPop *dv, int nd, int vel) {
 
 static void classify(Population *pop, int doMove) {
 	pinc_pop_flush_host(pop);
+	pinc_pop_settle(pop); /* (before emigValid changes below) */
 	if (!g_pinc.thrSet) msg(ERROR, "gCreateNeighborhood must run before puMove/extract");
 	PincDevPop *dv = pop->dev;
 	int nd = pop->nDims;
@@ -672,6 +698,7 @@ static void classify(Population *pop, int doMove) {
 	for (int s = 0; s < PINC_MAX_SPECIES; s++) dv->cntValid[s] = 0;
 	dv->depValid = 0;
 	dv->emigValid = 0; /* (flags of this classification: not counted) */
+	if (doMove) g_pinc.errSerial++;
 	int wrapMask = wrap_mask(pop);
 	pinc_pop_t p = pinc_devpop(pop);
 	for (int s = 0; s < pop->nSpecies; s++) {
@@ -688,20 +715,26 @@ static void classify(Population *pop, int doMove) {
 
 void puMove(Population *pop, Object *obj) {
 	(void)obj; /* particle-object collisions are out of scope (fact 6) */
-	pinc_phase_begin(0);
+	/* a pending fused move is a pointer swap: no device work, no timer
+	 * events (each costs the host an event record while the GPU waits) */
+	const int timed = !pop->dev->pending || pop->dev->hostDirty;
+	if (timed) pinc_phase_begin(0);
 	classify(pop, 1);
-	pinc_phase_end(0);
+	if (timed) pinc_phase_end(0);
 }
 
 /* ------------------------------------------------------------- extract -- */
 static void extract(Population *pop, MpiInfo *m) {
 	pinc_pop_flush_host(pop);
 	PincDevPop *dv = pop->dev;
+	pinc_pop_settle(pop);
 	/* the flags of the last push, whose flagged counts are known */
 	const int known = g_pinc.extractSkip && dv->flagsValid && dv->emigValid;
 	if (!dv->flagsValid) classify(pop, 0);
-	pinc_phase_begin(1);
 	int ns = pop->nSpecies, nN = m->nNeighbors;
+	int work = !known;
+	for (int s = 0; s < ns; s++) work |= dv->emigLast[s] != 0;
+	if (work) pinc_phase_begin(1);
 	memset(m->nEmigrants, 0, nN * ns * sizeof(long));
 	for (int s = 0; s < ns; s++) {
 		if (known && dv->emigLast[s] == 0) {
@@ -736,7 +769,7 @@ static void extract(Population *pop, MpiInfo *m) {
 	dv->flagsValid = 0;
 	dv->emigValid = 0;
 	if (dv->depValid) dv->depExtracted = 1;
-	pinc_phase_end(1);
+	if (work) pinc_phase_end(1);
 }
 
 void puExtractEmigrants3D(Population *pop, MpiInfo *m) { extract(pop, m); }
@@ -870,9 +903,12 @@ static void puMigrateImport(Population *pop, MpiInfo *m) {
 void puMigrate(Population *pop, MpiInfo *m, Grid *grid) {
 	(void)grid;
 	pinc_pop_flush_host(pop);
-	pinc_phase_begin(2);
 	PincDevPop *dv = pop->dev;
 	int ns = pop->nSpecies;
+	/* one rank without emigrants: nothing to import (no timer events) */
+	int work = g_pinc.nranks > 1;
+	for (int s = 0; s < ns; s++) work |= dv->nEmig[s] != 0;
+	if (work) pinc_phase_begin(2);
 	memset(m->nImmigrants, 0, m->nNeighbors * ns * sizeof(long));
 	long before[PINC_MAX_SPECIES];
 	for (int s = 0; s < ns; s++) before[s] = pop->iStop[s] - pop->iStart[s];
@@ -885,7 +921,7 @@ void puMigrate(Population *pop, MpiInfo *m, Grid *grid) {
 				pinc_check(pinc_hip_count_keys(p, s, before[s], dv->geom, dv->tileWidth, dv->keyCnt[s], g_pinc.stream),
 				           "count immigrant keys");
 			}
-	pinc_phase_end(2);
+	if (work) pinc_phase_end(2);
 }
 
 /* ------------------------------------------------------------- deposit -- */
@@ -1010,12 +1046,14 @@ static void acc(Population *pop, Grid *E, int ke) {
 		dv->pendingESerial = E->dev->serial;
 		dv->pendingEGen = E->dev->gen;
 		dv->flagsValid = 0;
-		if (ke) {
+		if (ke && dv->cntPending) {
+			/* the sums come with the sort counters (push_all): kinEnergy is
+			 * filled when they are taken in (pinc_pop_settle: pSumKinEnergy,
+			 * pWriteEnergy, the next push or extraction) */
+			dv->keDeferred = 1;
+		} else if (ke) {
 			double sums[PINC_MAX_SPECIES];
-			if (dv->keSumsValid) /* read with the sort counters (push_all) */
-				memcpy(sums, dv->keSums, sizeof(sums));
-			else
-				pinc_check(pinc_hip_d2h(sums, PINC_SLOT(16), pop->nSpecies * sizeof(double), g_pinc.stream), "ke readback");
+			pinc_check(pinc_hip_d2h(sums, PINC_SLOT(16), pop->nSpecies * sizeof(double), g_pinc.stream), "ke readback");
 			for (int s = 0; s < pop->nSpecies; s++) pop->kinEnergy[s] = sums[s] * (0.5 * pop->mass[s]);
 		}
 		pinc_phase_end(6);

@@ -64,8 +64,13 @@ static void report_errors(int err) {
 	if (err & 2) msg(ERROR, "Particle is out of bounds after migration (population.c:316-340)");
 }
 
+/* pPosAssertInLocalFrame's read of the assert word, unless no launch that
+ * can set it ran since the word was last read (the step's closing read
+ * covers the push that made this step's move) */
 static void check_errors(void) {
+	if (g_pinc.errSerial == g_pinc.errRead) return;
 	int err = 0;
+	g_pinc.errRead = g_pinc.errSerial;
 	pinc_check(pinc_hip_d2h(&err, g_pinc.dErr, sizeof(int), g_pinc.stream), "assert word");
 	report_errors(err);
 }
@@ -210,12 +215,15 @@ static void sim_step(PincSim *S) {
 	pinc_phase_end(5);
 	S->acc(pop, S->E);
 	pinc_phase_begin(7);
-	pSumKinEnergy(pop);
-	/* gPotEnergy and the error word in one read (PINC_SLOT(3..4)) */
+	/* gPotEnergy and the error word in one read (PINC_SLOT(3..4)); the
+	 * push's counters and kinetic energies, copied before it, are in by then
+	 * (pSumKinEnergy takes them in without a wait of its own) */
 	pinc_pot_energy_launch(S->rho, S->phi);
 	pinc_check(pinc_hip_d2d(PINC_SLOT(4), g_pinc.dErr, sizeof(int), g_pinc.stream), "assert word");
+	g_pinc.errRead = g_pinc.errSerial;
 	double r[2];
 	pinc_check(pinc_hip_d2h(r, PINC_SLOT(3), sizeof(r), g_pinc.stream), "potential energy");
+	pSumKinEnergy(pop);
 	pop->potEnergy[pop->nSpecies] = 0.5 * r[0];
 	pinc_phase_end(7);
 	int err = 0;
@@ -359,6 +367,7 @@ int pinc_sim_op(PincSim *S, const char *op) {
 }
 
 int pinc_sim_energy(PincSim *S, double *ke, double *pe, double *keSpecies) {
+	pinc_pop_settle(S->pop);
 	int ns = S->pop->nSpecies;
 	double v[PINC_MAX_SPECIES + 2];
 	v[0] = S->pop->kinEnergy[ns];
@@ -485,12 +494,17 @@ int pinc_sim_sync(PincSim *S) {
 
 int pinc_sim_timers(PincSim *S, double *ms) {
 	(void)S;
+	pinc_phase_flush();
 	for (int i = 0; i < PINC_NPHASES; i++) ms[i] = g_pinc.phaseMs[i];
 	return 0;
 }
 
 int pinc_sim_timers_reset(PincSim *S) {
 	(void)S;
-	for (int i = 0; i < PINC_NPHASES; i++) g_pinc.phaseMs[i] = 0;
+	/* intervals still in flight are dropped with the totals */
+	for (int i = 0; i < PINC_NPHASES; i++) {
+		g_pinc.phaseMs[i] = 0;
+		if (!g_pinc.phaseOpen[i]) g_pinc.phaseN[i] = 0;
+	}
 	return 0;
 }

@@ -7,6 +7,8 @@ start of the next one (count and total time per call name over the group).
 The schema's tables and views go to stdout first when a query fails.
 
     python tools/api_gaps.py <prof_dir> [min_us] [top_pairs]
+    python tools/api_gaps.py <prof_dir> --step [k]   (the k-th whole step,
+        default the middle one: every gap of 3 us or more with its HIP calls)
 """
 import glob
 import re
@@ -21,7 +23,56 @@ def short(name: str) -> str:
     return n.split("(")[0][:48]
 
 
+def step_timeline(kern, api, k):
+    """a step = from a push of the first species after a field kernel to the next"""
+    steps, sawField = [], False
+    for i, r in enumerate(kern):
+        n = short(r[0])
+        if n.startswith("k_efield"):
+            sawField = True
+        elif n.startswith("k_push") and sawField:
+            steps.append(i)
+            sawField = False
+    if len(steps) < 3:
+        print("fewer than 3 steps in the trace")
+        return
+    k = k if k is not None else len(steps) // 2
+    a, b = steps[k], steps[k + 1]
+    starts = [x[1] for x in api]
+    t0 = kern[a][1]
+    idle = 0
+    print(f"step {k} of {len(steps) - 1}: {(kern[b][1] - t0) / 1e6:.3f} ms, kernels {b - a}")
+    for i in range(a + 1, b + 1):
+        (pn, ps, pe), (nn, ns, ne) = kern[i - 1], kern[i]
+        gap = ns - pe
+        if gap <= 0:
+            continue
+        idle += gap
+        if gap < 3e3:
+            continue
+        j = bisect_left(starts, pe)
+        calls = defaultdict(lambda: [0, 0.0])
+        while j < len(api) and api[j][1] < ns:
+            calls[api[j][0]][0] += 1
+            calls[api[j][0]][1] += api[j][2] - api[j][1]
+            j += 1
+        cs = ", ".join(f"{n.replace('hip', '')}x{c}:{t / 1e3:.0f}" for n, (c, t) in
+                       sorted(calls.items(), key=lambda kv: -kv[1][1])[:5])
+        print(f"  {(pe - t0) / 1e3:9.1f} us  gap {gap / 1e3:6.1f}  {short(pn)[:30]:30s} -> {short(nn)[:30]:30s} {cs}")
+    print(f"idle {idle / 1e3:.1f} us")
+
+
 def main():
+    if len(sys.argv) > 2 and sys.argv[2] == "--step":
+        kern, api = [], []
+        for d in glob.glob(f"{sys.argv[1]}/**/*.db", recursive=True):
+            c = sqlite3.connect(d)
+            kern += c.execute("select name, start, end from kernels").fetchall()
+            api += c.execute("select name, start, end from regions").fetchall()
+        kern.sort(key=lambda r: r[1])
+        api.sort(key=lambda r: r[1])
+        step_timeline(kern, api, int(sys.argv[3]) if len(sys.argv) > 3 else None)
+        return
     minUs = float(sys.argv[2]) if len(sys.argv) > 2 else 50.0
     top = int(sys.argv[3]) if len(sys.argv) > 3 else 8
     kern, api = [], []
