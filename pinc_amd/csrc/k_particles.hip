@@ -1107,19 +1107,35 @@ __global__ __launch_bounds__(kThreads) void k_sort_count(const double *__restric
 // the sorting push's key counts: per brick, at the brick's first key (the
 // push reserves per brick; immigrants joining the counts, or counts made
 // without a counting push)
+// Cell a particle is sorted by in the in-push sort (the counting push, the
+// brick counts and the sorting push must agree): with PINC_SORT_AHEAD (the
+// default) the cell of x + v, where the next push's drift takes it before its
+// kick, so that a sorting push's output lies in the bricks it was ranked
+// into (sorted by the input cell x, the output of every block spread one
+// cell around its bricks: E and charge boxes 6 x 6 x 3 cells instead of
+// 4 x 4 x 1).  Clamped to the grid like every key (a particle that wraps
+// through a periodic face is placed at the face it left: order only).
+#ifndef PINC_SORT_AHEAD
+#define PINC_SORT_AHEAD 1
+#endif
+__device__ __forceinline__ int sort_cell(double x, double v) { return PINC_SORT_AHEAD ? (int)(x + v) : (int)x; }
+
 template <int ND>
 __global__ __launch_bounds__(kThreads) void k_count_bricks(const double *__restrict__ x0,
                                                            const double *__restrict__ x1,
-                                                           const double *__restrict__ x2, long n,
+                                                           const double *__restrict__ x2,
+                                                           const double *__restrict__ v0,
+                                                           const double *__restrict__ v1,
+                                                           const double *__restrict__ v2, long n,
                                                            TileGeo tg, int *__restrict__ counts) {
-	const double *xs[3] = {x0, x1, x2};
+	const double *xs[3] = {x0, x1, x2}, *vs[3] = {v0, v1, v2};
 	for (long base = (long)blockIdx.x * blockDim.x; base < n; base += (long)gridDim.x * blockDim.x) {
 		long i = base + threadIdx.x;
 		bool act = i < n;
 		int c[3] = {0, 0, 0};
 		if (act) {
 #pragma unroll
-			for (int d = 0; d < ND; d++) c[d] = (int)xs[d][i];
+			for (int d = 0; d < ND; d++) c[d] = sort_cell(xs[d][i], vs[d][i]);
 		}
 		agg_add(counts, act ? brick_first_key<ND>(tg, c) : 0, act);
 	}
@@ -2077,21 +2093,29 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	const Box eB = (KICK && !empty) ? make_box(clo, chi, cmid, 0, 1, ND, EC) : Box{{0, 0, 0}, {1, 1, 1}, 0};
 	const Box rB = !empty ? make_box(clo, chi, cmid, 1, 2, ND, RC) : Box{{0, 0, 0}, {1, 1, 1}, 0};
 	// (the sorting push's cell box: the core of its brick box ib below)
-	const Box iB = (SORT && !empty) ? make_box(clo, chi, cmid, 0, 0, ND, kInCellCap) : Box{{0, 0, 0}, {1, 1, 1}, 0};
+	const int ahead = PINC_SORT_AHEAD ? 1 : 0;  // (sort cells: input cells +-1, sort_cell)
+	const Box iB = (SORT && !empty) ? make_box(clo, chi, cmid, ahead, ahead, ND, kInCellCap) : Box{{0, 0, 0}, {1, 1, 1}, 0};
 	// the sorting push reserves per brick from the cursor of the brick's
 	// first cell, so the counting push counts per brick (at its first key):
 	// a block's output falls into a few bricks.  Only the brick counters live
 	// in LDS, so the cell box they cover may be 16 times their number; a
 	// brick box beyond the counters (far movers) counts in memory.
-	const Box oB = (a.cntNext && !empty) ? make_box(clo, chi, cmid, 1, 1, ND, 16 * kOutCellCap) : Box{{0, 0, 0}, {1, 1, 1}, 0};
+	const Box oB = (a.cntNext && !empty) ? make_box(clo, chi, cmid, 1 + ahead, 1 + ahead, ND, 16 * kOutCellCap)
+	                                     : Box{{0, 0, 0}, {1, 1, 1}, 0};
 	BrickBox obb = (a.cntNext && !empty) ? make_brick_box<ND>(a.tg, oB) : BrickBox{{0, 0, 0}, {1, 1, 1}, 0};
 	if (obb.vol > kOutCellCap) obb.vol = 0;
 	// sorting push: the items inside the wide brick box ib are ranked by
 	// brick (one run of each brick per block); only items outside it take a
 	// global slot one by one.  The brick counters live in cntOut, which a
 	// sorting push does not use (it never counts).
+	int slo[3] = {0, 0, 0}, shi[3] = {0, 0, 0};
+#pragma unroll
+	for (int d = 0; d < ND; d++) {
+		slo[d] = clo[d] - ahead;
+		shi[d] = chi[d] + ahead;
+	}
 	const BrickBox ib = (SORT && !empty)
-	                        ? wide_brick_box<ND>(a.tg, clo, chi, cmid, 8, kInCellCap, make_brick_box<ND>(a.tg, iB))
+	                        ? wide_brick_box<ND>(a.tg, slo, shi, cmid, 8, kInCellCap, make_brick_box<ND>(a.tg, iB))
 	                        : BrickBox{{0, 0, 0}, {1, 1, 1}, 0};
 	static_assert(kOutCellCap >= 2 * kInCellCap, "brick counters in cntOut");
 	int *const bCnt = cntOut, *const bBase = cntOut + kInCellCap;
@@ -2149,7 +2173,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 		for (int k = 0; k < kPushItems; k++) {
 			int c[3] = {0, 0, 0};
 #pragma unroll
-			for (int d = 0; d < ND; d++) c[d] = (int)p[k][d];
+			for (int d = 0; d < ND; d++) c[d] = sort_cell(p[k][d], vv[k][d]);
 			const bool ok = (valid >> k) & 1u;
 			const int lb = ok ? brick_inside<ND>(a.tg, ib, c) : -1;
 			// plain LDS atomics: a wave's lanes share a few bricks (same-address
@@ -2492,7 +2516,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 			const bool mine = (dep >> k) & 1u;
 			int c[3] = {0, 0, 0};
 #pragma unroll
-			for (int d = 0; d < ND; d++) c[d] = (int)p[k][d];
+			for (int d = 0; d < ND; d++) c[d] = sort_cell(p[k][d], vv[k][d]);
 			const int lb = mine ? brick_inside<ND>(a.tg, obb, c) : -1;
 			// (aggregated: plain atomics here, or after the deposit, cost the
 			// plain instance, which carries this code behind a runtime test,
@@ -3320,10 +3344,13 @@ extern "C" int pinc_hip_count_keys(pinc_pop_t pop, int s, long first, pinc_geom_
 	if (nb > 65536L * 8) nb = 65536L * 8;
 	int nd = g.nd;
 	const double *x0 = pop.x[0] + b0, *x1 = nd > 1 ? pop.x[1] + b0 : nullptr, *x2 = nd > 2 ? pop.x[2] + b0 : nullptr;
+	const double *v0 = pop.v[0] + b0, *v1 = nd > 1 ? pop.v[1] + b0 : nullptr, *v2 = nd > 2 ? pop.v[2] + b0 : nullptr;
 	hipStream_t st = (hipStream_t)stream;
-	if (nd == 3) hipLaunchKernelGGL(k_count_bricks<3>, dim3(nb), dim3(kThreads), 0, st, x0, x1, x2, n, tg, counts);
-	else if (nd == 2) hipLaunchKernelGGL(k_count_bricks<2>, dim3(nb), dim3(kThreads), 0, st, x0, x1, x2, n, tg, counts);
-	else hipLaunchKernelGGL(k_count_bricks<1>, dim3(nb), dim3(kThreads), 0, st, x0, x1, x2, n, tg, counts);
+	if (nd == 3)
+		hipLaunchKernelGGL(k_count_bricks<3>, dim3(nb), dim3(kThreads), 0, st, x0, x1, x2, v0, v1, v2, n, tg, counts);
+	else if (nd == 2)
+		hipLaunchKernelGGL(k_count_bricks<2>, dim3(nb), dim3(kThreads), 0, st, x0, x1, x2, v0, v1, v2, n, tg, counts);
+	else hipLaunchKernelGGL(k_count_bricks<1>, dim3(nb), dim3(kThreads), 0, st, x0, x1, x2, v0, v1, v2, n, tg, counts);
 	return check_launch("count_keys");
 }
 

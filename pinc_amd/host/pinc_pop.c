@@ -94,6 +94,12 @@ Population *pAlloc(const dictionary *ini) {
 		dv->sortInterval = iniHas(ini, "population:sortInterval") ? iniGetInt(ini, "population:sortInterval") : 8;
 		if (dv->sortInterval < 1) msg(ERROR, "population:sortInterval must be >= 1");
 		dv->tileWidth = nd == 3 ? 4 : (nd == 2 ? 8 : 32);
+		/* population:tileWidth (or PINC_TILE_WIDTH, experiments): cells per
+		 * tile edge, a power of two */
+		if (iniHas(ini, "population:tileWidth")) dv->tileWidth = iniGetInt(ini, "population:tileWidth");
+		if (getenv("PINC_TILE_WIDTH") && *getenv("PINC_TILE_WIDTH")) dv->tileWidth = atoi(getenv("PINC_TILE_WIDTH"));
+		if (dv->tileWidth < 2 || (dv->tileWidth & (dv->tileWidth - 1)))
+			msg(ERROR, "population:tileWidth must be a power of two >= 2, not %d", dv->tileWidth);
 		for (int s = 0; s < PINC_MAX_SPECIES; s++) dv->cellValid[s] = -1;
 	}
 	/* tiled + fused: the counting sort rides in every sortInterval-th push
