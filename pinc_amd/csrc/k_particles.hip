@@ -2168,7 +2168,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	// after it +1 %).
 	if (SORT) {
 		static_assert(kInCellCap <= 256 && kPushChunk <= (1 << 23), "rank/brick packing");
-		int rl[kPushItems];
+		int no = 0;  // (trace: items outside ib)
 #pragma unroll
 		for (int k = 0; k < kPushItems; k++) {
 			int c[3] = {0, 0, 0};
@@ -2182,14 +2182,11 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 			const int rank = lb >= 0 ? atomicAdd(&bCnt[lb], 1) : 0;
 			const bool out = ok && lb < 0;
 			const int g = agg_add(a.cursor, out ? brick_first_key<ND>(a.tg, c) : 0, out);
-			rl[k] = lb >= 0 ? (rank << 8 | lb) : (ok ? ~g : -1);
+			const int rl = lb >= 0 ? (rank << 8 | lb) : (ok ? ~g : -1);
+			rlL[k * kPushThreads + threadIdx.x] = rl;  // (stored at once: no item's rank stays live)
+			no += rl < 0 && ok;
 		}
-#pragma unroll
-		for (int k = 0; k < kPushItems; k++) rlL[k * kPushThreads + threadIdx.x] = rl[k];
 		if (a.diag) {
-			int no = 0;
-#pragma unroll
-			for (int k = 0; k < kPushItems; k++) no += rl[k] < 0 && ((valid >> k) & 1u);
 			no = wave_sum_i(no);
 			if (lane == 0 && no) atomicAdd(&a.diag[0], (unsigned long long)no);
 		}

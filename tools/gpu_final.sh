@@ -11,6 +11,7 @@ mkdir -p $O
 timeout -k 10 600 python -u bench.py > $O/bench_c4.json 2> $O/bench_c4.err || { tail -20 $O/bench_c4.err; exit 1; }
 cat $O/bench_c4.json
 bash tools/profile_bench.sh --steps 10 --warmup 3 > $O/profile.log 2>&1 || { tail -20 $O/profile.log; exit 1; }
+python3 tools/kernel_gaps.py gpurun_out/prof 12 > $O/${T}_kernel_gaps.txt || exit 1
 python3 tools/pmc_summary.py $T gpurun_out/prof gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/prof_bench.json > $O/pmc_summary.txt || exit 1
 cp profiles/${T}_* $O/ && cp gpurun_out/prof_bench.json $O/prof_bench_c4.json
 rm -rf gpurun_out/prof gpurun_out/pmc_fetch gpurun_out/pmc_write
