@@ -432,9 +432,15 @@ def main() -> int:
     device_sync()
     sim.sync()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        sim.step()
-        log(f"timed step {i} done at {time.perf_counter() - t0:.2f} s")
+    # the steps run in the library in chunks of 10 (no return to Python
+    # between steps; a progress line per chunk)
+    done = 0
+    chunk = 1 if os.environ.get("PINC_BENCH_PYLOOP") == "1" else 10  # (1: a Python call per step)
+    while done < args.steps:
+        k = min(chunk, args.steps - done)
+        sim.step(k)
+        done += k
+        log(f"timed steps to {done} done at {time.perf_counter() - t0:.2f} s")
     sim.sync()
     device_sync()
     barrier()

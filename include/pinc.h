@@ -362,6 +362,7 @@ PincSim *pinc_sim_create(const char *iniPath, int nOver, const char **over, cons
 void pinc_sim_free(PincSim *sim);
 int pinc_sim_init(PincSim *sim);            /* initial conditions + fields + half step */
 int pinc_sim_step(PincSim *sim);            /* one iteration of main.c:197-274 */
+int pinc_sim_steps(PincSim *sim, int n);    /* n iterations without returning to the caller */
 int pinc_sim_op(PincSim *sim, const char *op);
 int pinc_sim_energy(PincSim *sim, double *ke, double *pe, double *keSpecies); /* rank-summed */
 long pinc_sim_cycles(const PincSim *sim);

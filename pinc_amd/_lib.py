@@ -91,6 +91,7 @@ _sigs = {
     "pinc_sim_free": (None, [C.c_void_p]),
     "pinc_sim_init": (C.c_int, [C.c_void_p]),
     "pinc_sim_step": (C.c_int, [C.c_void_p]),
+    "pinc_sim_steps": (C.c_int, [C.c_void_p, C.c_int]),
     "pinc_sim_op": (C.c_int, [C.c_void_p, C.c_char_p]),
     "pinc_sim_energy": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "pinc_sim_cycles": (C.c_long, [C.c_void_p]),

@@ -488,6 +488,7 @@ void pinc_ctx_init(void) {
 	pinc_check(pinc_hip_malloc((void **)&g_pinc.dScratch, (PINC_PARTIALS + 256) * sizeof(double)),
 	           "scratch");
 	pinc_check(pinc_hip_malloc((void **)&g_pinc.dErr, 64), "err word");
+	pinc_check(pinc_hip_host_alloc((void **)&g_pinc.hPinned, 32 * sizeof(double)), "pinned host scratch");
 	pinc_check(pinc_hip_memset(g_pinc.dErr, 0, 64, g_pinc.stream), "err word");
 	if (g_pinc.nranks < 1) g_pinc.nranks = 1;
 	g_pinc.verbose = getenv("PINC_VERBOSE") ? atoi(getenv("PINC_VERBOSE")) : 0;

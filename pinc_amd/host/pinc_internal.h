@@ -25,6 +25,7 @@ typedef struct {
 	void *comm;
 	int rank, nranks;
 	double *dScratch;   /* device: 8192 partials + 256 scalar slots */
+	double *hPinned;    /* host, pinned: 32 doubles for the step's small reads */
 	int *dErr;          /* device error word (asserts) */
 	double maxVel;
 	double thr[9];      /* migration thresholds lo[nd], up[nd], assert bound[nd] */

@@ -221,8 +221,9 @@ static void sim_step(PincSim *S) {
 	pinc_pot_energy_launch(S->rho, S->phi);
 	pinc_check(pinc_hip_d2d(PINC_SLOT(4), g_pinc.dErr, sizeof(int), g_pinc.stream), "assert word");
 	g_pinc.errRead = g_pinc.errSerial;
-	double r[2];
-	pinc_check(pinc_hip_d2h(r, PINC_SLOT(3), sizeof(r), g_pinc.stream), "potential energy");
+	/* (into pinned memory: no staging copy on the host's wake-up path) */
+	double *r = g_pinc.hPinned;
+	pinc_check(pinc_hip_d2h(r, PINC_SLOT(3), 2 * sizeof(double), g_pinc.stream), "potential energy");
 	pSumKinEnergy(pop);
 	pop->potEnergy[pop->nSpecies] = 0.5 * r[0];
 	pinc_phase_end(7);
@@ -334,6 +335,11 @@ int pinc_sim_init(PincSim *S) {
 
 int pinc_sim_step(PincSim *S) {
 	sim_step(S);
+	return 0;
+}
+
+int pinc_sim_steps(PincSim *S, int n) {
+	for (int i = 0; i < n; i++) sim_step(S);
 	return 0;
 }
 

@@ -65,8 +65,12 @@ class Sim:
         HOST.pinc_sim_init(self._h)
 
     def step(self, n: int = 1) -> None:
-        for _ in range(n):
+        """n iterations of the main loop (one library call: no return to
+        Python between them)."""
+        if n == 1:
             HOST.pinc_sim_step(self._h)
+        elif n > 1:
+            HOST.pinc_sim_steps(self._h, n)
 
     def op(self, name: str) -> None:
         if HOST.pinc_sim_op(self._h, name.encode()):
