@@ -2951,6 +2951,14 @@ extern "C" int pinc_hip_move_classify(pinc_pop_t pop, int s, int doMove, const d
 	return check_launch("move_classify");
 }
 
+// pinned host words for the extraction's two small reads (a read into
+// pageable memory is staged and copied again on the host's wake-up path)
+static int *pinned_ints() {
+	static int *p = nullptr;
+	if (!p && hipHostMalloc((void **)&p, 64 * sizeof(int), hipHostMallocDefault) != hipSuccess) p = nullptr;
+	return p;
+}
+
 extern "C" int pinc_hip_extract(pinc_pop_t pop, int s, const unsigned char *flags, int *chunkCount,
                                 int center, int nNeighbors, pinc_extract_ws_t ws, long *nEmig,
                                 long *neCount, void *stream) {
@@ -2973,11 +2981,13 @@ extern "C" int pinc_hip_extract(pinc_pop_t pop, int s, const unsigned char *flag
 		hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)nsb), dim3(kThreads), 0, st, chunkCount, (long)nChunks, boff,
 		                   ws.chunkOffset);
 	}
-	int E = 0;
-	hipError_t e = hipMemcpyAsync(&E, ws.chunkOffset + nChunks, sizeof(int), hipMemcpyDeviceToHost, st);
+	int *hp = pinned_ints();
+	if (!hp) return set_error(hipErrorOutOfMemory, "extract: pinned host words");
+	hipError_t e = hipMemcpyAsync(hp, ws.chunkOffset + nChunks, sizeof(int), hipMemcpyDeviceToHost, st);
 	if (e != hipSuccess) return set_error(e, "extract: count readback");
 	e = hipStreamSynchronize(st);
 	if (e != hipSuccess) return set_error(e, "extract: sync");
+	const int E = hp[0];
 	*nEmig = E;
 	if (E == 0) return check_launch("extract(scan)");
 	if (E > ws.cap) return PINC_ERR_CAPACITY;
@@ -2994,12 +3004,12 @@ extern "C" int pinc_hip_extract(pinc_pop_t pop, int s, const unsigned char *flag
 	                   (long)E, ws.blockHist, ws.scratch, pop, sb, ws.buf, ws.cap, ws.bufNe);
 	hipLaunchKernelGGL(k_fill_holes, dim3((unsigned)ceil_div(E, 256)), dim3(256), 0, st, pop, sb,
 	                   ws.tail, ws.holes, ws.scratch);
-	int cnt[kMaxNe];
-	e = hipMemcpyAsync(cnt, ws.scratch + 64, sizeof(cnt), hipMemcpyDeviceToHost, st);
+	static_assert(kMaxNe <= 64, "pinned words");
+	e = hipMemcpyAsync(hp, ws.scratch + 64, kMaxNe * sizeof(int), hipMemcpyDeviceToHost, st);
 	if (e != hipSuccess) return set_error(e, "extract: direction counts");
 	e = hipStreamSynchronize(st);
 	if (e != hipSuccess) return set_error(e, "extract: sync 2");
-	for (int q = 0; q < kMaxNe; q++) neCount[q] = cnt[q];
+	for (int q = 0; q < kMaxNe; q++) neCount[q] = hp[q];
 	return check_launch("extract");
 }
 

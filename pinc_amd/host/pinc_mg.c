@@ -226,10 +226,10 @@ MultigridSolver *mgAllocSolver(const dictionary *ini, Grid *rho, Grid *phi) {
 	S->speculate = S->native && !S->shard && !S->useGraph && S->nLevels > 1 &&
 	               (!iniHas(ini, "multigrid:speculate") || iniGetInt(ini, "multigrid:speculate")) &&
 	               !(getenv("PINC_MG_SPECULATE") && !atoi(getenv("PINC_MG_SPECULATE")));
-	if (S->speculate) {
-		pinc_check(pinc_hip_host_alloc((void **)&S->hostNorm, sizeof(double)), "mg norm");
-		pinc_check(pinc_hip_event_create(&S->normEvent), "mg norm");
-	}
+	/* the norm is read into pinned memory (no staging copy on the host's
+	 * wake-up path), with an event when speculating */
+	pinc_check(pinc_hip_host_alloc((void **)&S->hostNorm, sizeof(double)), "mg norm");
+	if (S->speculate) pinc_check(pinc_hip_event_create(&S->normEvent), "mg norm");
 	if (S->native && S->nLevels >= 2 && iniHas(ini, "multigrid:spectralCoarse") &&
 	    iniGetInt(ini, "multigrid:spectralCoarse")) {
 		pinc_check(pinc_hip_fft_create(&S->fftCoarse, S->L[1].nd, S->L[1].T, g_pinc.stream), "mg spectral coarse");
@@ -692,7 +692,8 @@ void mgSolve(MultigridSolver *S, Grid *rho, Grid *phi, const MpiInfo *mpiInfo) {
 				pinc_check(pinc_hip_event_sync(S->normEvent), "norm");
 				sum = *S->hostNorm;
 			} else {
-				pinc_check(pinc_hip_d2h(&sum, PINC_SLOT(TMP_SLOT + 1), sizeof(double), g_pinc.stream), "norm");
+				pinc_check(pinc_hip_d2h(S->hostNorm, PINC_SLOT(TMP_SLOT + 1), sizeof(double), g_pinc.stream), "norm");
+				sum = *S->hostNorm;
 			}
 			barRes = sqrt(sum / S->Ng0);
 			if (S->histN < S->histCap) S->hist[S->histN] = barRes;
