@@ -281,6 +281,10 @@ def main() -> int:
     ap.add_argument("--mg-extrapolate", type=int, default=1,
                     help="1: native multigrid starts each solve from 2 phi_n - phi_(n-1) instead of phi_n "
                          "(multigrid:extrapolate; with an object, the two solves of a step from their own histories)")
+    ap.add_argument("--mg-smooth", default="4,4",
+                    help="native multigrid: smoothing counts PRE,POST (multigrid:nPreSmooth/nPostSmooth; default "
+                         "4,4, the measured best at C4: 4 two-grid cycles per solve instead of 3 at the ini's 10,10, "
+                         "same 1e-10 stop; 'ini' keeps the ini's)")
     ap.add_argument("--mg", default="native", choices=["native", "reference"],
                     help="native: correction-scheme V-cycle with the coarse h^2 factor (default; the reference "
                          "algorithm does not converge at 256^3 with 5 levels, DESIGN.md section 6); reference: "
@@ -394,7 +398,8 @@ def main() -> int:
                                obj_second_guess=args.obj_second_guess, c5_fused=args.c5_fused, layout=args.layout,
                                sort_interval=args.sort_interval, sort_in_push=args.sort_in_push,
                                sort_fraction=args.sort_fraction, sort_max=args.sort_max,
-                               sort_spread=args.sort_spread)
+                               sort_spread=args.sort_spread,
+                               mg_smooth=args.mg_smooth if args.mg == "native" and args.mg_smooth != "ini" else None)
     nspecies = int(cfg["population"]["nSpecies"])
     ini = configs.write_ini(cfg)
     spread_note = (f" and the blocks' mean cell box grew {args.sort_spread:g}x since the last sort"
@@ -550,7 +555,8 @@ def main() -> int:
                         (f"multigrid mgVRecursive, 2 levels used ({S}^{nd}, {S // 2}^{nd} solved exactly), "
                          if args.mg == "native" and args.mg_spectral_coarse else
                          f"multigrid mgVRecursive, {mg_levels} levels ({S}^{nd} down to {S >> (mg_levels - 1)}^{nd}), ")
-                        + "RB Gauss-Seidel 10/10/10, "
+                        + (f"RB Gauss-Seidel {cfg['multigrid']['nPreSmooth']}/{cfg['multigrid']['nPostSmooth']}/"
+                           f"{cfg['multigrid']['nCoarseSolve']} (pre/post/coarse), ")
                         + ("native mode (correction scheme, coarse h^2 factor; the ini's 5 levels extended"
                            + (("; initial guesses extrapolated: the first solve of a step from the last two "
                                "steps' first solutions, the second from the first + "

@@ -111,6 +111,7 @@ def ini_for(size: int, levels: int, *, native: bool = False, stack: bool = False
     """One 3-D subdomain of size^3 (the warm family's grid keys); native:
     the native V-cycle; stack: the bench's whole solver stack
     (configs.bench_config: native, extrapolated guess, FFT coarse solve,
+    the bench's smoothing counts,
     multigrid:shard as given -- 'auto' is the bench's, which keeps one rank
     replicated; '1' runs the sharded level 0 with its deep halo on one
     rank)."""
@@ -122,6 +123,9 @@ def ini_for(size: int, levels: int, *, native: bool = False, stack: bool = False
         cfg["multigrid"]["shard"] = shard
         cfg["multigrid"]["extrapolate"] = "1"
         cfg["multigrid"]["spectralCoarse"] = "1"
+        bench_mg = configs.bench_config("c4", size=size, ppc=1)["multigrid"]
+        cfg["multigrid"]["nPreSmooth"] = bench_mg["nPreSmooth"]
+        cfg["multigrid"]["nPostSmooth"] = bench_mg["nPostSmooth"]
     return configs.write_ini(cfg)
 
 

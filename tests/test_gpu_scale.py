@@ -86,7 +86,9 @@ def test_c4_per_gpu_load_matches_oracle(built):
     for row in log:
         print("step %d KE %.12g/%.12g PE %.12g/%.12g cycles %d/%d  gpu %.2fs cpu %.2fs" % row)
     assert sorts >= 2 and plain > sorts, (sorts, plain)
-    assert sum(g for g, _ in cyc) <= 3 * steps + 2   # the extrapolated guess: ~3 cycles per solve
+    # the extrapolated guess with the bench's 4/4 smoothing: ~4 two-grid
+    # cycles per solve (3 at the ini's 10/10)
+    assert sum(g for g, _ in cyc) <= 4 * steps + 2
 
 
 _C4TS_SORTS = {}
