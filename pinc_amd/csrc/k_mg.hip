@@ -29,6 +29,11 @@ constexpr int kMaxBlocks = 2048;
 inline long ceil_div(long a, long b) { return (a + b - 1) / b; }
 
 
+// 1: the 3-D residual norm on x pairs (k_residual_sumsq3p)
+#ifndef PINC_MG_NORM_PAIRS
+#define PINC_MG_NORM_PAIRS 1
+#endif
+
 struct Lv {
 	int T[3];
 	long s[3];
@@ -173,6 +178,49 @@ __global__ __launch_bounds__(kThreads) void k_residual_sumsq(const double *__res
 		}
 		double v = residual_at<ND>(phi, rho, L, c, g);
 		acc += v * v;
+	}
+	double t = block_sum(acc, red);
+	if (threadIdx.x == 0) partial[blockIdx.x] = t;
+}
+
+// k_residual_sumsq<3> on x pairs (x even): the point and its x+1 neighbour,
+// and the pairs of the y and z neighbour rows, as 16-B loads, the outer x
+// neighbours as 8-B loads.  Each residual is residual_at's expression in its
+// order; only the order of the squares' sum differs.  Levels with an even x
+// extent and 16-B aligned arrays.
+__global__ __launch_bounds__(kThreads) void k_residual_sumsq3p(const double *__restrict__ phi,
+                                                               const double *__restrict__ rho, pinc_lvl_t Lp,
+                                                               double *__restrict__ partial) {
+	__shared__ double red[kThreads / 64];
+	const unsigned T0 = Lp.T[0], T1 = Lp.T[1], T2 = Lp.T[2];
+	const unsigned hx = T0 / 2;
+	const long sy = T0, sz = (long)T0 * T1;
+	const long n2 = (long)hx * T1 * T2;
+	double acc = 0.;
+	const Walk w = point_walk(n2);
+	for (long q = w.g0; q < w.g1; q += w.step) {
+		const unsigned u = (unsigned)q, r = u / hx;
+		const int x = 2 * (int)(u - r * hx), y = (int)(r % T1), z = (int)(r / T1);
+		const long g = (long)x + y * sy + z * sz;
+		const long oym = y > 0 ? -sy : (long)(T1 - 1) * sy, oyp = y + 1 < (int)T1 ? sy : -(long)(T1 - 1) * sy;
+		const long ozm = z > 0 ? -sz : (long)(T2 - 1) * sz, ozp = z + 1 < (int)T2 ? sz : -(long)(T2 - 1) * sz;
+		const long oxm = x > 0 ? -1 : (long)T0 - 1, oxp = x + 2 < (int)T0 ? 2 : 2 - (long)T0;
+		const double2 c = *reinterpret_cast<const double2 *>(phi + g);
+		const double2 pr = *reinterpret_cast<const double2 *>(rho + g);
+		const double2 ym = *reinterpret_cast<const double2 *>(phi + g + oym);
+		const double2 yp = *reinterpret_cast<const double2 *>(phi + g + oyp);
+		const double2 zm = *reinterpret_cast<const double2 *>(phi + g + ozm);
+		const double2 zp = *reinterpret_cast<const double2 *>(phi + g + ozp);
+		const double xm0 = phi[g + oxm], xp1 = phi[g + oxp];
+		// residual_at<3>: -6 phi + (x+ + x- + y+ + y- + z+ + z-) + rho
+		double r0 = -6. * c.x;
+		r0 += c.y + xm0 + yp.x + ym.x + zp.x + zm.x;
+		r0 = r0 + pr.x;
+		double r1 = -6. * c.y;
+		r1 += xp1 + c.x + yp.y + ym.y + zp.y + zm.y;
+		r1 = r1 + pr.y;
+		acc += r0 * r0;
+		acc += r1 * r1;
 	}
 	double t = block_sum(acc, red);
 	if (threadIdx.x == 0) partial[blockIdx.x] = t;
@@ -1381,7 +1429,12 @@ extern "C" int pinc_hip_residual_sumsq(const double *phi, const double *rho, pin
 	hipStream_t st = (hipStream_t)stream;
 	unsigned nb = blocks_for(npts(L));
 	*nBlocks = (int)nb;
-	if (L.nd == 3) hipLaunchKernelGGL(k_residual_sumsq<3>, dim3(nb), dim3(kThreads), 0, st, phi, rho, L, partial);
+	if (L.nd == 3 && PINC_MG_NORM_PAIRS && L.T[0] % 2 == 0 &&
+	    !((reinterpret_cast<unsigned long>(phi) | reinterpret_cast<unsigned long>(rho)) & 15)) {
+		nb = blocks_for(npts(L) / 2);
+		*nBlocks = (int)nb;
+		hipLaunchKernelGGL(k_residual_sumsq3p, dim3(nb), dim3(kThreads), 0, st, phi, rho, L, partial);
+	} else if (L.nd == 3) hipLaunchKernelGGL(k_residual_sumsq<3>, dim3(nb), dim3(kThreads), 0, st, phi, rho, L, partial);
 	else if (L.nd == 2) hipLaunchKernelGGL(k_residual_sumsq<2>, dim3(nb), dim3(kThreads), 0, st, phi, rho, L, partial);
 	else hipLaunchKernelGGL(k_residual_sumsq<1>, dim3(nb), dim3(kThreads), 0, st, phi, rho, L, partial);
 	return check_launch("residual_sumsq");

@@ -3059,6 +3059,7 @@ extern "C" int pinc_hip_deposit(pinc_pop_t pop, int s, pinc_geom_t g, double *rh
 
 extern "C" int pinc_hip_field_chain(const double *E, double *Es, long n, const double *qm,
                                     const double *mq, double pre, int s, void *stream) {
+	if (n > 0 && (!E || !Es || !qm || !mq)) return set_error(hipErrorInvalidValue, "field_chain: null array");
 	if (n <= 0) return 0;
 	long nb = ceil_div(n, (long)kThreads * 4);
 	if (nb > 8192) nb = 8192;
@@ -3071,6 +3072,7 @@ extern "C" int pinc_hip_accelerate(pinc_pop_t pop, int s, pinc_geom_t g, const d
 	long n = pop.iStop[s] - pop.iStart[s];
 	*nBlocks = 0;
 	if (n <= 0) return 0;
+	if (!Es) return set_error(hipErrorInvalidValue, "accelerate: null E");
 	long b0 = pop.iStart[s];
 	long nb = ceil_div(n + (b0 & 1L), (long)kAccChunk);
 	*nBlocks = (int)nb;
@@ -3317,6 +3319,7 @@ extern "C" int pinc_hip_push(pinc_pop_t pop, int s, pinc_geom_t g, const pinc_pu
 	*nBlocks = (int)nb;
 	hipStream_t st = (hipStream_t)stream;
 	const bool kick = args->kick != 0;
+	if (kick && !args->Es) return set_error(hipErrorInvalidValue, "push: kick without E");
 	// a sorting push never counts (its brick counters use the count's LDS)
 	if (sort) a.cntNext = nullptr;
 #define LAUNCH_PUSH(ND, V3D, OBJ)                                                                                       \
