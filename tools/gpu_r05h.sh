@@ -1,6 +1,10 @@
+# round-5 final tree: full GPU suite, smoke, then the evidence run (bench
+# lines, rocprof stats, PMC passes, kernel gaps) under the tag r05h
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/r05h
-timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_reference_kat.py -x -q --timeout 200 --timeout-method thread -m gpu > gpurun_out/r05h/tests.log 2>&1 || { tail -30 gpurun_out/r05h/tests.log; exit 1; }
-tail -2 gpurun_out/r05h/tests.log
-bash tools/gpu_ab.sh r05h prev:pinc_amd/lib_prev new:pinc_amd/lib -- --steps 10 --warmup 3
+timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > gpurun_out/r05h/gpu_full_suite.log 2>&1 || { tail -30 gpurun_out/r05h/gpu_full_suite.log; exit 1; }
+tail -1 gpurun_out/r05h/gpu_full_suite.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/r05h/smoke.log 2>&1 || { tail -20 gpurun_out/r05h/smoke.log; exit 1; }
+tail -1 gpurun_out/r05h/smoke.log
+bash tools/gpu_final.sh r05h
