@@ -54,7 +54,7 @@ ROCPROF_NAMES = {
     "accelerate": "k_accel<3, true, true>",
     "move_classify": "k_move_classify<3>",
     "deposit": "k_deposit_tiled<3, true>",
-    "residual_sumsq": "k_residual_sumsq<3>",
+    "residual_sumsq": "k_residual_sumsq3p",
     "mg_cycle": "one V-cycle, replayed as a HIP graph (all levels)",
 }
 
