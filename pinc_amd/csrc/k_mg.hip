@@ -792,12 +792,34 @@ struct S4Node {
 	unsigned roff;     // byte offset of the node in a plane of the level
 };
 
+// diagnostics only (timing by elimination, wrong results): bit 0 skips the
+// rho loads, bit 1 the phi fetch, bit 2 pads LDS to two workgroups per CU
+#ifndef PINC_MG_S4_DIAG
+#define PINC_MG_S4_DIAG 0
+#endif
+// 1: rho rides in an LDS ring of its own, fetched like phi (three
+// row-contiguous loads per thread and step) and read by each stage from its
+// node's LDS index; 0: each thread gathers the rho of its four stages' nodes
+// from memory (five colour-strided 8-B gathers per step, every value loaded
+// four times).  Elimination builds (PINC_MG_S4_DIAG) put the gathers at half
+// the launch: 0.168 ms with them, 0.089 ms without, while halving the
+// workgroups per CU costs 5 %; the ring takes 80 KB, two workgroups per CU
+#ifndef PINC_MG_S4_RHOLDS
+#define PINC_MG_S4_RHOLDS 1
+#endif
 template <int SX, int SY, int NT>
 __global__ __launch_bounds__(NT) void k_gs_sweep4c(const double *__restrict__ phiIn, double *__restrict__ phiOut,
                                                    const double *__restrict__ rho, pinc_lvl_t Lp, int zPlanes) {
 	using S = Sweep4c<SX, SY, NT>;
 	constexpr int H = S::H, HX = S::HX, HW = S::HW, PL = S::PL;
 	__shared__ double L[8 * PL];
+#if PINC_MG_S4_RHOLDS
+	__shared__ double Rl[8 * PL];
+#endif
+#if PINC_MG_S4_DIAG & 4
+	__shared__ double padL[38 * 128];
+	if (zPlanes < 0) padL[threadIdx.x] = 1.0, phiOut[threadIdx.x] = padL[(threadIdx.x * 7) % (38 * 128)];
+#endif
 	const int TX = Lp.T[0], TY = Lp.T[1], TZ = Lp.T[2];
 	const long sz = (long)TX * TY;
 	const int ntx = TX / SX, nty = TY / SY;
@@ -861,6 +883,10 @@ __global__ __launch_bounds__(NT) void k_gs_sweep4c(const double *__restrict__ ph
 	// branch the compiler's vmcnt waits cannot count the newer loads in
 	// flight and wait for the prefetch just issued
 	auto fetch = [&](int q, double *f) {
+#if PINC_MG_S4_DIAG & 2
+		f[0] = f[1] = f[2] = (double)q;
+		return;
+#endif
 		const double *b = plane(phiIn, q);
 		f[0] = at(b, foff[0]);
 		f[1] = at(b, foff[1]);
@@ -871,11 +897,32 @@ __global__ __launch_bounds__(NT) void k_gs_sweep4c(const double *__restrict__ ph
 		L[slot * PL + fli[1]] = f[1];
 		if (f2ok) L[slot * PL + fli[2]] = f[2];
 	};
+#if PINC_MG_S4_RHOLDS
+	auto fetchR = [&](int q, double *f) {
+#if PINC_MG_S4_DIAG & 1
+		f[0] = f[1] = f[2] = (double)q;
+		return;
+#endif
+		const double *b = plane(rho, q);
+		f[0] = at(b, foff[0]);
+		f[1] = at(b, foff[1]);
+		f[2] = at(b, foff[2]);
+	};
+	auto putRho = [&](int slot, const double *f) {
+		Rl[slot * PL + fli[0]] = f[0];
+		Rl[slot * PL + fli[1]] = f[1];
+		if (f2ok) Rl[slot * PL + fli[2]] = f[2];
+	};
+#endif
 	struct Rho {
 		double r1[2], b1, r2, b2;
 	};
 	// rho of the four stages of step t (t of parity PT)
 	auto fetchRho = [&](int t, int PT, Rho &R) {
+#if PINC_MG_S4_DIAG & 1
+		R.r1[0] = R.r1[1] = R.b1 = R.r2 = R.b2 = (double)t;
+		return;
+#endif
 		const double *b3 = plane(rho, t + 3), *b2p = plane(rho, t + 2), *b0 = plane(rho, t), *bm = plane(rho, t - 2);
 		R.r1[0] = at(b3, r1n[PT ^ 1][0].roff);
 		R.r1[1] = at(b3, r1n[PT ^ 1][1].roff);
@@ -913,12 +960,23 @@ __global__ __launch_bounds__(NT) void k_gs_sweep4c(const double *__restrict__ ph
 		putPhi(q & 7, F[0]);
 	}
 	fetch(z0 - 1, F[1]);
+#if PINC_MG_S4_RHOLDS
+	// rho planes on the phi ring's schedule: z0-4 .. z0-2 into LDS, z0-1 into
+	// G[1]; plane s+6 fetched and s+5 stored at step s
+	double G[2][3];
+	for (int q = z0 - 4; q <= z0 - 2; q++) {
+		fetchR(q, G[0]);
+		putRho(q & 7, G[0]);
+	}
+	fetchR(z0 - 1, G[1]);
+#else
 	// rho of step k in R[k % 3], loaded two steps ahead; the unroll over 24
 	// steps keeps the rotation in register names (a copy of a set just
 	// loaded would wait for its loads every step)
 	Rho R[3];
 	fetchRho(z0 - 6, 0, R[0]);
 	fetchRho(z0 - 5, 1, R[1]);
+#endif
 	__syncthreads();
 	const int zEnd = z0 + zPlanes;  // outputs z0 .. zEnd-1
 	// steps s = z0-6 .. zEnd+1: zPlanes + 8 of them (a multiple of 24), in
@@ -930,36 +988,63 @@ __global__ __launch_bounds__(NT) void k_gs_sweep4c(const double *__restrict__ ph
 			const int s = s0 + k;
 			const int P = k & 1;  // parity of s (s0 even)
 			auto sl = [&](int d) { return (2 + k + d) & 7; };
+#if PINC_MG_S4_RHOLDS
+			// rho of a stage's node: its LDS index in the plane's rho slot
+			auto rr = [&](int SL, unsigned li) { return Rl[SL * PL + li]; };
+			fetch(s + 6, F[P]);
+			fetchR(s + 6, G[P]);
+#else
 			Rho &RA = R[k % 3];
 			// two steps ahead of their use (the last step's loads are unused)
 			fetch(s + 6, F[P]);
 			fetchRho(s + 2, P, R[(k + 2) % 3]);
+#endif
 			if (s + 3 <= zEnd + 2) {  // red, 1st iteration, plane s+3 (parity P^1)
 				const S4Node &a = r1n[P ^ 1][0], &b = r1n[P ^ 1][1];
-				const double va = upd(sl(3), sl(2), sl(4), a.li, a.lxm, RA.r1[0]);
+#if PINC_MG_S4_RHOLDS
+				const double ra = rr(sl(3), a.li), rb = rr(sl(3), b.li);
+#else
+				const double ra = RA.r1[0], rb = RA.r1[1];
+#endif
+				const double va = upd(sl(3), sl(2), sl(4), a.li, a.lxm, ra);
 				double vb = 0;
-				if (r1second) vb = upd(sl(3), sl(2), sl(4), b.li, b.lxm, RA.r1[1]);
+				if (r1second) vb = upd(sl(3), sl(2), sl(4), b.li, b.lxm, rb);
 				L[sl(3) * PL + a.li] = va;
 				if (r1second) L[sl(3) * PL + b.li] = vb;
 			}
 			if (s >= z0 - 1 && s <= zEnd && r2ok) {  // red, 2nd, plane s
 				const S4Node &a = r2n[P];
+#if PINC_MG_S4_RHOLDS
+				L[sl(0) * PL + a.li] = upd(sl(0), sl(-1), sl(1), a.li, a.lxm, rr(sl(0), a.li));
+#else
 				L[sl(0) * PL + a.li] = upd(sl(0), sl(-1), sl(1), a.li, a.lxm, RA.r2);
+#endif
 			}
 			{  // black, 2nd, plane s-2: out.  Before the first output plane the
 			   // store goes to plane z0, rewritten with its value later (the
 			   // store is unconditional for the same reason as the loads)
 				double v = L[sl(-2) * PL + oli];
+#if PINC_MG_S4_RHOLDS
+				if (oblack0 ^ P) v = upd(sl(-2), sl(-3), sl(-1), oli, olxm, rr(sl(-2), oli));
+#else
 				if (oblack0 ^ P) v = upd(sl(-2), sl(-3), sl(-1), oli, olxm, RA.b2);
+#endif
 				*(double *)((char *)plane(phiOut, s - 2 >= z0 ? s - 2 : z0) + ooff) = v;
 			}
 			__syncthreads();
 			if (s + 2 >= z0 - 2 && s + 2 <= zEnd + 1 && b1ok) {  // black, 1st, plane s+2
 				const S4Node &a = b1n[P];
+#if PINC_MG_S4_RHOLDS
+				L[sl(2) * PL + a.li] = upd(sl(2), sl(1), sl(3), a.li, a.lxm, rr(sl(2), a.li));
+#else
 				L[sl(2) * PL + a.li] = upd(sl(2), sl(1), sl(3), a.li, a.lxm, RA.b1);
+#endif
 			}
 			// phi s+5 into the slot of s-3 (last read by the black output above)
 			putPhi(sl(5), F[P ^ 1]);
+#if PINC_MG_S4_RHOLDS
+			putRho(sl(5), G[P ^ 1]);  // (rho s-3: last read by the black output a step ago)
+#endif
 			__syncthreads();
 		}
 	}
