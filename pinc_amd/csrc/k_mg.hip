@@ -807,6 +807,12 @@ struct S4Node {
 #ifndef PINC_MG_S4_RHOLDS
 #define PINC_MG_S4_RHOLDS 1
 #endif
+// with the rho ring: phi and rho planes fetched this many steps ahead of
+// the step that stores them to LDS minus one (2: plane s+6 at step s; 3:
+// s+7, one register set more, for two workgroups per CU)
+#ifndef PINC_MG_S4_AHEAD
+#define PINC_MG_S4_AHEAD 2
+#endif
 template <int SX, int SY, int NT>
 __global__ __launch_bounds__(NT) void k_gs_sweep4c(const double *__restrict__ phiIn, double *__restrict__ phiOut,
                                                    const double *__restrict__ rho, pinc_lvl_t Lp, int zPlanes) {
@@ -954,21 +960,25 @@ __global__ __launch_bounds__(NT) void k_gs_sweep4c(const double *__restrict__ ph
 
 	// prologue: phi z0-4 .. z0-2 into LDS, z0-1 into F[1]; rho of the first
 	// two steps (z0 is a multiple of 8: plane q sits in slot q & 7)
-	double F[2][3];
+	constexpr int A = PINC_MG_S4_RHOLDS ? PINC_MG_S4_AHEAD : 2;
+	static_assert(A == 2 || A == 3, "24-step unroll: register sets rotate by 2 or 3");
+	double F[A][3];
 	for (int q = z0 - 4; q <= z0 - 2; q++) {
 		fetch(q, F[0]);
 		putPhi(q & 7, F[0]);
 	}
 	fetch(z0 - 1, F[1]);
+	if (A == 3) fetch(z0, F[2]);
 #if PINC_MG_S4_RHOLDS
 	// rho planes on the phi ring's schedule: z0-4 .. z0-2 into LDS, z0-1 into
 	// G[1]; plane s+6 fetched and s+5 stored at step s
-	double G[2][3];
+	double G[A][3];
 	for (int q = z0 - 4; q <= z0 - 2; q++) {
 		fetchR(q, G[0]);
 		putRho(q & 7, G[0]);
 	}
 	fetchR(z0 - 1, G[1]);
+	if (A == 3) fetchR(z0, G[2]);
 #else
 	// rho of step k in R[k % 3], loaded two steps ahead; the unroll over 24
 	// steps keeps the rotation in register names (a copy of a set just
@@ -991,8 +1001,10 @@ __global__ __launch_bounds__(NT) void k_gs_sweep4c(const double *__restrict__ ph
 #if PINC_MG_S4_RHOLDS
 			// rho of a stage's node: its LDS index in the plane's rho slot
 			auto rr = [&](int SL, unsigned li) { return Rl[SL * PL + li]; };
-			fetch(s + 6, F[P]);
-			fetchR(s + 6, G[P]);
+			// plane s+4+A into set k % A; the set stored below, plane s+5,
+			// was fetched A-1 steps ago into set (k + 1) % A
+			fetch(s + 4 + A, F[k % A]);
+			fetchR(s + 4 + A, G[k % A]);
 #else
 			Rho &RA = R[k % 3];
 			// two steps ahead of their use (the last step's loads are unused)
@@ -1041,9 +1053,9 @@ __global__ __launch_bounds__(NT) void k_gs_sweep4c(const double *__restrict__ ph
 #endif
 			}
 			// phi s+5 into the slot of s-3 (last read by the black output above)
-			putPhi(sl(5), F[P ^ 1]);
+			putPhi(sl(5), F[(k + 1) % A]);
 #if PINC_MG_S4_RHOLDS
-			putRho(sl(5), G[P ^ 1]);  // (rho s-3: last read by the black output a step ago)
+			putRho(sl(5), G[(k + 1) % A]);  // (rho s-3: last read by the black output a step ago)
 #endif
 			__syncthreads();
 		}
