@@ -813,6 +813,12 @@ struct S4Node {
 #ifndef PINC_MG_S4_AHEAD
 #define PINC_MG_S4_AHEAD 2
 #endif
+// 1: the phi and rho plane fetches as 16-B x pairs (two loads per thread
+// and plane, the second on the last wave) instead of three 8-B loads
+#ifndef PINC_MG_S4_PAIRS
+#define PINC_MG_S4_PAIRS 1
+#endif
+typedef double s4pair __attribute__((ext_vector_type(2)));
 template <int SX, int SY, int NT>
 __global__ __launch_bounds__(NT) void k_gs_sweep4c(const double *__restrict__ phiIn, double *__restrict__ phiOut,
                                                    const double *__restrict__ rho, pinc_lvl_t Lp, int zPlanes) {
@@ -883,11 +889,52 @@ __global__ __launch_bounds__(NT) void k_gs_sweep4c(const double *__restrict__ ph
 	auto at = [](const double *base, unsigned byteOff) {
 		return *(const double *)((const char *)base + byteOff);
 	};
+#if PINC_MG_S4_PAIRS
+	// x pairs of the region (x0 and the region's first column are even, and
+	// so is the level's x extent: a pair never straddles the periodic wrap
+	// and is 16-B aligned): pair q = tid, and q = tid + 64 on the last wave
+	static_assert(PL % 2 == 0 && HX % 2 == 0 && PL / 2 > NT && PL / 2 - NT <= 64, "pair slots");
+	typedef s4pair FV;
+	constexpr int FN = 2;
+	unsigned qoff[2], qli[2];
+	const bool q1ok = tid >= NT - (PL / 2 - NT);
+#pragma unroll
+	for (int k = 0; k < 2; k++) {
+		int q = k == 0 ? tid : tid + (PL / 2 - NT);
+		if (q >= PL / 2) q = 0;
+		const int c = q % (HX / 2), ly = q / (HX / 2);
+		qoff[k] = poff(x0 + 2 * c - H, y0 + ly - H);
+		qli[k] = lidx(2 * c, ly);  // (x + 1 at qli + HW)
+	}
+	auto atp = [](const double *base, unsigned byteOff) {
+		return *(const s4pair *)((const char *)base + byteOff);
+	};
+#else
+	typedef double FV;
+	constexpr int FN = 3;
+#endif
 	auto plane = [&](const double *a, int q) { return a + (long)wrapi(q, TZ) * sz; };
 	// every load below is issued unconditionally (idle lanes and steps past
 	// the end load a valid element they do not use): with loads under a
 	// branch the compiler's vmcnt waits cannot count the newer loads in
 	// flight and wait for the prefetch just issued
+#if PINC_MG_S4_PAIRS
+	auto fetchP = [&](const double *a, int q, FV *f) {
+		const double *b = plane(a, q);
+		f[0] = atp(b, qoff[0]);
+		f[1] = atp(b, qoff[1]);
+	};
+	auto putP = [&](double *R, int slot, const FV *f) {
+		R[slot * PL + qli[0]] = f[0].x;
+		R[slot * PL + qli[0] + HW] = f[0].y;
+		if (q1ok) {
+			R[slot * PL + qli[1]] = f[1].x;
+			R[slot * PL + qli[1] + HW] = f[1].y;
+		}
+	};
+	auto fetch = [&](int q, FV *f) { fetchP(phiIn, q, f); };
+	auto putPhi = [&](int slot, const FV *f) { putP(L, slot, f); };
+#else
 	auto fetch = [&](int q, double *f) {
 #if PINC_MG_S4_DIAG & 2
 		f[0] = f[1] = f[2] = (double)q;
@@ -903,7 +950,11 @@ __global__ __launch_bounds__(NT) void k_gs_sweep4c(const double *__restrict__ ph
 		L[slot * PL + fli[1]] = f[1];
 		if (f2ok) L[slot * PL + fli[2]] = f[2];
 	};
-#if PINC_MG_S4_RHOLDS
+#endif
+#if PINC_MG_S4_RHOLDS && PINC_MG_S4_PAIRS
+	auto fetchR = [&](int q, FV *f) { fetchP(rho, q, f); };
+	auto putRho = [&](int slot, const FV *f) { putP(Rl, slot, f); };
+#elif PINC_MG_S4_RHOLDS
 	auto fetchR = [&](int q, double *f) {
 #if PINC_MG_S4_DIAG & 1
 		f[0] = f[1] = f[2] = (double)q;
@@ -962,7 +1013,7 @@ __global__ __launch_bounds__(NT) void k_gs_sweep4c(const double *__restrict__ ph
 	// two steps (z0 is a multiple of 8: plane q sits in slot q & 7)
 	constexpr int A = PINC_MG_S4_RHOLDS ? PINC_MG_S4_AHEAD : 2;
 	static_assert(A == 2 || A == 3, "24-step unroll: register sets rotate by 2 or 3");
-	double F[A][3];
+	FV F[A][FN];
 	for (int q = z0 - 4; q <= z0 - 2; q++) {
 		fetch(q, F[0]);
 		putPhi(q & 7, F[0]);
@@ -972,7 +1023,7 @@ __global__ __launch_bounds__(NT) void k_gs_sweep4c(const double *__restrict__ ph
 #if PINC_MG_S4_RHOLDS
 	// rho planes on the phi ring's schedule: z0-4 .. z0-2 into LDS, z0-1 into
 	// G[1]; plane s+6 fetched and s+5 stored at step s
-	double G[A][3];
+	FV G[A][FN];
 	for (int q = z0 - 4; q <= z0 - 2; q++) {
 		fetchR(q, G[0]);
 		putRho(q & 7, G[0]);
@@ -1588,6 +1639,9 @@ extern "C" int pinc_hip_gs_sweep2x(const double *phiIn, double *phiOut, const do
 	// >= 1024 workgroups where the level allows (at least 16)
 	if (L.nd != 3 || L.T[0] % 32 || L.T[1] % 8 || L.T[2] % 16)
 		return set_error(hipErrorInvalidValue, "gs_sweep2x: level not a multiple of the 32x8x16 tile");
+	if ((reinterpret_cast<unsigned long>(phiIn) | reinterpret_cast<unsigned long>(phiOut) |
+	     reinterpret_cast<unsigned long>(rho)) & 15)
+		return set_error(hipErrorInvalidValue, "gs_sweep2x: arrays not 16-byte aligned (x-pair fetches)");
 	long cols = (long)(L.T[0] / 32) * (L.T[1] / 8);
 	int zp = 16;
 	for (int z = 64; z > 16; z /= 2)
