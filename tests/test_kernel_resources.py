@@ -14,7 +14,7 @@ from pinc_amd import build
 # least waves per SIMD they are designed for
 HOT = {
     "k_pushILi3E": 4,           # every 3-D fused push instance (plain / count / sort, objects)
-    "k_gs_sweep4cILi32ELi8ELi256E": 4,
+    "k_gs_sweep4cILi32ELi8ELi256E": 2,  # (round 5: phi and rho rings, 80 KB of LDS: two workgroups per CU)
     "k_gs_sweep2ILi32ELi8ELi256E": 1,
     "k_resid_restrict3": 1,
     "k_prolong_add3c": 1,
