@@ -33,6 +33,10 @@ inline long ceil_div(long a, long b) { return (a + b - 1) / b; }
 #ifndef PINC_MG_NORM_PAIRS
 #define PINC_MG_NORM_PAIRS 1
 #endif
+// 1: the level-0 residual and restriction on x pairs (k_resid_restrict3p)
+#ifndef PINC_MG_RR_PAIRS
+#define PINC_MG_RR_PAIRS 1
+#endif
 
 struct Lv {
 	int T[3];
@@ -1465,6 +1469,70 @@ __global__ __launch_bounds__(kThreads) void k_resid_restrict3(const double *__re
 	}
 }
 
+// k_resid_restrict3 with the fine values read as 16-B x pairs: a coarse
+// point's seven residuals need phi on 19 pairs of rows around its fine point
+// and rho on 6, instead of 56 single loads.  Each residual is residual_at's
+// expression, the restriction the same sum: bit-identical.  Fine x extent
+// even and 16-B aligned arrays (the launcher checks).
+template <bool HW3D>
+__global__ __launch_bounds__(kThreads) void k_resid_restrict3p(const double *__restrict__ phi,
+                                                               const double *__restrict__ rho,
+                                                               double *__restrict__ coarse, pinc_lvl_t Lcp,
+                                                               double scale) {
+	const int FX = 2 * Lcp.T[0], FY = 2 * Lcp.T[1], FZ = 2 * Lcp.T[2];
+	const long sy = FX, sz = (long)FX * FY;
+	const unsigned CX = Lcp.T[0], CY = Lcp.T[1];
+	const unsigned n = CX * CY * (unsigned)Lcp.T[2];
+	for (unsigned gc = blockIdx.x * blockDim.x + threadIdx.x; gc < n; gc += gridDim.x * blockDim.x) {
+		const unsigned r = gc / CX;
+		const int X = 2 * (int)(gc - r * CX), Y = 2 * (int)(r % CY), Z = 2 * (int)(r / CY);
+		auto wy = [&](int y) { return (long)(y < 0 ? y + FY : (y >= FY ? y - FY : y)) * sy; };
+		auto wz = [&](int z) { return (long)(z < 0 ? z + FZ : (z >= FZ ? z - FZ : z)) * sz; };
+		const int xm2 = X >= 2 ? X - 2 : X - 2 + FX, xp2 = X + 2 < FX ? X + 2 : X + 2 - FX;
+		auto pr = [](const double *a, long o) { return *reinterpret_cast<const double2 *>(a + o); };
+		// rows by (dy, dz); x pairs at X-2 (.y = X-1), X (.x = X, .y = X+1), X+2 (.x)
+		const long r00 = wy(Y) + wz(Z);
+		const double2 c_m = pr(phi, r00 + xm2), c_0 = pr(phi, r00 + X), c_p = pr(phi, r00 + xp2);
+		const long ryp = wy(Y + 1) + wz(Z), rym = wy(Y - 1) + wz(Z);
+		const long rzp = wy(Y) + wz(Z + 1), rzm = wy(Y) + wz(Z - 1);
+		const double2 yp_m = pr(phi, ryp + xm2), yp_0 = pr(phi, ryp + X);
+		const double2 ym_m = pr(phi, rym + xm2), ym_0 = pr(phi, rym + X);
+		const double2 zp_m = pr(phi, rzp + xm2), zp_0 = pr(phi, rzp + X);
+		const double2 zm_m = pr(phi, rzm + xm2), zm_0 = pr(phi, rzm + X);
+		const double y2p = pr(phi, wy(Y + 2) + wz(Z) + X).x, y2m = pr(phi, wy(Y - 2) + wz(Z) + X).x;
+		const double z2p = pr(phi, wy(Y) + wz(Z + 2) + X).x, z2m = pr(phi, wy(Y) + wz(Z - 2) + X).x;
+		const double ypzp = pr(phi, wy(Y + 1) + wz(Z + 1) + X).x, ypzm = pr(phi, wy(Y + 1) + wz(Z - 1) + X).x;
+		const double ymzp = pr(phi, wy(Y - 1) + wz(Z + 1) + X).x, ymzm = pr(phi, wy(Y - 1) + wz(Z - 1) + X).x;
+		const double2 q_m = pr(rho, r00 + xm2), q_0 = pr(rho, r00 + X);
+		const double q_yp = pr(rho, ryp + X).x, q_ym = pr(rho, rym + X).x;
+		const double q_zp = pr(rho, rzp + X).x, q_zm = pr(rho, rzm + X).x;
+		// residual_at<3>: -6 phi + (x+ + x- + y+ + y- + z+ + z-) + rho
+		auto res = [](double c, double xp, double xm, double yp, double ym, double zp, double zm, double q) {
+			double v = -6. * c;
+			v += xp + xm + yp + ym + zp + zm;
+			return v + q;
+		};
+		const double f0 = res(c_0.x, c_0.y, c_m.y, yp_0.x, ym_0.x, zp_0.x, zm_0.x, q_0.x);
+		const double xp = res(c_0.y, c_p.x, c_0.x, yp_0.y, ym_0.y, zp_0.y, zm_0.y, q_0.y);
+		const double xm = res(c_m.y, c_0.x, c_m.x, yp_m.y, ym_m.y, zp_m.y, zm_m.y, q_m.y);
+		const double yp = res(yp_0.x, yp_0.y, yp_m.y, y2p, c_0.x, ypzp, ypzm, q_yp);
+		const double ym = res(ym_0.x, ym_0.y, ym_m.y, c_0.x, y2m, ymzp, ymzm, q_ym);
+		const double zp = res(zp_0.x, zp_0.y, zp_m.y, ypzp, ymzp, z2p, c_0.x, q_zp);
+		const double zm = res(zm_0.x, zm_0.y, zm_m.y, ypzm, ymzm, c_0.x, z2m, q_zm);
+		double v;
+		if (HW3D) {
+			v = (1. / 12.) * (6 * f0 + xp + xm + yp + ym + zp + zm);
+		} else {
+			v = (2. * 3) * f0;
+			v += xp + xm;
+			v += yp + ym;
+			v += zp + zm;
+			v *= 1. / (3 * 4);
+		}
+		coarse[gc] = v * scale;
+	}
+}
+
 // phi_f += P(phi_c) (mgBilinProl3D + gAddTo): one thread per coarse cell
 // writes its 2 x 2 x 2 fine points (x pairs as 16-byte accesses) from the 8
 // coarse corner values, each point with prol_low's nesting (x outermost, z
@@ -1519,7 +1587,14 @@ extern "C" int pinc_hip_resid_restrict(const double *phi, const double *rho, dou
 	if (8 * npts(Lc) >= (1L << 31)) return set_error(hipErrorInvalidValue, "resid_restrict: level too large");
 	hipStream_t st = (hipStream_t)stream;
 	const unsigned nb = blocks_for(npts(Lc));
-	if (hw3d) hipLaunchKernelGGL(k_resid_restrict3<true>, dim3(nb), dim3(kThreads), 0, st, phi, rho, coarse, Lc, scale);
+	const bool pairs = PINC_MG_RR_PAIRS &&
+	                   !((reinterpret_cast<unsigned long>(phi) | reinterpret_cast<unsigned long>(rho)) & 15);
+	if (pairs && hw3d)
+		hipLaunchKernelGGL(k_resid_restrict3p<true>, dim3(nb), dim3(kThreads), 0, st, phi, rho, coarse, Lc, scale);
+	else if (pairs)
+		hipLaunchKernelGGL(k_resid_restrict3p<false>, dim3(nb), dim3(kThreads), 0, st, phi, rho, coarse, Lc, scale);
+	else if (hw3d)
+		hipLaunchKernelGGL(k_resid_restrict3<true>, dim3(nb), dim3(kThreads), 0, st, phi, rho, coarse, Lc, scale);
 	else hipLaunchKernelGGL(k_resid_restrict3<false>, dim3(nb), dim3(kThreads), 0, st, phi, rho, coarse, Lc, scale);
 	return check_launch("resid_restrict");
 }

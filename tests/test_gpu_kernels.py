@@ -155,3 +155,49 @@ def test_cell_sort(hip, n, T, start):
     a = np.concatenate([P, V], 1)
     b = np.concatenate([P0, V0], 1)
     np.testing.assert_array_equal(a[np.lexsort(a.T[::-1])], b[np.lexsort(b.T[::-1])])
+
+
+@pytest.mark.parametrize("hw3d", [1, 0])
+@pytest.mark.parametrize("shape", [(4, 4, 4), (32, 8, 16), (64, 32, 96), (96, 24, 32)])
+def test_resid_restrict_equals_residual_then_restrict(hip, shape, hw3d):
+    """pinc_hip_resid_restrict (k_resid_restrict3p: x pairs, the residual
+    never stored) is bit for bit the residual (mgResidual), then the
+    restriction (mgHalfRestrict3D or the ND form), then the native x4; and
+    the residual norm (k_residual_sumsq3p) matches numpy's to rounding."""
+    import torch
+    vp = C.c_void_p
+    hip.pinc_hip_resid_restrict.argtypes = [vp, vp, vp, Lvl, C.c_int, C.c_double, vp]
+    hip.pinc_hip_residual.argtypes = [vp, vp, vp, Lvl, vp]
+    hip.pinc_hip_restrict.argtypes = [vp, vp, Lvl, C.c_int, vp]
+    hip.pinc_hip_scale.argtypes = [vp, C.c_long, C.c_double, vp]
+    hip.pinc_hip_residual_sumsq.argtypes = [vp, vp, Lvl, vp, C.POINTER(C.c_int), vp]
+    hip.pinc_hip_reduce.argtypes = [vp, C.c_int, C.c_double, vp, vp]
+    tx, ty, tz = shape
+    n = tx * ty * tz
+    g = torch.Generator(device="cpu").manual_seed(5)
+    phi = torch.randn(n, dtype=torch.float64, generator=g).cuda()
+    rho = torch.randn(n, dtype=torch.float64, generator=g).cuda()
+    Lf = Lvl(3, (C.c_int * 3)(tx, ty, tz))
+    Lc = Lvl(3, (C.c_int * 3)(tx // 2, ty // 2, tz // 2))
+    nc = n // 8
+    out = torch.full((nc,), float("nan"), dtype=torch.float64, device="cuda")
+    res = torch.empty_like(phi)
+    ref = torch.empty_like(out)
+    assert hip.pinc_hip_resid_restrict(phi.data_ptr(), rho.data_ptr(), out.data_ptr(), Lc, hw3d, 4.0, None) == 0
+    assert hip.pinc_hip_residual(res.data_ptr(), phi.data_ptr(), rho.data_ptr(), Lf, None) == 0
+    assert hip.pinc_hip_restrict(res.data_ptr(), ref.data_ptr(), Lc, hw3d, None) == 0
+    assert hip.pinc_hip_scale(ref.data_ptr(), nc, 4.0, None) == 0
+    part = torch.empty(65536, dtype=torch.float64, device="cuda")
+    tot = torch.empty(1, dtype=torch.float64, device="cuda")
+    nb = C.c_int()
+    assert hip.pinc_hip_residual_sumsq(phi.data_ptr(), rho.data_ptr(), Lf, part.data_ptr(), C.byref(nb), None) == 0
+    assert hip.pinc_hip_reduce(part.data_ptr(), nb.value, 1.0, tot.data_ptr(), None) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    a = phi.cpu().numpy().reshape(tz, ty, tx)
+    r = rho.cpu().numpy().reshape(tz, ty, tx)
+    s = (np.roll(a, -1, 2) + np.roll(a, 1, 2)) + np.roll(a, -1, 1)
+    s = ((s + np.roll(a, 1, 1)) + np.roll(a, -1, 0)) + np.roll(a, 1, 0)
+    resn = (-6.0 * a + s) + r
+    np.testing.assert_array_equal(res.cpu().numpy().reshape(tz, ty, tx), resn)
+    np.testing.assert_allclose(tot.item(), float((resn * resn).sum()), rtol=1e-12)
