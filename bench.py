@@ -507,7 +507,10 @@ def main() -> int:
                       "bytes_per_launch": p["mean_bytes"], "achieved_GBs": gbs, "frac": gbs / HBM_PEAK_GBS,
                       "launches": p["launches"], "samples": p["samples"],
                       "est_ms_per_step": p["mean_ms"] * p["launches"] / args.steps}
-    dom = max(kernels, key=lambda k: kernels[k]["est_ms_per_step"])
+    # the dominant kernel with algorithmic bytes (a replayed V-cycle graph,
+    # "mg_cycle", is timed as a whole and has none: no roofline of its own)
+    real = [k for k in kernels if kernels[k]["bytes_per_launch"] > 0] or list(kernels)
+    dom = max(real, key=lambda k: kernels[k]["est_ms_per_step"])
     dk = kernels[dom]
     if "push_plain" in sub:
         for k in ("push_count", "push_sort"):

@@ -158,6 +158,9 @@ typedef struct {
 	                             of the nodes with an id: only cells there are looked up */
 	unsigned long long *emigTotal; /* if set: += the particles flagged to leave (every flag but the
 	                                  centre: emigrants, collected, outside the frame) */
+	int flagsSparse;  /* 1: write only the flags that are not the centre (every other flag of the
+	                     species' range must already be the centre: pinc_hip_extract puts the
+	                     extracted particles' flags back to it); 0: write every live particle's flag */
 } pinc_push_t;
 int pinc_hip_push(pinc_pop_t pop, int s, pinc_geom_t g, const pinc_push_t *args, int *nBlocks, void *stream);
 /* number of sort keys (cells incl. the wrap layer) of the tiled layout */
@@ -224,7 +227,9 @@ typedef struct {
  * has PINC_NE_CODES entries */
 #define PINC_NE_SINK 27
 #define PINC_NE_CODES 28
-int pinc_hip_extract(pinc_pop_t pop, int s, const unsigned char *flags, int *chunkCount,
+/* The flags of the extracted particles are set back to the centre, so that a
+ * species' flags are all the centre again after its extraction. */
+int pinc_hip_extract(pinc_pop_t pop, int s, unsigned char *flags, int *chunkCount,
                      int center, int nNeighbors, pinc_extract_ws_t ws, long *nEmig,
                      long *neCount, void *stream);
 
@@ -380,7 +385,11 @@ int pinc_hip_mg_coarse(const double *rho, double *phi, int nLevels, const pinc_l
  *                        times 4 (coarse h^2 factor)
  *   prolong_add_slab     every slab plane += the global level-1 correction
  *                        (Lc global); slab plane zl is global plane z0 + zl
- *                        (mod Tz) */
+ *                        (mod Tz)
+ *   prolong_add_own      the owned planes [hz, hz + nloc) += the correction
+ *                        of this rank's own level-1 planes, held in phiCx
+ *                        with one halo plane on each side (Lcx: T0/2 x T1/2
+ *                        x (nloc/2 + 2)); level 1 decomposed as level 0 */
 int pinc_hip_residual_slab(double *res, const double *phi, const double *rho, pinc_lvl_t Lx, int zlo, int zhi,
                            void *stream);
 int pinc_hip_residual_sumsq_slab(const double *phi, const double *rho, pinc_lvl_t Lx, int zlo, int zhi,
@@ -389,6 +398,8 @@ int pinc_hip_restrict_slab(const double *fineX, pinc_lvl_t Lx, int zf0, double *
                            void *stream);
 int pinc_hip_prolong_add_slab(double *phiX, pinc_lvl_t Lx, int z0, int Tz, const double *phiC, pinc_lvl_t Lc,
                               void *stream);
+int pinc_hip_prolong_add_own(double *phiX, pinc_lvl_t Lx, int hz, int nloc, const double *phiCx, pinc_lvl_t Lcx,
+                             void *stream);
 int pinc_hip_gs_materialize(double *phi, pinc_lvl_t L, int lastPass, const double *muA,
                             const double *muB, void *stream);
 /* phi -= *mu over all points */

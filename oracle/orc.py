@@ -41,6 +41,7 @@ def _load() -> C.CDLL:
         "orc_pop_set": (None, [vp, C.c_int, C.c_int, C.c_long, vp, vp, vp]),
         "orc_mpi_emigrants": (None, [vp, C.c_int, vp]),
         "orc_mpi_thresholds": (None, [vp, C.c_int, vp]),
+        "orc_mpi_emigrant_buffer": (C.c_long, [vp, C.c_int, C.c_int, vp]),
         "orc_mpi_alloc": (None, [vp, C.c_int, vp]),
         "orc_kat_acc": (None, [C.c_int, vp, C.c_int, vp, C.c_long, vp, vp, C.c_double, C.c_double, C.c_int, vp]),
         "orc_kat_distr": (None, [C.c_int, vp, C.c_int, vp, C.c_long, vp, C.c_double, C.c_int]),
@@ -48,6 +49,7 @@ def _load() -> C.CDLL:
         "orc_kat_rank_to_neighbor": (C.c_int, [vp, vp, C.c_int]),
         "orc_kat_reciprocal": (C.c_int, [C.c_int, C.c_int]),
         "orc_kat_neighborhood": (None, [C.c_char_p, vp, vp]),
+        "orc_kat_extract": (None, [C.c_char_p, C.c_int, vp, vp, vp, vp, C.c_int, vp, vp, C.c_long, vp]),
         "orc_world_ndims": (C.c_int, [vp]),
         "orc_world_mg_limit": (None, [vp, C.c_long, C.c_long]),
         "orc_world_mg_history": (C.c_long, [vp, vp, C.c_long]),
@@ -179,6 +181,14 @@ class World:
         out = np.zeros(n, dtype=np.int64)
         LIB.orc_mpi_emigrants(self._h, rank, out.ctypes.data)
         return out.reshape(3 ** self.ndims, self.nspecies)
+
+    def emigrant_records(self, ne: int, rank: int = 0) -> np.ndarray:
+        """emigrants[ne] of the last extraction: one row (pos, vel) per record."""
+        n = LIB.orc_mpi_emigrant_buffer(self._h, rank, ne, None)
+        out = np.zeros((n, 2 * self.ndims))
+        if n:
+            LIB.orc_mpi_emigrant_buffer(self._h, rank, ne, out.ctypes.data)
+        return out
 
     @property
     def ndims(self) -> int:

@@ -581,6 +581,16 @@ void orc_mpi_emigrants(OWorld *w, int r, long *nEmigrants){
 	OMpi *m = &w->r[r].mpi;
 	memcpy(nEmigrants, m->nEmigrants, m->nNeighbors*w->nSpecies*sizeof(long));
 }
+/* emigrants[ne] of the last extraction (pusher.c:827-833 layout: pos then
+ * vel, nDims each, species after species): the number of records */
+long orc_mpi_emigrant_buffer(OWorld *w, int r, int ne, double *out){
+	OMpi *m = &w->r[r].mpi;
+	if(ne < 0 || ne >= m->nNeighbors || ne == m->center) return 0;
+	long cnt = 0;
+	for(int s = 0; s < w->nSpecies; s++) cnt += m->nEmigrants[ne*w->nSpecies + s];
+	if(out) memcpy(out, m->emigrants[ne], 2*w->nDims*cnt*sizeof(double));
+	return cnt;
+}
 void orc_mpi_thresholds(OWorld *w, int r, double *thr){
 	memcpy(thr, w->r[r].mpi.thresholds, 2*w->nDims*sizeof(double));
 }
@@ -667,6 +677,45 @@ void orc_kat_neighborhood(const char *iniText, double *thr, long *alloc){
 	om_create_neighborhood(&m, ini, &g);
 	memcpy(thr, m.thresholds, 2*m.nDims*sizeof(double));
 	memcpy(alloc, m.nEmigrantsAlloc, m.nNeighbors*sizeof(long));
+	og_free(&g);
+	oini_free(ini);
+}
+
+/* testExtractEmigrantsXD (test/pusher.test.c:360-545): the neighbourhood of
+ * the ini text (gCreateNeighborhood, thresholds by the current rule), then
+ * opu_extract3d (use3d) or opu_extractnd on the given AoS particles; no
+ * operator selection (the test selects none, so puSanity's threshold bound
+ * does not apply).  pos/vel/iStop are updated in place; nEmigrants gets the
+ * nNeighbors*nSpecies counts, bufs the nNeighbors buffers of cap records
+ * (2*nDims doubles each), thr the thresholds. */
+void orc_kat_extract(const char *iniText, int nSpecies, const long *iStart, long *iStop, double *pos, double *vel,
+                     int use3d, long *nEmigrants, double *bufs, long cap, double *thr){
+	OIni *ini = oini_from_string(iniText);
+	OGrid g;
+	og_alloc(&g, ini, 1);
+	OMpi m; memset(&m, 0, sizeof(m));
+	m.nDims = oini_int(ini, "grid:nDims");
+	m.nSpecies = nSpecies;
+	om_create_neighborhood(&m, ini, &g);
+	const int nd = m.nDims;
+	OPop p; memset(&p, 0, sizeof(p));
+	p.nDims = nd; p.nSpecies = nSpecies;
+	p.iStart = (long*)iStart; p.iStop = iStop; p.pos = pos; p.vel = vel;
+	p.id = calloc(iStart[nSpecies], sizeof(long));
+	if(use3d) opu_extract3d(&p, &m); else opu_extractnd(&p, &m);
+	memcpy(nEmigrants, m.nEmigrants, m.nNeighbors*nSpecies*sizeof(long));
+	memcpy(thr, m.thresholds, 2*nd*sizeof(double));
+	for(int ne = 0; ne < m.nNeighbors; ne++){
+		if(ne == m.center) continue;
+		long cnt = 0;
+		for(int s = 0; s < nSpecies; s++) cnt += m.nEmigrants[ne*nSpecies + s];
+		if(cnt > cap) orc_die("orc_kat_extract: %ld records for direction %d, cap %ld", cnt, ne, cap);
+		memcpy(bufs + (long)ne*cap*2*nd, m.emigrants[ne], cnt*2*nd*sizeof(double));
+		free(m.emigrants[ne]);
+		free(m.emigrantIds[ne]);
+	}
+	free(m.emigrants); free(m.emigrantIds); free(m.nEmigrants); free(m.nImmigrants); free(m.nEmigrantsAlloc);
+	free(p.id);
 	og_free(&g);
 	oini_free(ini);
 }

@@ -1419,6 +1419,31 @@ __global__ void k_prolong_add_slab(double *__restrict__ phiX, pinc_lvl_t Lxp, in
 	}
 }
 
+// the owned planes [hz, hz + nz) of the extended slab += prolongated
+// correction of this rank's own level-1 planes (phiCx: those planes with one
+// halo plane on each side).  The owned slab starts at an even global plane,
+// so fine plane hz + k sits at plane k + 2 of the frame whose coarse plane 0
+// is phiCx's lower halo plane: the same parities, the same prol_low
+// expression, and every coarse plane it reads lies in phiCx (k + 2 in
+// [2, nz + 2) reads coarse planes 1 .. nz/2 + 1).
+__global__ void k_prolong_add_own(double *__restrict__ phiX, pinc_lvl_t Lxp, int hz, int nz,
+                                  const double *__restrict__ phiCx, pinc_lvl_t Lcp) {
+	Lv X = make_lv(Lxp), C = make_lv(Lcp);
+	const long n = (long)X.T[0] * X.T[1] * nz;
+	const Walk w = point_walk(n);
+	for (long q = w.g0; q < w.g1; q += w.step) {
+		int cf[3];
+		{  // 32-bit index arithmetic (levels hold < 2^31 points, checked on the host)
+			const unsigned u = (unsigned)q, t0 = (unsigned)X.T[0], t1 = (unsigned)X.T[1];
+			const unsigned r = u / t0;
+			cf[0] = (int)(u - r * t0);
+			cf[1] = (int)(r % t1);
+			cf[2] = (int)(r / t1) + 2;
+		}
+		phiX[(long)hz * X.s[2] + q] += prol_low<3, 0>(phiCx, C, cf);
+	}
+}
+
 // ------------------------------------------ level-0 transfers, 3-D (round 4)
 // The three point stencils around the coarse correction, restructured so
 // that each thread does the work of a whole coarse cell and no point index is
@@ -1803,6 +1828,19 @@ extern "C" int pinc_hip_restrict_slab(const double *fineX, pinc_lvl_t Lx, int zf
 	if (nd3) hipLaunchKernelGGL(k_restrict_slab<true>, dim3(nb), dim3(kThreads), 0, st, fineX, Lx, zf0, coarse, Lc);
 	else hipLaunchKernelGGL(k_restrict_slab<false>, dim3(nb), dim3(kThreads), 0, st, fineX, Lx, zf0, coarse, Lc);
 	return check_launch("restrict_slab");
+}
+
+extern "C" int pinc_hip_prolong_add_own(double *phiX, pinc_lvl_t Lx, int hz, int nloc, const double *phiCx,
+                                        pinc_lvl_t Lcx, void *stream) {
+	if (Lx.nd != 3 || Lcx.nd != 3 || 2 * Lcx.T[0] != Lx.T[0] || 2 * Lcx.T[1] != Lx.T[1] || nloc % 2 ||
+	    2 * (Lcx.T[2] - 2) != nloc || hz < 0 || hz + nloc > Lx.T[2])
+		return set_error(hipErrorInvalidValue, "prolong_add_own: geometry");
+	if ((long)Lx.T[0] * Lx.T[1] * nloc >= (1L << 31))
+		return set_error(hipErrorInvalidValue, "prolong_add_own: slab too large for 32-bit indexing");
+	const long n = (long)Lx.T[0] * Lx.T[1] * nloc;
+	hipLaunchKernelGGL(k_prolong_add_own, dim3(blocks_for(n)), dim3(kThreads), 0, (hipStream_t)stream, phiX, Lx, hz,
+	                   nloc, phiCx, Lcx);
+	return check_launch("prolong_add_own");
 }
 
 extern "C" int pinc_hip_prolong_add_slab(double *phiX, pinc_lvl_t Lx, int z0, int Tz, const double *phiC,

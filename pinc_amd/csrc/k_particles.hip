@@ -232,9 +232,9 @@ __global__ __launch_bounds__(kMaxNe * 32) void k_hist_scan(int *__restrict__ blo
 
 // stable scatter of emigrants into the direction-ordered buffer
 __global__ __launch_bounds__(kThreads) void k_rank_scatter(
-		const unsigned char *__restrict__ flags, const int *__restrict__ order, long E,
+		unsigned char *__restrict__ flags, const int *__restrict__ order, long E,
 		const int *__restrict__ blockHist, const int *__restrict__ scratch, pinc_pop_t pop,
-		long sbase, double *__restrict__ buf, long cap, unsigned char *__restrict__ bufNe) {
+		long sbase, double *__restrict__ buf, long cap, unsigned char *__restrict__ bufNe, int center) {
 	__shared__ int waveCnt[kThreads / 64][kMaxNe];
 	__shared__ int running[kMaxNe];
 	int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -268,6 +268,8 @@ __global__ __launch_bounds__(kThreads) void k_rank_scatter(
 				buf[(3 + d) * cap + dst] = pop.v[d][src];
 			}
 			bufNe[dst] = (unsigned char)ne;
+			flags[j] = (unsigned char)center;  // (read above by this thread only: the species' flags are
+			                                   // all the centre again after the extraction)
 		}
 		__syncthreads();
 		if (threadIdx.x < kMaxNe) {
@@ -1400,6 +1402,7 @@ struct PushArgs {
 	int *objCount;
 	int objLo[3], objExt[3];     // bounding box of the object nodes: lower corner, extent - 1
 	unsigned long long *emigTotal;  // += particles flagged to leave (nullable)
+	int flagsSparse;                // only the non-centre flags are written
 };
 // phase timestamp of the block (thread 0, s_memrealtime at 100 MHz)
 #define PUSH_TS(slot) \
@@ -2466,7 +2469,10 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 		if (SORT) {
 			stageF[k * kPushThreads + threadIdx.x] = (unsigned char)ne;  // by item
 		}
-		if (!SORT) a.flags[i] = (unsigned char)ne;
+		// (sparse: the species' flags are the centre already -- the last
+		// extraction put them back -- so only the leavers' are written, 1 B
+		// per particle less at one rank, where every dimension wraps in place)
+		if (!SORT && (!a.flagsSparse || ne != a.center)) a.flags[i] = (unsigned char)ne;
 		if (ne != a.center) {
 			cnt++;
 		} else {
@@ -2501,7 +2507,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 				a.vo[d][o] = vv[k][d];
 			}
 			const int f = stageF[k * kPushThreads + threadIdx.x];
-			a.flags[o] = (unsigned char)f;
+			if (!a.flagsSparse || f != a.center) a.flags[o] = (unsigned char)f;
 			if (f != a.center) atomicAdd(&a.chunkCount[o / PINC_CHUNK], 1);
 		}
 	}
@@ -2959,7 +2965,7 @@ static int *pinned_ints() {
 	return p;
 }
 
-extern "C" int pinc_hip_extract(pinc_pop_t pop, int s, const unsigned char *flags, int *chunkCount,
+extern "C" int pinc_hip_extract(pinc_pop_t pop, int s, unsigned char *flags, int *chunkCount,
                                 int center, int nNeighbors, pinc_extract_ws_t ws, long *nEmig,
                                 long *neCount, void *stream) {
 	(void)nNeighbors;
@@ -3001,7 +3007,7 @@ extern "C" int pinc_hip_extract(pinc_pop_t pop, int s, const unsigned char *flag
 	hipLaunchKernelGGL(k_hist_scan, dim3(1), dim3(kMaxNe * 32), 0, st, ws.blockHist, nb,
 	                   ws.scratch);
 	hipLaunchKernelGGL(k_rank_scatter, dim3(nb), dim3(kThreads), 0, st, flags + sb, ws.order,
-	                   (long)E, ws.blockHist, ws.scratch, pop, sb, ws.buf, ws.cap, ws.bufNe);
+	                   (long)E, ws.blockHist, ws.scratch, pop, sb, ws.buf, ws.cap, ws.bufNe, center);
 	hipLaunchKernelGGL(k_fill_holes, dim3((unsigned)ceil_div(E, 256)), dim3(256), 0, st, pop, sb,
 	                   ws.tail, ws.holes, ws.scratch);
 	static_assert(kMaxNe <= 64, "pinned words");
@@ -3300,6 +3306,7 @@ extern "C" int pinc_hip_push(pinc_pop_t pop, int s, pinc_geom_t g, const pinc_pu
 	a.tstamp = args->tstamp;
 	a.diag = args->diag;
 	a.emigTotal = args->emigTotal;
+	a.flagsSparse = args->flagsSparse;
 	a.objIn = args->objInside;
 	a.objSy = args->objSy;
 	a.objSz = args->objSz;

@@ -494,6 +494,7 @@ void pinc_ctx_init(void) {
 	g_pinc.verbose = getenv("PINC_VERBOSE") ? atoi(getenv("PINC_VERBOSE")) : 0;
 	g_pinc.traceSort = getenv("PINC_TRACE_SORT") ? atoi(getenv("PINC_TRACE_SORT")) : 0;
 	g_pinc.extractSkip = !(getenv("PINC_EXTRACT_SKIP") && !atoi(getenv("PINC_EXTRACT_SKIP")));
+	g_pinc.flagsSparse = !(getenv("PINC_FLAGS_SPARSE") && !atoi(getenv("PINC_FLAGS_SPARSE")));
 	for (int p = 0; p < PINC_NPHASES; p++)
 		for (int i = 0; i < 2 * PINC_PHASE_RING; i++) pinc_check(pinc_hip_event_create(&g_pinc.ev[p][i]), "event");
 	g_pinc.initialised = 1;
@@ -569,6 +570,13 @@ int pinc_probe_start(int kernel, int maxSamples) {
 			pinc_check(pinc_hip_event_create(&g_pinc.probeEv[k][i]), "probe event");
 	}
 	return 0;
+}
+
+/* a launch of probe k that is not timed (sampling every launch would put an
+ * event record, ~5 us of host time, between back-to-back kernels): counted
+ * so that launches x mean time is the kernel's whole cost */
+void pinc_probe_count(int k) {
+	if (g_pinc.probeOn[k] && !g_pinc.capturing) g_pinc.probeLaunches[k]++;
 }
 
 int pinc_probe_begin(int k) {

@@ -36,6 +36,7 @@ typedef struct {
 	 * word was last read: an unchanged word is not read again */
 	unsigned long errSerial, errRead;
 	int extractSkip; /* PINC_EXTRACT_SKIP=0 turns off skipping extractions the push counted empty */
+	int flagsSparse; /* PINC_FLAGS_SPARSE=0: every push writes every particle's flag (pinc_pusher.c) */
 	int verbose;        /* PINC_VERBOSE=n: progress every n V-cycles */
 	int timing;
 	/* phase timers: event pairs per phase, read when the ring is full or
@@ -56,6 +57,7 @@ typedef struct {
 
 /* probe hooks around a launch of kernel k with algorithmic byte count b */
 int pinc_probe_begin(int k);
+void pinc_probe_count(int k);
 void pinc_phase_flush(void);
 void pinc_probe_end(int k, int slot, double bytes);
 void pinc_probe_tag(int k, int slot, int tag);
@@ -72,6 +74,12 @@ struct PincDevPop {
 	int *chunkCount;              /* per species at chunkBase[s] */
 	long chunkBase[PINC_MAX_SPECIES + 1];
 	int flagsValid;
+	/* what the flag bytes of species s's whole range hold (pinc_pusher.c,
+	 * flags_before_write): PINC_FLAGS_CLEAN all the centre, so a push may
+	 * write only its leavers' flags; PINC_FLAGS_PENDING the centre except at
+	 * the particles the last write flagged, all below flagN[s]; else unknown */
+	int flagState[PINC_MAX_SPECIES];
+	long flagN[PINC_MAX_SPECIES];
 	pinc_extract_ws_t ws[PINC_MAX_SPECIES];
 	long nEmig[PINC_MAX_SPECIES];
 	long neCount[PINC_MAX_SPECIES][PINC_NE_CODES]; /* directions + the object sink */
@@ -198,8 +206,14 @@ struct PincDevGrid {
 	unsigned long long gen, serial;
 	PincDevGrid *liveNext;
 };
+enum { PINC_FLAGS_UNKNOWN = 0, PINC_FLAGS_CLEAN = 1, PINC_FLAGS_PENDING = 2 };
+int pinc_flags_before_write(Population *pop, int s, int sparseOk);
+void pinc_flags_after_extract(Population *pop, int s, long nBefore);
 /* d is about to be rewritten: a pending sorting push that kicked with this
- * grid first materialises its kicked velocities (pinc_pusher.c) */
+ * grid first materialises its kicked velocities (pinc_pusher.c).  EVERY
+ * operator that writes a grid's device data must call this first (gMul,
+ * gFinDiff1st, gHaloOp, gSyncToDevice, gFree do): gen only moves here, so
+ * the re-kick's guard cannot see a write that skips it. */
 void pinc_grid_touch(Grid *g);
 /* populations whose pending sorting push may need its E (pinc_pusher.c) */
 void pinc_pending_register(Population *pop);
@@ -275,6 +289,16 @@ struct MultigridSolver {
 	int z0;                        /* global plane of extended plane 0 */
 	double *rho1Slab;              /* this rank's level-1 planes before the all-gather */
 	pinc_lvl_t L1s;
+	/* sharded level 0 with multigrid:spectralCoarse: level 1 stays
+	 * decomposed (dist1), as the reference keeps every level on its
+	 * subdomain (mgAllocSubGrids, multigrid.c:128): the correction of this
+	 * rank's level-1 planes comes from the slab-distributed transform
+	 * (fftCoarseSlab; all-to-all transposes instead of an all-gather of
+	 * level 1) into phi1Ext, which holds one halo plane on each side for the
+	 * prolongation of the owned level-0 planes */
+	int dist1;
+	pinc_fft_slab_t *fftCoarseSlab;
+	double *phi1Ext;
 	/* the per-cycle norm read without idling the GPU (mgSolve): the norm
 	 * goes to pinned memory asynchronously and, while the host waits for
 	 * it, the next cycle's first double sweep (phi -> res, which leaves phi

@@ -232,8 +232,26 @@ MultigridSolver *mgAllocSolver(const dictionary *ini, Grid *rho, Grid *phi) {
 	if (S->speculate) pinc_check(pinc_hip_event_create(&S->normEvent), "mg norm");
 	if (S->native && S->nLevels >= 2 && iniHas(ini, "multigrid:spectralCoarse") &&
 	    iniGetInt(ini, "multigrid:spectralCoarse")) {
-		pinc_check(pinc_hip_fft_create(&S->fftCoarse, S->L[1].nd, S->L[1].T, g_pinc.stream), "mg spectral coarse");
-		pinc_check(pinc_hip_fft_set_symbol(S->fftCoarse, 1), "mg spectral coarse");
+		/* sharded level 0: level 1 stays decomposed when its slabs can be
+		 * transposed (y divisible by the rank count), as the reference keeps
+		 * every level on its subdomain (multigrid.c:128-180); PINC_MG_DIST1=0
+		 * all-gathers it instead (the round-5 form) */
+		const int n1 = S->shard ? S->nloc0 / 2 : 0;
+		if (S->shard && n1 >= 1 && S->L[1].T[1] % g_pinc.nranks == 0 && S->L[1].T[2] == n1 * g_pinc.nranks &&
+		    !(getenv("PINC_MG_DIST1") && !atoi(getenv("PINC_MG_DIST1")))) {
+			S->dist1 = 1;
+			pinc_check(pinc_hip_fft_slab_create(&S->fftCoarseSlab, S->L[1].T, n1, g_pinc.nranks, g_pinc.rank,
+			                                    g_pinc.stream),
+			           "mg spectral coarse (slabs)");
+			pinc_check(pinc_hip_fft_slab_set_symbol(S->fftCoarseSlab, 1), "mg spectral coarse (slabs)");
+			const long ps1 = (long)S->L[1].T[0] * S->L[1].T[1];
+			pinc_check(pinc_hip_malloc((void **)&S->phi1Ext, ps1 * (n1 + 2) * sizeof(double)), "mg level 1 slab");
+			pinc_check(pinc_hip_memset(S->phi1Ext, 0, ps1 * (n1 + 2) * sizeof(double), g_pinc.stream),
+			           "mg level 1 slab");
+		} else {
+			pinc_check(pinc_hip_fft_create(&S->fftCoarse, S->L[1].nd, S->L[1].T, g_pinc.stream), "mg spectral coarse");
+			pinc_check(pinc_hip_fft_set_symbol(S->fftCoarse, 1), "mg spectral coarse");
+		}
 	}
 	if (S->secondSpectral == 1) {
 		pinc_check(pinc_hip_malloc((void **)&S->rhoSave, S->N[0] * sizeof(double)), "mg second guess");
@@ -270,6 +288,8 @@ void mgFreeSolver(MultigridSolver *S) {
 	pinc_hip_fft_destroy(S->fft);
 	pinc_hip_fft_slab_destroy(S->fftSlab);
 	pinc_hip_fft_destroy(S->fftCoarse);
+	pinc_hip_fft_slab_destroy(S->fftCoarseSlab);
+	pinc_hip_free(S->phi1Ext);
 	pinc_hip_host_free(S->hostNorm);
 	if (S->normEvent) pinc_hip_event_destroy(S->normEvent);
 	free(S->hist);
@@ -394,7 +414,16 @@ static void neutralize_level(MultigridSolver *S, int q, double *a) {
 
 /* phi[qf] += prolongated phi[qf + 1] */
 static void prolong_into(MultigridSolver *S, int qf) {
-	if (qf == 0 && S->shard)
+	if (qf == 0 && S->dist1) {
+		/* the owned planes only, from this rank's level-1 planes and one halo
+		 * plane each side; the halo planes of level 0 come from the
+		 * neighbours' owned planes at the refresh before the post-smoothing */
+		pinc_lvl_t Lcx = S->L[1];
+		Lcx.T[2] = S->nloc0 / 2 + 2;
+		pinc_check(pinc_hip_prolong_add_own(S->phi[0], S->L[0], S->hz, S->nloc0, S->phi1Ext, Lcx, g_pinc.stream),
+		           "prolong own planes");
+		if (S->nPost <= 0) shard_halo(S, S->phi[0]);
+	} else if (qf == 0 && S->shard)
 		pinc_check(pinc_hip_prolong_add_slab(S->phi[0], S->L[0], S->z0, S->L[1].T[2] * 2, S->phi[1], S->L[1],
 		                                     g_pinc.stream),
 		           "prolong slab");
@@ -414,6 +443,7 @@ static void restrict_residual(MultigridSolver *S, int q) {
 		pinc_check(pinc_hip_restrict_slab(S->res[0], S->L[0], h, S->rho1Slab, S->L1s, S->restr3d, g_pinc.stream),
 		           "restrict slab");
 		long n1 = (long)S->L1s.T[0] * S->L1s.T[1] * S->L1s.T[2];
+		if (S->dist1) return; /* level 1 stays in its slabs (vrec) */
 		if (g_pinc.nranks > 1) pinc_comm_allgather(S->rho1Slab, S->rho[1], n1, "gather level 1");
 		else pinc_check(pinc_hip_d2d(S->rho[1], S->rho1Slab, n1 * sizeof(double), g_pinc.stream), "level 1");
 		return;
@@ -447,7 +477,11 @@ static void smooth_native(MultigridSolver *S, int q, int nIter, int nd3) {
 	int k = 0;
 	/* two iterations per launch (pinc_hip_gs_sweep2x) in pairs, so that the
 	 * ping-pong ends in phi */
-	int fused2 = fused && L.T[0] % 32 == 0 && L.T[1] % 8 == 0;
+	/* (its x-pair fetches need 16-B aligned arrays: otherwise the single
+	 * sweeps, as the residual norm and the restriction fall back to their
+	 * scalar kernels -- every x-pair kernel falls back, none fails) */
+	int fused2 = fused && L.T[0] % 32 == 0 && L.T[1] % 8 == 0 &&
+	             !(((uintptr_t)S->phi[q] | (uintptr_t)S->res[q] | (uintptr_t)S->rho[q]) & 15);
 	if (q == 0 && S->preDone) {
 		/* the first double sweep ran while the host read the last cycle's
 		 * norm (mgSolve), and its ping-pong swap is applied */
@@ -462,6 +496,7 @@ static void smooth_native(MultigridSolver *S, int q, int nIter, int nd3) {
 		 * whichever buffer holds the iterate, pp_restore puts it back) */
 		for (; k + 2 <= nIter; k += 2) {
 			int slot = q == 0 && (k & 2) == 0 ? pinc_probe_begin(PINC_PROBE_GS) : -1;
+			if (q == 0 && (k & 2)) pinc_probe_count(PINC_PROBE_GS);
 			pinc_check(pinc_hip_gs_sweep2x(S->phi[q], S->res[q], S->rho[q], L, g_pinc.stream), "gs sweep2x");
 			pinc_probe_end(PINC_PROBE_GS, slot, 24.0 * S->N[q]);
 			double *t = S->phi[q];
@@ -476,6 +511,7 @@ static void smooth_native(MultigridSolver *S, int q, int nIter, int nd3) {
 			pinc_check(pinc_hip_gs_sweep2x(S->phi[q], S->res[q], S->rho[q], L, g_pinc.stream), "gs sweep2x");
 			/* two full iterations: phi R + W, rho R (24 B per point) once */
 			pinc_probe_end(PINC_PROBE_GS, slot, 24.0 * S->N[q]);
+			pinc_probe_count(PINC_PROBE_GS);
 			pinc_check(pinc_hip_gs_sweep2x(S->res[q], S->phi[q], S->rho[q], L, g_pinc.stream), "gs sweep2x");
 		}
 	}
@@ -485,6 +521,7 @@ static void smooth_native(MultigridSolver *S, int q, int nIter, int nd3) {
 			pinc_check(pinc_hip_gs_sweep(S->phi[q], S->res[q], S->rho[q], L, g_pinc.stream), "gs sweep");
 			/* one full iteration: phi R + W, rho R (24 B per point) */
 			pinc_probe_end(PINC_PROBE_GS, slot, 24.0 * S->N[q]);
+			if (q == 0 && !fused2) pinc_probe_count(PINC_PROBE_GS);
 			pinc_check(pinc_hip_gs_sweep(S->res[q], S->phi[q], S->rho[q], L, g_pinc.stream), "gs sweep");
 		}
 	}
@@ -503,7 +540,8 @@ static int first_sweep_is_double(const MultigridSolver *S) {
 	const pinc_lvl_t L = S->L[0];
 	if (!S->native || S->shard || S->nPre < 2 || !S->pre3d) return 0;
 	int fused = L.nd == 3 && L.T[0] % 16 == 0 && L.T[1] % 16 == 0 && L.T[2] % 16 == 0 && S->N[0] >= S->fusedMin;
-	return fused && L.T[0] % 32 == 0 && L.T[1] % 8 == 0;
+	return fused && L.T[0] % 32 == 0 && L.T[1] % 8 == 0 &&
+	       !(((uintptr_t)S->phi[0] | (uintptr_t)S->res[0] | (uintptr_t)S->rho[0]) & 15);
 }
 
 /* the iterate back into phi[q]'s own buffer after a swapped smoothing */
@@ -568,6 +606,18 @@ static int coarse_start(const MultigridSolver *S) {
 
 static void vrec(MultigridSolver *S, int q) {
 	int bottom = S->nLevels - 1;
+	if (S->dist1 && q == 1) {
+		/* two-grid cycle, level 1 decomposed: this rank's restricted
+		 * residual planes through the slab-distributed transform with the
+		 * 7-point symbol (DC dropped), then one level-1 halo plane from each
+		 * neighbour for the prolongation */
+		const long ps1 = (long)S->L[1].T[0] * S->L[1].T[1];
+		const int n1 = S->nloc0 / 2;
+		pinc_slab_poisson(S->fftCoarseSlab, S->rho1Slab, S->phi1Ext + ps1, "mg spectral coarse (slabs)");
+		pinc_ext_halo(S->phi1Ext, ps1, n1, 1);
+		prolong_into(S, 0);
+		return;
+	}
 	if (S->fftCoarse && q == 1) {
 		/* two-grid cycle with an exact coarse solve: the level-1 correction
 		 * equation -L phi1 = rho1 (rho1 the restricted residual, times 4)

@@ -526,6 +526,10 @@ void pinc_obj_collect(PincObj *o, Population *pop, int discard) {
 				continue;
 			}
 			pinc_check(rc, "object collect");
+			/* the flags written over [first, iStop) are the centre again (the
+			 * extraction put the collected ones back); an earlier write's
+			 * leavers below first would not be */
+			if (dv->flagState[s] != PINC_FLAGS_CLEAN) dv->flagState[s] = PINC_FLAGS_UNKNOWN;
 			pinc_check(pinc_hip_d2h(hc, o->dCount, K * sizeof(int), g_pinc.stream), "object count");
 			pop->iStop[s] -= nRem;
 			/* removals reorder the tail: cell counts and sorted prefix */

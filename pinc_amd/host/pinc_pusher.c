@@ -210,6 +210,57 @@ static int wrap_mask(const Population *pop) {
 	return !pop->dev->tiled ? 0 : (g_pinc.nranks == 1 ? (1 << nd) - 1 : (1 << (nd - 1)) - 1);
 }
 
+/* ------------------------------------------------------------- flags -- */
+/* One flag byte per particle slot: its neighbour code after the last
+ * classification, which the extraction reads (pinc_hip_extract).  Only the
+ * leavers' codes differ from the centre, and the extraction puts theirs back
+ * to the centre.  So when all of species s's range holds the centre
+ * (PINC_FLAGS_CLEAN), a push writes only its leavers' flags: at one rank,
+ * where every dimension wraps in place, no flag at all instead of 1 B per
+ * particle.  A write that leaves flags behind the extraction cannot reach
+ * (a second push before an extraction, a range that shrank in between) makes
+ * the state unknown, and the next push first sets the range to the centre. */
+static int flag_center(const Population *pop) {
+	int c = 0;
+	for (int d = 0, p = 1; d < pop->nDims; d++, p *= 3) c += p;
+	return c;
+}
+
+/* before a launch that writes species s's flags: 1 if it may write only the
+ * leavers' (sparseOk: a push), 0 if it writes every live particle's */
+int pinc_flags_before_write(Population *pop, int s, int sparseOk) {
+	PincDevPop *dv = pop->dev;
+	const long n = pop->iStop[s] - pop->iStart[s];
+	if (sparseOk && g_pinc.flagsSparse) {
+		if (dv->flagState[s] != PINC_FLAGS_CLEAN) {
+			const long a = pop->iStart[s], len = pop->iStart[s + 1] - a;
+			if (len > 0)
+				pinc_check(pinc_hip_memset(dv->flags + a, flag_center(pop), (unsigned long)len, g_pinc.stream),
+				           "flags to the centre");
+		}
+		dv->flagState[s] = PINC_FLAGS_PENDING;
+		dv->flagN[s] = n;
+		return 1;
+	}
+	/* a full write covers [0, n): the flags of an earlier write survive only
+	 * beyond n */
+	if (dv->flagState[s] == PINC_FLAGS_CLEAN || (dv->flagState[s] == PINC_FLAGS_PENDING && n >= dv->flagN[s])) {
+		dv->flagState[s] = PINC_FLAGS_PENDING;
+		dv->flagN[s] = n;
+	} else {
+		dv->flagState[s] = PINC_FLAGS_UNKNOWN;
+	}
+	return 0;
+}
+
+/* after pinc_hip_extract of species s over its nBefore live particles: every
+ * flagged particle was extracted and its flag put back */
+void pinc_flags_after_extract(Population *pop, int s, long nBefore) {
+	PincDevPop *dv = pop->dev;
+	if (dv->flagState[s] == PINC_FLAGS_PENDING)
+		dv->flagState[s] = nBefore >= dv->flagN[s] ? PINC_FLAGS_CLEAN : PINC_FLAGS_UNKNOWN;
+}
+
 /* tiled + fused: key counts of the current positions and scratch */
 static void ensure_keys(Population *pop) {
 	PincDevPop *dv = pop->dev;
@@ -434,6 +485,7 @@ static int push_all(Population *pop, Grid *E, double *const *xout) {
 		a.wrapMask = wrap_mask(pop);
 		a.kePartial = dv->kePartial;
 		a.tileWidth = dv->tileWidth;
+		a.flagsSparse = pinc_flags_before_write(pop, s, 1);
 		pinc_check(pinc_hip_memset(a.chunkCount, 0, chunks * sizeof(int), g_pinc.stream), "chunk counts");
 		if (adaptive) {
 			a.moved = dv->movedCnt + s;
@@ -594,8 +646,12 @@ void pinc_pending_vel(const Population *pop, int s, double *const *dst) {
 	if (dv->permId[s] || dv->vKicked[s]) return;
 	if (!dv->pendingE) msg(ERROR, "pending sorted push without its E");
 	if (!pinc_grid_live(dv->pendingE, dv->pendingESerial) || dv->pendingE->dev->gen != dv->pendingEGen)
-		msg(ERROR, "internal: E was changed or freed between puAcc and a re-kick of the pending sorting push "
-		           "(pinc_grid_touch missed a write)");
+		/* this catches a freed or reallocated E, and a writer that called
+		 * pinc_grid_touch without the re-kick above it; a device write that
+		 * skips pinc_grid_touch leaves gen as it was and is not seen here, so
+		 * every E-writing operator must call it (pinc_grid.c) */
+		msg(ERROR, "internal: E was freed, reallocated or touched between puAcc and a re-kick of the pending "
+		           "sorting push");
 	PincDevGrid *eg = dv->pendingE->dev;
 	pinc_check(pinc_hip_field_chain(eg->d, eg->scaled, eg->n, dv->qm, dv->mq, 1.0, s, g_pinc.stream), "E chain");
 	pinc_pop_t p = pinc_devpop(pop);
@@ -698,12 +754,15 @@ static void classify(Population *pop, int doMove) {
 	for (int s = 0; s < PINC_MAX_SPECIES; s++) dv->cntValid[s] = 0;
 	dv->depValid = 0;
 	dv->emigValid = 0; /* (flags of this classification: not counted) */
-	if (doMove) g_pinc.errSerial++;
+	/* every launch gets dErr: a classification without a move still sets the
+	 * out-of-frame bit, so the next assert read must not be skipped */
+	g_pinc.errSerial++;
 	int wrapMask = wrap_mask(pop);
 	pinc_pop_t p = pinc_devpop(pop);
 	for (int s = 0; s < pop->nSpecies; s++) {
 		long n = pop->iStop[s] - pop->iStart[s];
 		int slot = doMove ? pinc_probe_begin(PINC_PROBE_MOVE) : -1;
+		pinc_flags_before_write(pop, s, 0);
 		pinc_check(pinc_hip_move_classify(p, s, doMove, g_pinc.thr, dv->flags, dv->chunkCount + dv->chunkBase[s],
 		                                  g_pinc.maxVel, g_pinc.dErr, wrapMask, g_pinc.stream),
 		           "move/classify");
@@ -738,7 +797,9 @@ static void extract(Population *pop, MpiInfo *m) {
 	memset(m->nEmigrants, 0, nN * ns * sizeof(long));
 	for (int s = 0; s < ns; s++) {
 		if (known && dv->emigLast[s] == 0) {
-			/* nothing flagged to leave: the extraction would find nothing */
+			/* nothing flagged to leave: the extraction would find nothing
+			 * (and every flag of the last write is the centre) */
+			if (dv->flagState[s] == PINC_FLAGS_PENDING) dv->flagState[s] = PINC_FLAGS_CLEAN;
 			dv->nEmig[s] = 0;
 			memset(dv->neCount[s], 0, sizeof(dv->neCount[s]));
 			if (dv->depValid) dv->depEnd[s] = pop->iStop[s];
@@ -754,6 +815,7 @@ static void extract(Population *pop, MpiInfo *m) {
 				continue;
 			}
 			pinc_check(rc, "extract emigrants");
+			pinc_flags_after_extract(pop, s, p.iStop[s] - p.iStart[s]);
 			dv->nEmig[s] = nEmig;
 			break;
 		}

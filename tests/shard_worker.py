@@ -27,6 +27,8 @@ def main() -> int:
     ap.add_argument("--seed", type=int, default=20261016)
     ap.add_argument("--out", required=True)
     ap.add_argument("--spectral", action="store_true", help="sSolver (slab-distributed) instead of the multigrid")
+    ap.add_argument("--spectral-coarse", action="store_true",
+                    help="multigrid:spectralCoarse (level 1 solved exactly; decomposed with the sharded level 0)")
     args = ap.parse_args()
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     import torch.distributed as dist
@@ -34,7 +36,9 @@ def main() -> int:
     import mg_history
     from pinc_amd import Sim
     from pinc_amd.transport import GlooTransport
-    ini = mg_history.ini_for(args.size, args.levels, True, nranks=world, shard="1", spectral=args.spectral)
+    ini = mg_history.ini_for(args.size, args.levels, True, nranks=world, shard="1", spectral=args.spectral,
+                             spectral_coarse=args.spectral_coarse)
+    from pinc_amd import _lib
     rho = mg_history.rank_slab(mg_history.make_rho(args.size, args.seed, 1.0), rank, world)
     out = {}
     try:
@@ -44,11 +48,15 @@ def main() -> int:
             else:
                 s.mg_limit(args.cycles, args.cycles)
                 out["halo"] = np.array(s.mg_shard)
+            _lib.comm_stats_start(1 << 12)
             for k in range(args.solves):
                 s.set_grid(0, rho)
                 s.op("solve")
                 if not args.spectral:
                     out[f"hist{k}"] = s.mg_history()
+            # collectives of the solves: calls and payload bytes per kind
+            for kind, c in _lib.comm_stats_read().items():
+                out[f"comm_{kind}"] = np.array([c["calls"], c["bytes"]])
             out["phi"] = s.grid(1)[..., 0].copy()
             s.op("efield")
             out["E"] = s.grid(2).copy()

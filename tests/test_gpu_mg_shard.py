@@ -73,7 +73,7 @@ def test_spectral_coarse_matches_native_oracle(shard):
     assert np.max(np.abs(g["phi"] - o["phi"])) <= 1e-9 * np.max(np.abs(o["phi"]))
 
 
-def _two_ranks(size, levels, tmp_path, fused_min=None, cycles=60, solves=2, world=2):
+def _two_ranks(size, levels, tmp_path, fused_min=None, cycles=60, solves=2, world=2, spectral_coarse=False):
     out = tmp_path / "shard"
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2")
     if fused_min is not None:
@@ -81,15 +81,15 @@ def _two_ranks(size, levels, tmp_path, fused_min=None, cycles=60, solves=2, worl
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr=127.0.0.1", f"--master-port={_port()}", str(ROOT / "tests" / "shard_worker.py"),
            "--size", str(size), "--levels", str(levels), "--cycles", str(cycles), "--solves", str(solves),
-           "--out", str(out)]
+           "--out", str(out)] + (["--spectral-coarse"] if spectral_coarse else [])
     p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     return [dict(np.load(f"{out}_r{r}.npz")) for r in range(world)]
 
 
-def _oracle_two_ranks(size, levels, cycles=60, solves=2, world=2):
+def _oracle_two_ranks(size, levels, cycles=60, solves=2, world=2, spectral_coarse=False):
     import orc
-    ini = mg_history.ini_for(size, levels, True, nranks=world)
+    ini = mg_history.ini_for(size, levels, True, nranks=world, spectral_coarse=spectral_coarse)
     rho = mg_history.make_rho(size, 20261016, 1.0)
     try:
         w = orc.World(ini)
@@ -143,6 +143,34 @@ def test_four_ranks_shard_matches_oracle(tmp_path):
         for k in range(2):
             _check_hist(g[r][f"hist{k}"], ho[k])
         assert np.max(np.abs(g[r]["phi"][1:-1] - po[r][1:-1])) <= 1e-9 * scale
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_ranks_decomposed_level1_matches_oracle(tmp_path, world):
+    """multigrid:spectralCoarse on the sharded level 0 with the level-1 solve
+    decomposed as well (the reference keeps every level
+    on its subdomain, multigrid.c:128-180, 1496-1556): each rank's restricted
+    residual planes go through the slab-distributed transform with the
+    7-point symbol, one level-1 halo plane comes from each neighbour, and
+    only the owned level-0 planes are corrected.  No all-gather in the
+    solve: the transposes replace it.  Against the oracle's native solve with
+    the exact level-1 solve (orc_discrete_poisson), 128^3 in 2 and 4 z-slabs:
+    residual history per cycle, phi to 1e-9 of its maximum, E to 1e-8."""
+    g = _two_ranks(128, 5, tmp_path, world=world, spectral_coarse=True)
+    ho, po, Eo = _oracle_two_ranks(128, 5, world=world, spectral_coarse=True)
+    scale = max(np.max(np.abs(p[1:-1])) for p in po)
+    inner = (slice(1, -1),) * 3
+    escale = max(np.max(np.abs(e[inner])) for e in Eo)
+    for r in range(world):
+        assert int(g[r]["halo"]) > 0
+        # the level-1 all-gather is gone; the transposes carry level 1
+        assert g[r]["comm_allgather"][0] == 0, g[r]["comm_allgather"]
+        assert g[r]["comm_spectral_transpose"][0] > 0
+        for k in range(2):
+            _check_hist(g[r][f"hist{k}"], ho[k])
+        assert np.max(np.abs(g[r]["phi"][1:-1] - po[r][1:-1])) <= 1e-9 * scale
+        assert np.max(np.abs(g[r]["E"][inner] - Eo[r][inner])) <= 1e-8 * escale
+    assert g[0]["hist0"][-1] <= 1e-10
 
 
 def test_shard_off_below_threshold(tmp_path):

@@ -189,7 +189,8 @@ class PushArgs(C.Structure):
                 ("tileWidth", C.c_int), ("cursor", C.c_void_p), ("cntNext", C.c_void_p), ("moved", C.c_void_p),
                 ("spread", C.c_void_p), ("tstamp", C.c_void_p), ("diag", C.c_void_p), ("objInside", C.c_void_p),
                 ("objSy", C.c_long), ("objSz", C.c_long), ("objNodes", C.c_long), ("objCount", C.c_void_p),
-                ("objLo", C.c_int * 3), ("objHi", C.c_int * 3), ("emigTotal", C.c_void_p)]
+                ("objLo", C.c_int * 3), ("objHi", C.c_int * 3), ("emigTotal", C.c_void_p),
+                ("flagsSparse", C.c_int)]
 
 
 def _embedded_fractions(rho_dev: np.ndarray, T, k):
@@ -273,3 +274,88 @@ def test_pudistr3d1_known_answers_tiled_cells(hip):
     assert hip.pinc_hip_deposit_cells(out, 0, g, 4, ends, n, rho.data_ptr(), None) == 0
     torch.cuda.synchronize()
     _embedded_fractions(rho.cpu().numpy(), T, k)
+
+
+class ExtractWs(C.Structure):
+    """pinc_extract_ws_t (include/pinc_hip.h)."""
+    _fields_ = [("chunkOffset", C.c_void_p), ("scanWork", C.c_void_p), ("tail", C.c_void_p), ("holes", C.c_void_p),
+                ("order", C.c_void_p), ("blockHist", C.c_void_p), ("scratch", C.c_void_p), ("buf", C.c_void_p),
+                ("bufNe", C.c_void_p), ("cap", C.c_long)]
+
+
+@pytest.mark.parametrize("nd_method", ["puExtractEmigrants3D", "puExtractEmigrantsND"])
+def test_extract_emigrants_back_fill_order(hip, nd_method):
+    """testExtractEmigrantsXD (pusher.test.c:360-545) through the HIP
+    classification (k_move_classify, doMove = 0, no wrap: the reference
+    layout) and the parallel back-fill extraction (k_extract_a/b, k_rank_*,
+    k_fill_holes) of libpinc_hip.so: the 81 emigrant counts, every
+    emigrants[ne] buffer in the reference's order (species after species,
+    extraction order inside), iStop = {17, 117, 200} and the 17 survivors of
+    each species in the serial back-fill's slot order, exactly.  (Both
+    reference methods classify a 3-D particle alike; the device has one
+    classification for any nDims, run here under each method's name.)
+    The oracle's restatement passes the same checks on the CPU
+    (tests/test_oracle_kat.py)."""
+    import torch
+    import extract_kat as X
+    hip.pinc_hip_extract.argtypes = [Pop, C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_int, ExtractWs,
+                                     C.POINTER(C.c_long), C.POINTER(C.c_long), C.c_void_p]
+    start = X.K["iStart"]
+    total = start[-1] + 100
+    p, v = X.inputs()
+    xs = [torch.zeros(total, dtype=torch.float64, device="cuda") for _ in range(3)]
+    vs = [torch.zeros(total, dtype=torch.float64, device="cuda") for _ in range(3)]
+    stop = list(start)
+    for s in X.K["species_with_particles"]:
+        for d in range(3):
+            xs[d][start[s]:start[s] + len(p)] = torch.from_numpy(p[:, d].copy())
+            vs[d][start[s]:start[s] + len(p)] = torch.from_numpy(v[:, d].copy())
+        stop[s] = start[s] + len(p)
+    pop = Pop((C.c_void_p * 3)(*[t.data_ptr() for t in xs]), (C.c_void_p * 3)(*[t.data_ptr() for t in vs]), 3, 3,
+              (C.c_long * 9)(*(start + [total])), (C.c_long * 8)(*stop))
+    t = X.K["expect_thresholds"]
+    hi = 8 + 1.0                                                    # local frame: true nodes 1..8
+    thr = (C.c_double * 9)(*t[:3], *t[3:], hi, hi, hi)
+    flags = torch.zeros(total, dtype=torch.uint8, device="cuda")
+    err = torch.zeros(1, dtype=torch.int32, device="cuda")
+    cap = 64
+    records = {}
+    counts = np.zeros((27, 3), dtype=np.int64)
+    keep = []
+    for s in range(3):
+        cnt = torch.zeros(4, dtype=torch.int32, device="cuda")
+        i32 = lambda n: torch.zeros(n, dtype=torch.int32, device="cuda")
+        ws_t = [i32(8), i32(8), i32(cap + 1), i32(cap + 1), i32(cap), i32(28 * 4 + 28), i32(128),
+                torch.zeros(6 * cap, dtype=torch.float64, device="cuda"), torch.zeros(cap, dtype=torch.uint8,
+                                                                                     device="cuda")]
+        keep += ws_t
+        ws = ExtractWs(*[a.data_ptr() for a in ws_t], cap)
+        assert hip.pinc_hip_move_classify(pop, s, 0, thr, flags.data_ptr(), cnt.data_ptr(), 1e30, err.data_ptr(),
+                                          0, None) == 0
+        ne_emig = C.c_long()
+        ne_count = (C.c_long * 28)()
+        assert hip.pinc_hip_extract(pop, s, flags.data_ptr(), cnt.data_ptr(), 13, 27, ws, C.byref(ne_emig),
+                                    ne_count, None) == 0
+        torch.cuda.synchronize()
+        pop.iStop[s] -= ne_emig.value
+        buf = ws_t[7].cpu().numpy().reshape(6, cap)
+        base = 0
+        for ne in range(28):
+            n = ne_count[ne]
+            if ne < 27:
+                counts[ne, s] = n
+            if n:
+                records.setdefault(ne, []).append(buf[:, base:base + n].T.copy())
+            base += n
+    assert int(err[0]) == 0
+    assert list(pop.iStop)[:3] == X.K["expect_iStop"]
+
+    def recs(ne):
+        r = records.get(ne, [])
+        return np.concatenate(r) if r else np.zeros((0, 6))
+
+    def survivors(s):
+        a, b = start[s], pop.iStop[s]
+        return (np.stack([x.cpu().numpy()[a:b] for x in xs], 1), np.stack([x.cpu().numpy()[a:b] for x in vs], 1))
+
+    X.check(counts, recs, survivors)

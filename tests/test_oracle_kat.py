@@ -109,3 +109,34 @@ def test_const_e_leapfrog():
             pos += vel
             lib.orc_kat_acc(3, _ptr(ts), 0, _ptr(E), 1, _ptr(pos), _ptr(vel), q, m, 1, _ptr(ke))
             assert abs(pos[0] - (x0 + 0.5 * (q / m) * n * n)) < k["tol"], (qm, n, pos[0])
+
+
+
+@pytest.mark.parametrize("use3d", [1, 0], ids=["puExtractEmigrants3D", "puExtractEmigrantsND"])
+def test_extract_emigrants_back_fill_order(use3d):
+    """testExtractEmigrantsXD (pusher.test.c:360-545): the 81 emigrant
+    counts, every emigrants[ne] buffer in order, iStop = {17, 117, 200} and
+    the 17 survivors of each species in the serial back-fill's slot order
+    (thresholds restated for the current upper rule, tests/extract_kat.py)."""
+    import extract_kat as X
+    lib = _lib()
+    start = np.array(X.K["iStart"] + [300], dtype=np.int64)
+    stop = start[:3].copy()
+    pos = np.zeros((300, 3))
+    vel = np.zeros((300, 3))
+    p, v = X.inputs()
+    for s in X.K["species_with_particles"]:
+        pos[start[s]:start[s] + len(p)] = p
+        vel[start[s]:start[s] + len(p)] = v
+        stop[s] = start[s] + len(p)
+    cap = 16
+    counts = np.zeros(27 * 3, dtype=np.int64)
+    bufs = np.zeros((27, cap, 6))
+    thr = np.zeros(6)
+    lib.orc_kat_extract(X.grid_ini_text().encode(), 3, _ptr(start), _ptr(stop), _ptr(pos), _ptr(vel), use3d,
+                        _ptr(counts), _ptr(bufs), cap, _ptr(thr))
+    np.testing.assert_array_equal(thr, X.K["expect_thresholds"])
+    np.testing.assert_array_equal(stop, X.K["expect_iStop"])
+    counts = counts.reshape(27, 3)
+    X.check(counts, lambda ne: bufs[ne, :counts[ne].sum()],
+            lambda s: (pos[start[s]:stop[s]], vel[start[s]:stop[s]]))
