@@ -1459,6 +1459,22 @@ constexpr int kPushGroupMin = PINC_PUSH_GROUP_MIN;
 #ifndef PINC_PUSH_NT
 #define PINC_PUSH_NT 0
 #endif
+// 1 (with PINC_PUSH_CONSEC): a full block's particle loads and stores are
+// contiguous per wave instruction (lane l: 16-B pair l, then pair 64 + l of
+// the wave's 256 particles) and adjacent lanes swap one pair each (DPP), so
+// that a thread still holds four consecutive particles: even lane 2k those
+// at 4k, odd lane 2k + 1 those at 128 + 4k.  The mapping where a thread
+// loads its own four (every other 16 B of 2 KB per instruction) copies at
+// 5.69 TB/s on this chip against 6.13 TB/s contiguous
+// (profiles/r06b_copy_probe3_lane_mapping.jsonl)
+#ifndef PINC_PUSH_XCH
+#define PINC_PUSH_XCH 2
+#endif
+// 1: the push stages its E box one 8-B word per lane (coalesced rows)
+// instead of one node (three strided words) per lane
+#ifndef PINC_PUSH_EWORDS
+#define PINC_PUSH_EWORDS 0
+#endif
 #ifndef PINC_PUSH_RHO_LDS
 #define PINC_PUSH_RHO_LDS 2048
 #endif
@@ -1940,7 +1956,27 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	const long base = (long)chunk * kPushChunk;
 	// item k of a thread: particles in lane-contiguous pairs (16-B loads and
 	// stores, 1 KiB per wave instruction), pair k/2 of the thread
-#if PINC_PUSH_CONSEC
+#if PINC_PUSH_CONSEC && PINC_PUSH_XCH == 2
+	// the kPushItems particles of a thread are consecutive, so a thread's
+	// particles mostly share a cell and their charge is summed in the thread
+	// before the LDS adds; rows of 16 lanes swap halves so that full blocks
+	// load and store contiguously (PINC_PUSH_XCH): row r of a wave holds the
+	// 64 consecutive particles at {0, 128, 64, 192}[r], lane i of it those
+	// at 4i of them
+	static_assert(kPushItems == 4 && kPushThreads % 64 == 0, "lane exchange: four items per thread");
+	auto item = [&](int k) -> long {
+		return base + (long)(wv * 256 + ((lane >> 4) & 1) * 128 + (lane >> 5) * 64 + (lane & 15) * 4 + k);
+	};
+#elif PINC_PUSH_CONSEC && PINC_PUSH_XCH
+	// the kPushItems particles of a thread are consecutive, so a thread's
+	// particles mostly share a cell and their charge is summed in the thread
+	// before the LDS adds; lane pairs swap halves so that full blocks load
+	// and store contiguously (PINC_PUSH_XCH)
+	static_assert(kPushItems == 4 && kPushThreads % 64 == 0, "lane exchange: four items per thread");
+	auto item = [&](int k) -> long {
+		return base + (long)(wv * 256 + (lane & 1) * 128 + (lane >> 1) * 4 + k);
+	};
+#elif PINC_PUSH_CONSEC
 	// the kPushItems particles of a thread are consecutive (two 16-B loads per
 	// array and thread: a wave instruction covers every other 16 B of 2 KB,
 	// the next one the rest, through L2), so a thread's particles mostly share
@@ -1971,6 +2007,76 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	double p[kPushItems][ND], vv[kPushItems][ND];
 	unsigned valid = 0;
 	static_assert(kPushItems % 2 == 0, "items come in pairs");
+#if PINC_PUSH_CONSEC && PINC_PUSH_XCH
+	// a full block of aligned arrays: two contiguous 16-B loads per array and
+	// thread (wave pairs lane and 64 + lane), then the odd lane's first pair
+	// and the even lane's second pair change places (quad_perm [1,0,3,2])
+	const bool full = al && base + kPushChunk <= a.n;
+	const bool odd = lane & 1;
+	auto swap_adj = [](dvec2 v) -> dvec2 { return dvec2{dpp<kDppQuadXor1>(v.x), dpp<kDppQuadXor1>(v.y)}; };
+	// (XCH 2) lane l loads pair pi(l) and 64 + pi(l) of the wave's 128: rows 0
+	// and 1 (2 and 3) interleave pairs 0..31 (32..63) even/odd, so the row
+	// swap (v_permlane16_swap: odd rows of the first <-> even rows of the
+	// second) leaves each lane two consecutive pairs; every wave instruction
+	// still covers one contiguous 1 KB
+	auto pi_lane = [](int l) { return ((l >> 5) << 5) + 2 * (l & 15) + ((l >> 4) & 1); };
+	auto rowswap = [](dvec2 &u, dvec2 &w) {
+		typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+		u32x4 A = __builtin_bit_cast(u32x4, u), B = __builtin_bit_cast(u32x4, w);
+#pragma unroll
+		for (int i = 0; i < 4; i++) {
+			const auto r = __builtin_amdgcn_permlane16_swap(A[i], B[i], false, false);
+			A[i] = r[0];
+			B[i] = r[1];
+		}
+		u = __builtin_bit_cast(dvec2, A);
+		w = __builtin_bit_cast(dvec2, B);
+	};
+	(void)pi_lane;
+	(void)rowswap;
+	if (full && PINC_PUSH_XCH == 2) {
+		valid = (1u << kPushItems) - 1;
+		const long q0 = base + wv * 256 + 2 * pi_lane(lane);
+#pragma unroll
+		for (int d = 0; d < ND; d++) {
+			dvec2 x0 = *reinterpret_cast<const dvec2 *>(a.xi[d] + q0);
+			dvec2 x1 = *reinterpret_cast<const dvec2 *>(a.xi[d] + q0 + 128);
+			dvec2 v0 = *reinterpret_cast<const dvec2 *>(a.vi[d] + q0);
+			dvec2 v1 = *reinterpret_cast<const dvec2 *>(a.vi[d] + q0 + 128);
+			rowswap(x0, x1);
+			rowswap(v0, v1);
+			p[0][d] = x0.x;
+			p[1][d] = x0.y;
+			p[2][d] = x1.x;
+			p[3][d] = x1.y;
+			vv[0][d] = v0.x;
+			vv[1][d] = v0.y;
+			vv[2][d] = v1.x;
+			vv[3][d] = v1.y;
+		}
+	} else if (full) {
+		valid = (1u << kPushItems) - 1;
+		const long q0 = base + wv * 256 + 2 * lane;  // the wave's pair `lane`; pair 64 + lane 128 later
+#pragma unroll
+		for (int d = 0; d < ND; d++) {
+			const dvec2 x0 = *reinterpret_cast<const dvec2 *>(a.xi[d] + q0);
+			const dvec2 x1 = *reinterpret_cast<const dvec2 *>(a.xi[d] + q0 + 128);
+			const dvec2 v0 = *reinterpret_cast<const dvec2 *>(a.vi[d] + q0);
+			const dvec2 v1 = *reinterpret_cast<const dvec2 *>(a.vi[d] + q0 + 128);
+			const dvec2 xr = swap_adj(odd ? x0 : x1), vr = swap_adj(odd ? v0 : v1);
+			const dvec2 xa = odd ? xr : x0, xb = odd ? x1 : xr;
+			const dvec2 va = odd ? vr : v0, vb = odd ? v1 : vr;
+			p[0][d] = xa.x;
+			p[1][d] = xa.y;
+			p[2][d] = xb.x;
+			p[3][d] = xb.y;
+			vv[0][d] = va.x;
+			vv[1][d] = va.y;
+			vv[2][d] = vb.x;
+			vv[3][d] = vb.y;
+		}
+	} else
+#endif
 #pragma unroll
 	for (int k = 0; k < kPushItems; k += 2) {
 		const long i = item(k);
@@ -2133,7 +2239,28 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	const int myCopy = (lane & (nCopy - 1)) * rStride;
 	for (int t = threadIdx.x; t < (PINC_PUSH_COPIES ? nCopy * rStride : rB.vol); t += kPushThreads) rhoL[t] = 0.0;
 	for (int t = threadIdx.x; t < (SORT ? kInCellCap : obb.vol); t += kPushThreads) cntOut[t] = 0;
-	if (KICK && !(PINC_PUSH_SKIP & 2)) {
+	if (KICK && !(PINC_PUSH_SKIP & 2) && PINC_PUSH_EWORDS && ND == 3) {
+		// one 8-B word per lane: consecutive lanes read consecutive words of
+		// a box row (value-major E: a row of n nodes is 3n contiguous words
+		// unless x wraps), instead of three 24-B-strided loads per node
+		const BoxRcp eq = box_rcp(eB);
+		for (int w = threadIdx.x; w < 3 * eB.vol; w += kPushThreads) {
+			const int t = (int)(((unsigned)w * 43691u) >> 17);  // w / 3 (w < 2^15)
+			const int comp = w - 3 * t;
+			int c[3] = {0, 0, 0};
+			box_coords(eB, eq, t, c, ND);
+			int off = 0;
+#pragma unroll
+			for (int d = 0; d < ND; d++) {
+				int o0, o1;
+				node_pair(G, d, c[d], o0, o1);
+				off += o0;
+			}
+			const double e = a.Es[(unsigned)(off * 3 + comp)];
+			if (comp < 2) eL[2 * t + comp] = e;
+			else eL[2 * EC + t] = e;
+		}
+	} else if (KICK && !(PINC_PUSH_SKIP & 2)) {
 		const BoxRcp eq = box_rcp(eB);
 		for (int t = threadIdx.x; t < eB.vol; t += kPushThreads) {
 			int c[3] = {0, 0, 0};
@@ -2482,6 +2609,38 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	// (all pairs after the last kick: storing each pair right after its
 	// kick, to free its velocity registers, measured 20.6 -> 26.2 ms per
 	// plain push at C4, profiles/r05j_push_early_store_ab.txt)
+#if PINC_PUSH_CONSEC && PINC_PUSH_XCH
+	if (!SORT && full && PINC_PUSH_XCH == 2) {
+		// the load's row swap backwards (an involution)
+		const long q0 = base + wv * 256 + 2 * pi_lane((int)(threadIdx.x & 63));
+		auto put = [&](double *o, const double (*q)[ND], int d) {
+			dvec2 a0{q[0][d], q[1][d]}, a1{q[2][d], q[3][d]};
+			rowswap(a0, a1);
+			*reinterpret_cast<dvec2 *>(o + q0) = a0;
+			*reinterpret_cast<dvec2 *>(o + q0 + 128) = a1;
+		};
+#pragma unroll
+		for (int d = 0; d < ND; d++) {
+			put(a.xo[d], p, d);
+			if (wvel) put(a.vo[d], vv, d);
+		}
+	} else if (!SORT && full) {
+		// the load's exchange backwards: contiguous 16-B stores per wave
+		// instruction (pair lane, then pair 64 + lane)
+		const long q0 = base + wv * 256 + 2 * lane;
+		auto put = [&](double *o, const double (*q)[ND], int d) {
+			const dvec2 a0{q[0][d], q[1][d]}, a1{q[2][d], q[3][d]};
+			const dvec2 r = swap_adj(odd ? a0 : a1);
+			*reinterpret_cast<dvec2 *>(o + q0) = odd ? r : a0;
+			*reinterpret_cast<dvec2 *>(o + q0 + 128) = odd ? a1 : r;
+		};
+#pragma unroll
+		for (int d = 0; d < ND; d++) {
+			put(a.xo[d], p, d);
+			if (wvel) put(a.vo[d], vv, d);
+		}
+	} else
+#endif
 	if (!SORT) {
 #pragma unroll
 		for (int k = 0; k < kPushItems; k += 2) store_pair(k);
