@@ -1470,6 +1470,15 @@ constexpr int kPushGroupMin = PINC_PUSH_GROUP_MIN;
 #ifndef PINC_PUSH_XCH
 #define PINC_PUSH_XCH 2
 #endif
+// (PINC_PUSH_XCH 2, full blocks) bit 0: nontemporal particle loads, bit 1:
+// nontemporal particle stores (every wave instruction covers whole lines).
+// Both (3): plain push 19.63 -> 19.06 ms per species launch at C4, loads
+// alone 19.39, stores alone 19.30 (profiles/r06g_push_nontemporal_ab.txt);
+// with the round-5 mapping, where two instructions shared each line,
+// nontemporal access was slower (27.1 -> 30.1-42 ms, round 2)
+#ifndef PINC_PUSH_XCH_NT
+#define PINC_PUSH_XCH_NT 3
+#endif
 // 1: the push stages its E box one 8-B word per lane (coalesced rows)
 // instead of one node (three strided words) per lane
 #ifndef PINC_PUSH_EWORDS
@@ -2037,12 +2046,16 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	if (full && PINC_PUSH_XCH == 2) {
 		valid = (1u << kPushItems) - 1;
 		const long q0 = base + wv * 256 + 2 * pi_lane(lane);
+		auto ld = [](const double *ptr) -> dvec2 {
+			if (PINC_PUSH_XCH_NT & 1) return __builtin_nontemporal_load(reinterpret_cast<const dvec2 *>(ptr));
+			return *reinterpret_cast<const dvec2 *>(ptr);
+		};
 #pragma unroll
 		for (int d = 0; d < ND; d++) {
-			dvec2 x0 = *reinterpret_cast<const dvec2 *>(a.xi[d] + q0);
-			dvec2 x1 = *reinterpret_cast<const dvec2 *>(a.xi[d] + q0 + 128);
-			dvec2 v0 = *reinterpret_cast<const dvec2 *>(a.vi[d] + q0);
-			dvec2 v1 = *reinterpret_cast<const dvec2 *>(a.vi[d] + q0 + 128);
+			dvec2 x0 = ld(a.xi[d] + q0);
+			dvec2 x1 = ld(a.xi[d] + q0 + 128);
+			dvec2 v0 = ld(a.vi[d] + q0);
+			dvec2 v1 = ld(a.vi[d] + q0 + 128);
 			rowswap(x0, x1);
 			rowswap(v0, v1);
 			p[0][d] = x0.x;
@@ -2616,8 +2629,13 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 		auto put = [&](double *o, const double (*q)[ND], int d) {
 			dvec2 a0{q[0][d], q[1][d]}, a1{q[2][d], q[3][d]};
 			rowswap(a0, a1);
-			*reinterpret_cast<dvec2 *>(o + q0) = a0;
-			*reinterpret_cast<dvec2 *>(o + q0 + 128) = a1;
+			if (PINC_PUSH_XCH_NT & 2) {
+				__builtin_nontemporal_store(a0, reinterpret_cast<dvec2 *>(o + q0));
+				__builtin_nontemporal_store(a1, reinterpret_cast<dvec2 *>(o + q0 + 128));
+			} else {
+				*reinterpret_cast<dvec2 *>(o + q0) = a0;
+				*reinterpret_cast<dvec2 *>(o + q0 + 128) = a1;
+			}
 		};
 #pragma unroll
 		for (int d = 0; d < ND; d++) {
