@@ -1479,6 +1479,15 @@ constexpr int kPushGroupMin = PINC_PUSH_GROUP_MIN;
 #ifndef PINC_PUSH_XCH_NT
 #define PINC_PUSH_XCH_NT 3
 #endif
+// 1: the sorting push's per-item stores nontemporal
+#ifndef PINC_PUSH_SORT_NT
+#define PINC_PUSH_SORT_NT 0
+#endif
+// 1: the counting push adds a thread's same-brick items with one plain LDS
+// atomic instead of wave-aggregated adds per item
+#ifndef PINC_PUSH_COUNT_RUNS
+#define PINC_PUSH_COUNT_RUNS 0
+#endif
 // 1: the push stages its E box one 8-B word per lane (coalesced rows)
 // instead of one node (three strided words) per lane
 #ifndef PINC_PUSH_EWORDS
@@ -2680,8 +2689,13 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 			const long o = r >= 0 ? (long)bBase[r & 255] + (r >> 8) : (long)~r;
 #pragma unroll
 			for (int d = 0; d < ND; d++) {
-				a.xo[d][o] = p[k][d];
-				a.vo[d][o] = vv[k][d];
+				if (PINC_PUSH_SORT_NT) {
+					__builtin_nontemporal_store(p[k][d], &a.xo[d][o]);
+					__builtin_nontemporal_store(vv[k][d], &a.vo[d][o]);
+				} else {
+					a.xo[d][o] = p[k][d];
+					a.vo[d][o] = vv[k][d];
+				}
 			}
 			const int f = stageF[k * kPushThreads + threadIdx.x];
 			if (!a.flagsSparse || f != a.center) a.flags[o] = (unsigned char)f;
@@ -2689,7 +2703,25 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 		}
 	}
 	PUSH_TS(5);
-	if (a.cntNext) {
+	if (a.cntNext && PINC_PUSH_COUNT_RUNS) {
+		// count the output bricks of the particles that stay (next push's
+		// sort): a thread's consecutive items mostly share one, so the items in
+		// the brick of its first counted item add once (plain LDS atomics)
+		int l0 = -1, nm = 0;
+#pragma unroll
+		for (int k = 0; k < kPushItems; k++) {
+			const bool mine = (dep >> k) & 1u;
+			int c[3] = {0, 0, 0};
+#pragma unroll
+			for (int d = 0; d < ND; d++) c[d] = sort_cell(p[k][d], vv[k][d]);
+			const int lb = mine ? brick_inside<ND>(a.tg, obb, c) : -1;
+			if (lb >= 0 && l0 < 0) l0 = lb;
+			if (lb >= 0 && lb == l0) nm++;
+			else if (lb >= 0) atomicAdd(&cntOut[lb], 1);
+			if (mine && lb < 0) atomicAdd(&a.cntNext[brick_first_key<ND>(a.tg, c)], 1);
+		}
+		if (nm) atomicAdd(&cntOut[l0], nm);
+	} else if (a.cntNext) {
 		// count the output bricks of the particles that stay (next push's sort)
 #pragma unroll
 		for (int k = 0; k < kPushItems; k++) {
