@@ -1479,14 +1479,12 @@ constexpr int kPushGroupMin = PINC_PUSH_GROUP_MIN;
 #ifndef PINC_PUSH_XCH_NT
 #define PINC_PUSH_XCH_NT 3
 #endif
-// 1: the sorting push's per-item stores nontemporal
-#ifndef PINC_PUSH_SORT_NT
-#define PINC_PUSH_SORT_NT 0
-#endif
 // 1: the counting push adds a thread's same-brick items with one plain LDS
-// atomic instead of wave-aggregated adds per item
+// atomic instead of wave-aggregated adds per item (counting push 22.36 ->
+// 21.79 ms at C4, plain push unchanged, no spill with the lane exchange's
+// registers; profiles/r06i_count_runs_sort_nt_ab.txt)
 #ifndef PINC_PUSH_COUNT_RUNS
-#define PINC_PUSH_COUNT_RUNS 0
+#define PINC_PUSH_COUNT_RUNS 1
 #endif
 // 1: the push stages its E box one 8-B word per lane (coalesced rows)
 // instead of one node (three strided words) per lane
@@ -2689,13 +2687,10 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 			const long o = r >= 0 ? (long)bBase[r & 255] + (r >> 8) : (long)~r;
 #pragma unroll
 			for (int d = 0; d < ND; d++) {
-				if (PINC_PUSH_SORT_NT) {
-					__builtin_nontemporal_store(p[k][d], &a.xo[d][o]);
-					__builtin_nontemporal_store(vv[k][d], &a.vo[d][o]);
-				} else {
-					a.xo[d][o] = p[k][d];
-					a.vo[d][o] = vv[k][d];
-				}
+				// (nontemporal, 8 B per lane: 24.4 -> 33.5 ms per sorting push,
+				// profiles/r06i_count_runs_sort_nt_ab.txt)
+				a.xo[d][o] = p[k][d];
+				a.vo[d][o] = vv[k][d];
 			}
 			const int f = stageF[k * kPushThreads + threadIdx.x];
 			if (!a.flagsSparse || f != a.center) a.flags[o] = (unsigned char)f;
