@@ -1491,11 +1491,6 @@ constexpr int kPushGroupMin = PINC_PUSH_GROUP_MIN;
 #ifndef PINC_PUSH_SORT_PAIRS
 #define PINC_PUSH_SORT_PAIRS 0
 #endif
-// 1: the push stages its E box one 8-B word per lane (coalesced rows)
-// instead of one node (three strided words) per lane
-#ifndef PINC_PUSH_EWORDS
-#define PINC_PUSH_EWORDS 0
-#endif
 #ifndef PINC_PUSH_RHO_LDS
 #define PINC_PUSH_RHO_LDS 2048
 #endif
@@ -2264,28 +2259,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	const int myCopy = (lane & (nCopy - 1)) * rStride;
 	for (int t = threadIdx.x; t < (PINC_PUSH_COPIES ? nCopy * rStride : rB.vol); t += kPushThreads) rhoL[t] = 0.0;
 	for (int t = threadIdx.x; t < (SORT ? kInCellCap : obb.vol); t += kPushThreads) cntOut[t] = 0;
-	if (KICK && !(PINC_PUSH_SKIP & 2) && PINC_PUSH_EWORDS && ND == 3) {
-		// one 8-B word per lane: consecutive lanes read consecutive words of
-		// a box row (value-major E: a row of n nodes is 3n contiguous words
-		// unless x wraps), instead of three 24-B-strided loads per node
-		const BoxRcp eq = box_rcp(eB);
-		for (int w = threadIdx.x; w < 3 * eB.vol; w += kPushThreads) {
-			const int t = (int)(((unsigned)w * 43691u) >> 17);  // w / 3 (w < 2^15)
-			const int comp = w - 3 * t;
-			int c[3] = {0, 0, 0};
-			box_coords(eB, eq, t, c, ND);
-			int off = 0;
-#pragma unroll
-			for (int d = 0; d < ND; d++) {
-				int o0, o1;
-				node_pair(G, d, c[d], o0, o1);
-				off += o0;
-			}
-			const double e = a.Es[(unsigned)(off * 3 + comp)];
-			if (comp < 2) eL[2 * t + comp] = e;
-			else eL[2 * EC + t] = e;
-		}
-	} else if (KICK && !(PINC_PUSH_SKIP & 2)) {
+	if (KICK && !(PINC_PUSH_SKIP & 2)) {
 		const BoxRcp eq = box_rcp(eB);
 		for (int t = threadIdx.x; t < eB.vol; t += kPushThreads) {
 			int c[3] = {0, 0, 0};
