@@ -275,6 +275,10 @@ def main() -> int:
     ap.add_argument("--mg-graph", type=int, default=None,
                     help="1: native multigrid replays each V-cycle as a captured HIP graph (multigrid:graph); "
                          "default 1 for the launch-bound C2, 0 elsewhere (neutral at C4)")
+    ap.add_argument("--mg-one-cu", type=int, default=None,
+                    help="1: a native one-rank 2-D solve of at most 16384 points runs all its cycles and the "
+                         "convergence test in one workgroup (multigrid:oneCU, pinc_hip_mg_solve_small; with "
+                         "--mg-spectral-coarse the level-1 correction by the f64 matrix cores); default 1 for C2")
     ap.add_argument("--mg-spectral-coarse", type=int, default=1,
                     help="1: native multigrid solves level 1's correction exactly by FFT (multigrid:spectralCoarse) "
                          "instead of recursing to the coarser levels")
@@ -392,15 +396,22 @@ def main() -> int:
         raise SystemExit("grid size must divide by the GPU count")
     if args.mg_graph is None:
         args.mg_graph = 1 if c2 else 0
+    if args.mg_one_cu is None:
+        args.mg_one_cu = 1 if c2 else 0
     cfg = configs.bench_config(args.workload, S, args.ppc, world, mg=args.mg, mg_shard=args.mg_shard,
                                mg_extrapolate=args.mg_extrapolate, mg_spectral_coarse=args.mg_spectral_coarse,
-                               mg_graph=args.mg_graph, obj_capacitance=args.obj_capacitance,
+                               mg_graph=args.mg_graph, mg_one_cu=args.mg_one_cu,
+                               obj_capacitance=args.obj_capacitance,
                                obj_second_guess=args.obj_second_guess, c5_fused=args.c5_fused, layout=args.layout,
                                sort_interval=args.sort_interval, sort_in_push=args.sort_in_push,
                                sort_fraction=args.sort_fraction, sort_max=args.sort_max,
                                sort_spread=args.sort_spread,
                                mg_smooth=args.mg_smooth if args.mg == "native" and args.mg_smooth != "ini" else None)
     nspecies = int(cfg["population"]["nSpecies"])
+    # the one-workgroup solve applies (pinc_mg.c small_eligible): native, one
+    # rank, 2-D, at most 16384 points
+    one_cu = (args.mg == "native" and args.mg_one_cu == 1 and world == 1 and nd == 2 and S * S <= 16384
+              and S & (S - 1) == 0)
     ini = configs.write_ini(cfg)
     spread_note = (f" and the blocks' mean cell box grew {args.sort_spread:g}x since the last sort"
                    if args.sort_spread > 0 else "")
@@ -503,7 +514,12 @@ def main() -> int:
                       "achieved_GBs": p["mean_bytes"] / (p["mean_ms"] * 1e-3) / 1e9}
             continue
         gbs = p["mean_bytes"] / (p["mean_ms"] * 1e-3) / 1e9
-        kernels[k] = {"rocprof_name": ROCPROF_NAMES[k], "mean_launch_ms": p["mean_ms"],
+        rname = ROCPROF_NAMES[k]
+        if k == "mg_cycle" and one_cu:
+            rname = "k_mg_solve_small2<*> (every cycle of a solve and its convergence test, one launch)"
+        elif nd == 2:
+            rname = re.sub(r"<3,[^>]*>", "<2, *>", rname)
+        kernels[k] = {"rocprof_name": rname, "mean_launch_ms": p["mean_ms"],
                       "bytes_per_launch": p["mean_bytes"], "achieved_GBs": gbs, "frac": gbs / HBM_PEAK_GBS,
                       "launches": p["launches"], "samples": p["samples"],
                       "est_ms_per_step": p["mean_ms"] * p["launches"] / args.steps}
@@ -568,8 +584,12 @@ def main() -> int:
                                + ("the exact discrete response to the correction charge (rocFFT)"
                                   if args.obj_second_guess == "spectral" else "the last correction response")
                                if c5 else "; initial guess 2 phi_n - phi_(n-1)") if args.mg_extrapolate else "")
-                           + ("; two-grid: the level-1 correction solved exactly by rocFFT with the 7-point symbol"
+                           + (("; two-grid: the level-1 correction solved exactly "
+                               + ("in LDS through the real Fourier basis on the f64 matrix cores" if one_cu else
+                                  "by rocFFT") + " with the 7-point symbol")
                               if args.mg_spectral_coarse else "")
+                           + ("; every cycle of a solve and its convergence test in one workgroup "
+                              "(multigrid:oneCU, k_mg_solve_small2)" if one_cu else "")
                            + "; RMS residual <= 1e-10 as the reference)"
                            if args.mg == "native" else "reference algorithm (parity mode)")
                         + (f", level 0 sharded over the slabs ({mg_halo} halo planes per side), levels >= 1 "

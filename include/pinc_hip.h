@@ -373,6 +373,21 @@ int pinc_hip_gs_sweep2x(const double *phiIn, double *phiOut, const double *rho, 
  * at zero and is written to `phi`; rho of the levels below is the restricted
  * residual times 4.  hw3d / gs3d select mgHalfRestrict3D / mgGS3D's forms
  * (3-D only), else the ND forms. */
+/* Native mode, one rank, a 2-D level 0 of T0 x T1 <= 16384 points (T0 a
+ * power of two, T1 even, T0 T1 a multiple of 2048; mgGSND form, the ND
+ * restriction), levels 1.. within k_mg_coarse's LDS budget: whole V-cycles
+ * of levels[0..nLevels) from phi (initial guess, in/out) with rho, in one
+ * workgroup, until the RMS residual is <= tol or maxCycles ran; res (T0 T1
+ * doubles) is scratch.  out[0] = cycles, out[1] = the last RMS residual,
+ * out[2 + c] = the residual after cycle c (c < 60).  coarseBasis NULL: the
+ * V-cycle of the per-level launches (k_mg_coarse for levels 1..);
+ * otherwise the two-grid cycle of multigrid:spectralCoarse with level 1
+ * (square, n = 16..64 in 16s) solved exactly: coarseBasis holds the real
+ * orthonormal Fourier basis Q (n x n, row-major, Q[j][k]) and then the n
+ * eigenvalues 2 - 2 cos(2 pi f_k / n) of its columns. */
+int pinc_hip_mg_solve_small(double *phi, const double *rho, double *res, int nLevels, const pinc_lvl_t *levels,
+                            int nPre, int nPost, int nCoarse, int maxCycles, double tol, const double *coarseBasis,
+                            double *out, void *stream);
 int pinc_hip_mg_coarse(const double *rho, double *phi, int nLevels, const pinc_lvl_t *levels, int nPre,
                        int nPost, int nCoarse, int hw3d, int gs3d, void *stream);
 /* Sharded level 0 of the native multigrid (several ranks, 3-D): this rank's

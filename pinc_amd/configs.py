@@ -156,7 +156,8 @@ def config(name: str, **kw) -> dict:
 
 def bench_config(workload: str = "c4", size: int | None = None, ppc: int | None = None, world: int = 1, *,
                  mg: str = "native", mg_shard: str = "auto", mg_extrapolate: int = 1, mg_spectral_coarse: int = 1,
-                 mg_graph: int | None = None, obj_capacitance: str = "solve", obj_second_guess: str = "spectral",
+                 mg_graph: int | None = None, mg_one_cu: int | None = None, obj_capacitance: str = "solve",
+                 obj_second_guess: str = "spectral",
                  c5_fused: int = 1, layout: str = "tiled", sort_interval: int = 8, sort_in_push: int = 1,
                  sort_fraction: float = 0.8, sort_max: int = 32, sort_spread: float = 0.0,
                  mg_smooth: str | None = "4,4") -> dict:
@@ -187,6 +188,8 @@ def bench_config(workload: str = "c4", size: int | None = None, ppc: int | None 
         cfg["multigrid"]["extrapolate"] = str(mg_extrapolate)
         cfg["multigrid"]["spectralCoarse"] = str(mg_spectral_coarse)
         cfg["multigrid"]["graph"] = str(mg_graph if mg_graph is not None else int(c2))
+        # the whole solve in one workgroup where it fits (C2's 128^2)
+        cfg["multigrid"]["oneCU"] = str(mg_one_cu if mg_one_cu is not None else int(c2))
         if mg_smooth:
             # native mode's own smoothing counts "pre,post" (None: the ini's
             # 10/10): the same discrete problem to the same 1e-10 RMS

@@ -1245,20 +1245,11 @@ __device__ __forceinline__ CLevel clevel(const CoarseArgs &a, double *lds, int l
 	return c;
 }
 
+// the V-cycle of the LDS levels: level 0 of the block holds rho (and phi = 0)
+// on entry and the correction on return (k_mg_coarse, k_mg_solve_small)
 template <int ND>
-__global__ __launch_bounds__(1024) void k_mg_coarse(const double *__restrict__ rhoIn,
-                                                    double *__restrict__ phiOut, CoarseArgs a) {
-	__shared__ double lds[kCoarseLds];
-	__shared__ double wred[16];
+__device__ void coarse_body(const CoarseArgs &a, double *lds, double *wred) {
 	const bool gs3d = a.gs3d;
-	{
-		CLevel t = clevel<ND>(a, lds, 0);
-		for (long g = threadIdx.x; g < t.N; g += blockDim.x) {
-			t.rho[g] = rhoIn[g];
-			t.phi[g] = 0.0;
-		}
-	}
-	__syncthreads();
 	const int B = a.nLevels - 1;
 	for (int l = 0; l < B; l++) {
 		CLevel f = clevel<ND>(a, lds, l), c = clevel<ND>(a, lds, l + 1);
@@ -1317,8 +1308,380 @@ __global__ __launch_bounds__(1024) void k_mg_coarse(const double *__restrict__ r
 		blk_smooth<ND>(f.phi, f.rho, f.L, a.nPost, gs3d);
 		blk_neutralize(f.phi, f.N, wred);
 	}
+}
+
+template <int ND>
+__global__ __launch_bounds__(1024) void k_mg_coarse(const double *__restrict__ rhoIn,
+                                                    double *__restrict__ phiOut, CoarseArgs a) {
+	__shared__ double lds[kCoarseLds];
+	__shared__ double wred[16];
+	{
+		CLevel t = clevel<ND>(a, lds, 0);
+		for (long g = threadIdx.x; g < t.N; g += blockDim.x) {
+			t.rho[g] = rhoIn[g];
+			t.phi[g] = 0.0;
+		}
+	}
+	__syncthreads();
+	coarse_body<ND>(a, lds, wred);
 	CLevel t = clevel<ND>(a, lds, 0);
 	for (long g = threadIdx.x; g < t.N; g += blockDim.x) phiOut[g] = t.phi[g];
+}
+
+// ------------------------------------------ a whole small solve in one CU ---
+// Native mode, one rank, a 2-D level 0 of at most kSmallMax points (x extent
+// a power of two; C2's 128^2): every cycle of a solve, and the convergence
+// test, in one 1024-thread workgroup.  Each thread owns fixed level-0 points
+// of alternating colours and keeps their rho in registers; phi lives in LDS
+// (colour-major) while it is smoothed, then goes through memory (phi, its own
+// buffer; the residual through res) while the LDS holds the coarse solve:
+// the V-cycle of levels 1.. (coarse_body), or with multigrid:spectralCoarse
+// level 1 solved exactly (below).  The operators and their expression order
+// are those of the multi-launch path (k_gs_pass with no shift = blk_update;
+// residual_at; k_restrict x 4; prol_low), so in the V-cycle form phi is
+// bit-identical to it for the same number of cycles; only the order of the
+// norm's sum differs.  This replaces the ~25 launches of each cycle (4-5 us
+// each at 128^2) and the host's norm read per cycle by one launch and one
+// read per solve.
+constexpr int kSmallMax = 16384;
+constexpr int kSmallPer = kSmallMax / 1024;
+static_assert(kSmallMax <= kCoarseLds, "level 0 in the coarse LDS block");
+
+// multigrid:spectralCoarse in the same workgroup: the level-1 correction
+// equation -L phi1 = rho1 on a square n x n level 1 (n a multiple of 16, at
+// most 64) solved exactly in LDS through the real orthonormal Fourier basis Q
+// of the periodic second difference (columns: DC, cos k, Nyquist, sin k;
+// eigenvalue 2 - 2 cos(2 pi k / n) per dimension, DC dropped) -- phi1 =
+// Q ((Q^T rho1 Q) / (lam_y + lam_x)) Q^T, four n^3 products on the f64
+// matrix cores (v_mfma_f64_16x16x4_f64, one 16 x 16 output tile per wave).
+// The same discrete problem as the rocFFT path's (k_spectral_scale's
+// symbol), in another rounding.  Matrices in LDS with rows padded to n + 1
+// doubles (the operand reads of 16 lanes down a column spread over the
+// banks).
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+// one 16 x 16 tile (rows i0.., columns j0..) of op(A) op(B), K the inner
+// extent; lane l returns D[i0 + (l >> 4) + 4 r][j0 + (l & 15)] in element r
+template <bool TA, bool TB>
+__device__ __forceinline__ f64x4 mm_tile(const double *A, const double *B, int ld, int i0, int j0, int K, int tid) {
+	const int lane = tid & 63;
+	const int ii = i0 + (lane & 15), jj = j0 + (lane & 15), kl = lane >> 4;
+	f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+	for (int k0 = 0; k0 < K; k0 += 4) {
+		const int kk = k0 + kl;
+		const double x = TA ? A[kk * ld + ii] : A[ii * ld + kk];
+		const double y = TB ? B[jj * ld + kk] : B[kk * ld + jj];
+		acc = __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, acc, 0, 0, 0);
+		// at most 8 operand reads (16 VGPRs) ahead
+		if ((k0 & 12) == 12) __builtin_amdgcn_sched_barrier(0);
+	}
+	return acc;
+}
+
+// D = op(A) op(B) (n x n, ld = n + 1) by the workgroup's waves, a tile per
+// wave (tid = threadIdx.x, passed in so the caller controls its hoisting);
+// scaled by 1 / (lam[row] + lam[col]) (0 at DC) when lam (LDS) is given
+template <bool TA, bool TB>
+__device__ __forceinline__ void mm_block(const double *A, const double *B, double *D, int n, const double *lam,
+                                         int tid) {
+	const int ld = n + 1, nt = n >> 4, w = tid >> 6, lane = tid & 63;
+	if (w < nt * nt) {
+		const int i0 = (w / nt) << 4, j0 = (w % nt) << 4;
+		const f64x4 acc = mm_tile<TA, TB>(A, B, ld, i0, j0, n, tid);
+		const int col = j0 + (lane & 15);
+#pragma unroll
+		for (int r = 0; r < 4; r++) {
+			const int row = i0 + (lane >> 4) + 4 * r;
+			double v = acc[r];
+			if (lam) v = (row == 0 && col == 0) ? 0.0 : v * (1.0 / (lam[row] + lam[col]));
+			D[row * ld + col] = v;
+		}
+	}
+	__syncthreads();
+}
+
+struct SmallArgs {
+	CoarseArgs c;      // levels 1 .. of the solve (c.T[0] = level 1)
+	int T0[2];         // level 0 (2-D)
+	int lgH;           // log2 of T0 / 2
+	int nPre, nPost;   // level-0 smoothing
+	int maxCycles;     // stop (with the history) after this many cycles
+	double tol;        // stop once the RMS residual is <= tol (or not finite)
+};
+
+#ifndef PINC_SMALL_DIAG
+#define PINC_SMALL_DIAG 0  // 1: the first cycle's phase times (100 MHz ticks) in out[2..] instead of the history
+#endif
+
+// (phi and res not __restrict__: other waves of the workgroup read what a
+// wave wrote before a barrier)
+template <bool SPEC, int P>
+__global__ __launch_bounds__(1024) void k_mg_solve_small2(double *phi, const double *__restrict__ rho, double *res,
+                                                          SmallArgs a, double *__restrict__ out,
+                                                          const double *__restrict__ basis) {
+	static_assert(P % 2 == 0 && P <= kSmallPer, "slots per thread");
+	constexpr int ND = 2;
+	__shared__ double lds[kCoarseLds];
+	__shared__ double wred[16];
+	pinc_lvl_t l0;
+	l0.nd = ND;
+	l0.T[0] = a.T0[0];
+	l0.T[1] = a.T0[1];
+	l0.T[2] = 1;
+	const Lv L = make_lv(l0);
+	const int T0 = a.T0[0], T1 = a.T0[1], N0 = T0 * T1, NH = N0 >> 1, H = T0 >> 1;
+	const int t = threadIdx.x;
+	// slot j of this thread: colour c = j & 1, pair q = t + 1024 k (k = j >> 1)
+	// of that colour: row y = q / H, x = 2 (q % H) + ((c + y) & 1).  In LDS
+	// level 0 is colour-major, point (x, y) of colour c at c NH + y H + x / 2,
+	// so a wave's updates and their neighbour reads are unit-stride.  With H
+	// dividing 512 the column q % H = t % H and the x parity do not depend on
+	// k, and slot k sits 1024 k above slot 0 in both colour arrays (2048 k in
+	// level 0's memory): per colour a handful of per-thread bases, the rest
+	// compile-time offsets (no address arithmetic per update but the y wrap)
+	const int R = 1024 >> a.lgH;  // rows per slot pair
+	// the per-colour bases, recomputed from the thread index at the top of
+	// each phase (refresh: the index through an empty asm), so that neither
+	// they nor the slots' addresses (5 per slot) stay live across the cycle
+	// loop -- only rho's registers do
+	int tid = t;
+	int y0, xc[2], own[2], xpI[2], xmI[2], ob[2], g0[2];
+	auto refresh = [&]() {
+		asm volatile("" : "+v"(tid));
+		const int i0 = tid & (H - 1);
+		y0 = tid >> a.lgH;
+#pragma unroll
+		for (int c = 0; c < 2; c++) {
+			const int x = 2 * i0 + ((c + y0) & 1);
+			const int row = (1 - c) * NH + y0 * H;  // row y0 of the other colour
+			xc[c] = x;
+			own[c] = c * NH + tid;
+			xpI[c] = row + (x + 1 < T0 ? (x + 1) >> 1 : 0);
+			xmI[c] = row + (x > 0 ? (x - 1) >> 1 : (T0 - 1) >> 1);
+			ob[c] = row + (x >> 1);
+			g0[c] = x + y0 * T0;
+		}
+	};
+	refresh();
+	struct Slot {
+		int g, li, x, y;
+	};
+	auto slot = [&](int j) -> Slot {
+		const int c = j & 1, k = j >> 1;
+		Slot r;
+		r.x = xc[c];
+		r.y = y0 + k * R;
+		r.g = g0[c] + 2048 * k;
+		r.li = own[c] + 1024 * k;
+		return r;
+	};
+	// the four neighbours' LDS indices (other colour): x+1, x-1, y+1, y-1
+	auto nbr = [&](const Slot &p, int j, int *o) {
+		const int c = j & 1, k = j >> 1;
+		const int b = ob[c] + 1024 * k;
+		o[0] = xpI[c] + 1024 * k;
+		o[1] = xmI[c] + 1024 * k;
+		o[2] = p.y + 1 < T1 ? b + H : b - p.y * H;
+		o[3] = p.y > 0 ? b - H : b + (T1 - 1) * H;
+	};
+	auto stamp = [&](int k) {
+		if (PINC_SMALL_DIAG && t == 0) out[2 + k] = (double)wall_clock64();
+	};
+#pragma unroll
+	for (int j = 0; j < P; j++) {
+		const Slot p = slot(j);
+		lds[p.li] = phi[p.g];
+		if (j & 1) __builtin_amdgcn_sched_barrier(0);  // 2 slots per batch
+	}
+	__syncthreads();
+	// r of slot j from the phi in LDS (residual_at's expression)
+	auto resid = [&](int j, double rj) {
+		const Slot p = slot(j);
+		int o[4];
+		nbr(p, j, o);
+		double r = -(2. * ND) * lds[p.li];
+		r += lds[o[0]] + lds[o[1]];
+		r += lds[o[2]] + lds[o[3]];
+		return r + rj;
+	};
+	// nIter red-black iterations (blk_update's expression: (x+ + x-) +
+	// (y+ + y-), + rho, / 4).  The thread's rho is loaded into registers at
+	// the start and dies at the end, so the other phases have the whole
+	// register budget.
+	auto smooth0 = [&](int nIter) {
+		refresh();
+		double rr[P];
+#pragma unroll
+		for (int j = 0; j < P; j++) rr[j] = rho[slot(j).g];
+		for (int it = 0; it < nIter; it++) {
+			for (int pass = 0; pass < 2; pass++) {
+				refresh();
+				// every read of the pass before its first write (the slots
+				// of one colour read only the other colour): the LDS reads
+				// of the thread's updates in flight together, 16 at a time
+				double v[P / 2];
+#pragma unroll
+				for (int k = 0; k < P / 2; k++) {
+					const int j = 2 * k + pass;
+					const Slot p = slot(j);
+					int o[4];
+					nbr(p, j, o);
+					v[k] = 0;
+					v[k] += lds[o[0]] + lds[o[1]];
+					v[k] += lds[o[2]] + lds[o[3]];
+					if ((k & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+				}
+#pragma unroll
+				for (int k = 0; k < P / 2; k++) {
+					const int j = 2 * k + pass;
+					const Slot p = slot(j);
+					double w = v[k] + rr[j];
+					w *= 1. / (2 * ND);
+					lds[p.li] = w;
+				}
+				__syncthreads();
+			}
+		}
+	};
+	// the residuals in a rolled loop over slot pairs, rho from memory (the
+	// residual's reads of every slot unrolled at once need more registers
+	// than the workgroup size allows at 16 slots): tail = 1 stores them and
+	// phi to memory (the restriction's input), tail = 2 returns the sum of
+	// their squares
+	auto residuals = [&](int tail) -> double {
+		double s2 = 0;
+		refresh();
+#pragma unroll 1
+		for (int k = 0; k < P / 2; k++) {
+#pragma unroll
+			for (int c = 0; c < 2; c++) {
+				const int j = 2 * k + c;
+				const Slot p = slot(j);
+				const double r = resid(j, rho[p.g]);
+				if (tail == 1) {
+					res[p.g] = r;
+					phi[p.g] = lds[p.li];
+				} else {
+					s2 += r * r;
+				}
+			}
+		}
+		return s2;
+	};
+	const CLevel c1 = clevel<ND>(a.c, lds, 0);
+	int cyc = 0;
+	double bar = 0;
+	for (;;) {
+		if (cyc == 0) stamp(0);
+		smooth0(a.nPre);
+		if (cyc == 0) stamp(1);
+		// the residual and phi of the own points to memory
+		residuals(1);
+		__syncthreads();
+		if (cyc == 0) stamp(2);
+		if constexpr (SPEC) {
+			// the restricted residual (x 4) into R, Q beside it, then the
+			// exact level-1 solve; phi1 ends in R
+			const int n = c1.L.T[0], ld = n + 1;
+			double *R = lds, *Tm = lds + n * ld, *Qs = lds + 2 * n * ld;
+			refresh();
+			for (int e = tid; e < n * n + n; e += 1024)  // Q, then lambda after its n padded rows
+				Qs[e < n * n ? (e / n) * ld + e % n : n * ld + e - n * n] = basis[e];
+			for (int gc = tid; gc < n * n; gc += 1024) {
+				int cf[3] = {2 * (gc % n), 2 * (gc / n), 0};
+				const long gf = cf[0] + (long)cf[1] * L.s[1];
+				double v = (2. * ND) * res[gf];
+#pragma unroll
+				for (int d = 0; d < ND; d++) v += res[gf + nb_up(L, cf, d)] + res[gf + nb_dn(L, cf, d)];
+				v *= 1. / (ND * 4);
+				R[(gc / n) * ld + gc % n] = v * 4.0;
+			}
+			__syncthreads();
+			if (cyc == 0) stamp(3);
+			refresh();
+			const double *lam = Qs + n * ld;
+			mm_block<false, false>(R, Qs, Tm, n, nullptr, tid);  // R Q
+			mm_block<true, false>(Qs, Tm, R, n, lam, tid);       // Q^T (R Q), / lambda
+			mm_block<false, true>(R, Qs, Tm, n, nullptr, tid);   // . Q^T
+			mm_block<false, false>(Qs, Tm, R, n, nullptr, tid);  // Q (.)
+			if (cyc == 0) stamp(4);
+			Lv C = c1.L;
+			C.s[1] = ld;
+			refresh();
+#pragma unroll
+			for (int j = 0; j < P; j++) {
+				const Slot p = slot(j);
+				int c[3] = {p.x, p.y, 0};
+				phi[p.g] = phi[p.g] + prol_low<ND, 0>(R, C, c);
+				if (j & 1) __builtin_amdgcn_sched_barrier(0);
+			}
+		} else {
+			// restriction (k_mg_coarse's expression, x 4) into the coarse block
+			refresh();
+			for (int gc = tid; gc < c1.N; gc += 1024) {
+				int cc[3], cf[3] = {0, 0, 0};
+				blk_coords(c1.L, gc, cc);
+				long gf = 0;
+#pragma unroll
+				for (int d = 0; d < ND; d++) {
+					cf[d] = 2 * cc[d];
+					gf += (long)cf[d] * L.s[d];
+				}
+				double v = (2. * ND) * res[gf];
+#pragma unroll
+				for (int d = 0; d < ND; d++) v += res[gf + nb_up(L, cf, d)] + res[gf + nb_dn(L, cf, d)];
+				v *= 1. / (ND * 4);
+				c1.rho[gc] = v * 4.0;
+				c1.phi[gc] = 0.0;
+			}
+			__syncthreads();
+			if (cyc == 0) stamp(3);
+			coarse_body<ND>(a.c, lds, wred);
+			if (cyc == 0) stamp(4);
+			// phi += prolongated level-1 correction, through memory
+			refresh();
+#pragma unroll
+			for (int j = 0; j < P; j++) {
+				const Slot p = slot(j);
+				int c[3] = {p.x, p.y, 0};
+				phi[p.g] = phi[p.g] + prol_low<ND, 0>(c1.phi, c1.L, c);
+				if (j & 1) __builtin_amdgcn_sched_barrier(0);
+			}
+		}
+		__syncthreads();
+		if (cyc == 0) stamp(5);
+		refresh();
+#pragma unroll
+		for (int j = 0; j < P; j++) {
+			const Slot p = slot(j);
+			lds[p.li] = phi[p.g];
+			if (j & 1) __builtin_amdgcn_sched_barrier(0);
+		}
+		__syncthreads();
+		if (cyc == 0) stamp(6);
+		smooth0(a.nPost);
+		if (cyc == 0) stamp(7);
+		// the RMS residual of the cycle
+		const double s2 = residuals(2);
+		// mgSolve's test: sqrt(sum / N0) > tol continues (a NaN or an
+		// infinity stops, for the host to report)
+		bar = sqrt(blk_sum(s2, wred) / (double)N0);
+		if (cyc == 0) stamp(8);
+		if (!PINC_SMALL_DIAG && t == 0 && cyc < 60) out[2 + cyc] = bar;
+		cyc++;
+		if (!(bar > a.tol) || isinf(bar) || cyc >= a.maxCycles) break;
+	}
+	refresh();
+#pragma unroll
+	for (int j = 0; j < P; j++) {
+		const Slot p = slot(j);
+		phi[p.g] = lds[p.li];
+		if (j & 1) __builtin_amdgcn_sched_barrier(0);
+	}
+	if (t == 0) {
+		out[0] = (double)cyc;
+		out[1] = bar;
+	}
 }
 
 // ----------------------------------------------- sharded level 0 (z-slabs) ---
@@ -1758,6 +2121,67 @@ extern "C" int pinc_hip_gs_sweep2x(const double *phiIn, double *phiOut, const do
 	                   zp);
 #endif
 	return check_launch("gs_sweep2x");
+}
+
+extern "C" int pinc_hip_mg_solve_small(double *phi, const double *rho, double *res, int nLevels,
+                                       const pinc_lvl_t *levels, int nPre, int nPost, int nCoarse, int maxCycles,
+                                       double tol, const double *coarseBasis, double *out, void *stream) {
+	if (nLevels < 2 || nLevels > 13) return set_error(hipErrorInvalidValue, "mg_solve_small: 2..13 levels");
+	if (levels[0].nd != 2) return set_error(hipErrorInvalidValue, "mg_solve_small: 2-D levels");
+	const int T0 = levels[0].T[0], T1 = levels[0].T[1];
+	int lg = 0;
+	while ((1 << lg) < T0) lg++;
+	if ((1 << lg) != T0 || T0 < 2 || T0 > 1024 || T1 % 2 || (long)T0 * T1 > kSmallMax || ((long)T0 * T1) % 2048)
+		return set_error(hipErrorInvalidValue,
+		                 "mg_solve_small: level 0 not T0 = 2^k <= 1024, T1 even, T0 T1 <= 16384 in 2048s");
+	if (maxCycles < 1 || maxCycles > 1000000) return set_error(hipErrorInvalidValue, "mg_solve_small: maxCycles");
+	SmallArgs a;
+	long tot = 0;
+	a.c.nLevels = nLevels - 1;
+	for (int l = 1; l < nLevels; l++) {
+		if (levels[l].nd != 2) return set_error(hipErrorInvalidValue, "mg_solve_small: mixed dimensions");
+		long n = 1;
+		for (int d = 0; d < 3; d++) {
+			if (d < 2 && 2 * levels[l].T[d] != levels[l - 1].T[d])
+				return set_error(hipErrorInvalidValue, "mg_solve_small: levels must halve");
+			a.c.T[l - 1][d] = levels[l].T[d];
+			n *= levels[l].T[d];
+		}
+		tot += 3 * n;
+	}
+	if (tot > kCoarseLds) return set_error(hipErrorInvalidValue, "mg_solve_small: levels exceed the LDS budget");
+	a.c.nPre = nPre;
+	a.c.nPost = nPost;
+	a.c.nCoarse = nCoarse;
+	a.c.hw3d = 0;
+	a.c.gs3d = 0;
+	a.T0[0] = T0;
+	a.T0[1] = T1;
+	a.lgH = lg - 1;
+	a.nPre = nPre;
+	a.nPost = nPost;
+	a.maxCycles = maxCycles;
+	a.tol = tol;
+	if (coarseBasis) {
+		const int n = levels[1].T[0];
+		if (levels[1].T[1] != n || n % 16 || n > 64 || 3 * n * (n + 1) + n > kCoarseLds)
+			return set_error(hipErrorInvalidValue, "mg_solve_small: the spectral level 1 must be square, n = 16, 32, 48, 64");
+	}
+	// one instance per slot count (compile-time: unrolled slot loops with
+	// the thread's rho in fixed registers)
+	const int P = (T0 * T1) >> 10;
+	if (P != 2 && P != 4 && P != 8 && P != 16)
+		return set_error(hipErrorInvalidValue, "mg_solve_small: level 0 of 2048, 4096, 8192 or 16384 points");
+	auto kern = coarseBasis ? (P == 2 ? k_mg_solve_small2<true, 2>
+	                           : P == 4 ? k_mg_solve_small2<true, 4>
+	                           : P == 8 ? k_mg_solve_small2<true, 8>
+	                                    : k_mg_solve_small2<true, 16>)
+	                        : (P == 2 ? k_mg_solve_small2<false, 2>
+	                           : P == 4 ? k_mg_solve_small2<false, 4>
+	                           : P == 8 ? k_mg_solve_small2<false, 8>
+	                                    : k_mg_solve_small2<false, 16>);
+	hipLaunchKernelGGL(kern, dim3(1), dim3(1024), 0, (hipStream_t)stream, phi, rho, res, a, out, coarseBasis);
+	return check_launch("mg_solve_small");
 }
 
 extern "C" int pinc_hip_mg_coarse(const double *rho, double *phi, int nLevels, const pinc_lvl_t *levels, int nPre,

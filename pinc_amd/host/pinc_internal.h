@@ -311,6 +311,13 @@ struct MultigridSolver {
 	long lastCycles[4];
 	double *hostNorm;
 	void *normEvent;
+	/* a small 2-D solve on one rank runs its V-cycles and the convergence
+	 * test in one workgroup (pinc_hip_mg_solve_small): the cycle count, the
+	 * last residual and the history come back in one read (smallOut, pinned
+	 * hostSmall) per launch */
+	int small;
+	double *smallOut, *hostSmall;
+	double *smallBasis; /* with multigrid:spectralCoarse: level 1's Fourier basis and eigenvalues */
 };
 
 /* collectives over RCCL or the host transport (pinc_comm.c) */

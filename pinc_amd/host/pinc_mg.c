@@ -105,6 +105,88 @@ static void shard_setup(MultigridSolver *S, const dictionary *ini, const Grid *r
 	S->useGraph = 0; /* the halo exchanges are host-driven */
 }
 
+enum { kSmallOut = 64, kSmallHist = 60, kSmallChunk = 1000 };
+
+/* native mode, one rank, a 2-D level 0 of at most 16384 points (a multiple
+ * of 2048) with a power-of-two x extent, its levels 1.. within the one-workgroup
+ * coarse solve's LDS budget: the whole solve in one launch per solve
+ * (pinc_hip_mg_solve_small).  multigrid:oneCU (default 0) or PINC_MG_SMALL
+ * (experiments) turn it on; it replaces multigrid:spectralCoarse. */
+static int small_eligible(const MultigridSolver *S, const dictionary *ini) {
+	int want = iniHas(ini, "multigrid:oneCU") && iniGetInt(ini, "multigrid:oneCU");
+	if (getenv("PINC_MG_SMALL")) want = atoi(getenv("PINC_MG_SMALL"));
+	if (!want || !S->native || S->shard || g_pinc.nranks != 1 || S->nLevels < 2) return 0;
+	const pinc_lvl_t L = S->L[0];
+	const long n0 = (long)L.T[0] * L.T[1];
+	if (L.nd != 2 || (L.T[0] & (L.T[0] - 1)) || L.T[0] < 2 || L.T[1] % 2 || n0 > 16384 || n0 % 2048) return 0;
+	long tot = 0;
+	for (int q = 1; q < S->nLevels; q++) tot += 3 * S->N[q];
+	return tot <= 5500 * 3 && S->nLevels - 1 <= 12;
+}
+
+/* level 1's real orthonormal Fourier basis for the workgroup's exact
+ * coarse solve (pinc_hip_mg_solve_small): Q[j][k] = DC 1/sqrt(n) (k = 0),
+ * sqrt(2/n) cos(2 pi j k / n) (0 < k < n/2), Nyquist (-1)^j / sqrt(n)
+ * (k = n/2), sqrt(2/n) sin(2 pi j (k - n/2) / n) (k > n/2); then the
+ * eigenvalue 2 - 2 cos(2 pi f / n) of each column (k_spectral_scale's
+ * symbol, per dimension) */
+static void small_basis(MultigridSolver *S, int n) {
+	double *h = malloc((size_t)(n * n + n) * sizeof(double));
+	const int hn = n / 2;
+	for (int j = 0; j < n; j++)
+		for (int k = 0; k < n; k++) {
+			double v;
+			if (k == 0) v = 1.0 / sqrt((double)n);
+			else if (k < hn) v = sqrt(2.0 / n) * cos(2 * M_PI * (double)((long)j * k % n) / n);
+			else if (k == hn) v = (j & 1 ? -1.0 : 1.0) / sqrt((double)n);
+			else v = sqrt(2.0 / n) * sin(2 * M_PI * (double)((long)j * (k - hn) % n) / n);
+			h[j * n + k] = v;
+		}
+	for (int k = 0; k < n; k++) {
+		const int f = k <= hn ? k : k - hn;
+		h[n * n + k] = 2.0 - 2.0 * cos(2 * M_PI * f / n);
+	}
+	pinc_check(pinc_hip_malloc((void **)&S->smallBasis, (size_t)(n * n + n) * sizeof(double)), "mg small basis");
+	pinc_check(pinc_hip_h2d(S->smallBasis, h, (size_t)(n * n + n) * sizeof(double), g_pinc.stream), "mg small basis");
+	pinc_check(pinc_hip_stream_sync(g_pinc.stream), "mg small basis");
+	free(h);
+}
+
+/* the V-cycles of one solve in launches of at most kSmallChunk cycles (at
+ * most kSmallHist when a history is kept), until the RMS residual is at most
+ * 1e-10 as mgSolve's loop; returns the cycles run */
+static long small_solve(MultigridSolver *S, long cap, double *lastRes) {
+	long c = 0;
+	double barRes = 2.;
+	for (;;) {
+		long chunk = S->histCap > 0 ? kSmallHist : kSmallChunk;
+		if (cap > 0 && cap - c < chunk) chunk = cap - c;
+		int slot = pinc_probe_begin(PINC_PROBE_CYCLE);
+		pinc_check(pinc_hip_mg_solve_small(S->phi[0], S->rho[0], S->res[0], S->nLevels, S->L, S->nPre, S->nPost,
+		                                   S->nCoarse, (int)chunk, 1.E-10, S->smallBasis, S->smallOut, g_pinc.stream),
+		           "mg small solve");
+		pinc_probe_end(PINC_PROBE_CYCLE, slot, 0.0);
+		pinc_check(pinc_hip_d2h(S->hostSmall, S->smallOut, kSmallOut * sizeof(double), g_pinc.stream), "mg small solve");
+		const long n = (long)S->hostSmall[0];
+		barRes = S->hostSmall[1];
+		for (long k = 0; k < n; k++) {
+			if (S->histN < S->histCap) S->hist[S->histN] = k < kSmallHist ? S->hostSmall[2 + k] : NAN;
+			S->histN++;
+			if (g_pinc.verbose && ((c + k + 1) % g_pinc.verbose == 0) && k < kSmallHist) {
+				fprintf(stderr, "[pinc] rank %d solve cycle %ld residual %.3e\n", g_pinc.rank, c + k + 1,
+				        S->hostSmall[2 + k]);
+				fflush(stderr);
+			}
+		}
+		c += n;
+		S->cycles += n;
+		if (!(barRes > 1.E-10) || !isfinite(barRes) || (cap > 0 && c >= cap)) break;
+		if (c > 1000000) break;
+	}
+	*lastRes = barRes;
+	return c;
+}
+
 MultigridSolver *mgAllocSolver(const dictionary *ini, Grid *rho, Grid *phi) {
 	MultigridSolver *S = calloc(1, sizeof(*S));
 	int nd = rho->rank - 1;
@@ -230,7 +312,19 @@ MultigridSolver *mgAllocSolver(const dictionary *ini, Grid *rho, Grid *phi) {
 	 * wake-up path), with an event when speculating */
 	pinc_check(pinc_hip_host_alloc((void **)&S->hostNorm, sizeof(double)), "mg norm");
 	if (S->speculate) pinc_check(pinc_hip_event_create(&S->normEvent), "mg norm");
-	if (S->native && S->nLevels >= 2 && iniHas(ini, "multigrid:spectralCoarse") &&
+	S->small = small_eligible(S, ini);
+	if (S->small && iniHas(ini, "multigrid:spectralCoarse") && iniGetInt(ini, "multigrid:spectralCoarse")) {
+		/* the two-grid cycle in the workgroup: level 1 square, n = 16..64 in
+		 * 16s (otherwise the per-level launches with rocFFT) */
+		const int n = S->L[1].T[0];
+		if (S->L[1].T[1] == n && n % 16 == 0 && n <= 64) small_basis(S, n);
+		else S->small = 0;
+	}
+	if (S->small) {
+		pinc_check(pinc_hip_malloc((void **)&S->smallOut, kSmallOut * sizeof(double)), "mg small solve");
+		pinc_check(pinc_hip_host_alloc((void **)&S->hostSmall, kSmallOut * sizeof(double)), "mg small solve");
+	}
+	if (S->native && S->nLevels >= 2 && !S->small && iniHas(ini, "multigrid:spectralCoarse") &&
 	    iniGetInt(ini, "multigrid:spectralCoarse")) {
 		/* sharded level 0: level 1 stays decomposed when its slabs can be
 		 * transposed (y divisible by the rank count), as the reference keeps
@@ -291,6 +385,9 @@ void mgFreeSolver(MultigridSolver *S) {
 	pinc_hip_fft_slab_destroy(S->fftCoarseSlab);
 	pinc_hip_free(S->phi1Ext);
 	pinc_hip_host_free(S->hostNorm);
+	pinc_hip_free(S->smallOut);
+	pinc_hip_free(S->smallBasis);
+	pinc_hip_host_free(S->hostSmall);
 	if (S->normEvent) pinc_hip_event_destroy(S->normEvent);
 	free(S->hist);
 	for (int q = 0; q < S->nLevels; q++) {
@@ -689,6 +786,17 @@ void mgSolve(MultigridSolver *S, Grid *rho, Grid *phi, const MpiInfo *mpiInfo) {
 		long c = 0;
 		S->histN = 0;
 		if (S->native) neutralize_level(S, 0, S->rho[0]);
+		if (S->small) {
+			c = small_solve(S, cap, &barRes);
+			if (!(S->maxCycles && !isfinite(barRes)) && (!isfinite(barRes) || (c > maxCycles && barRes > 1.E-10)))
+				msg(ERROR, "multigrid did not converge (residual %g)", barRes);
+			if (!isfinite(barRes))
+				fprintf(stderr, "[pinc] rank %d solve stopped: residual %g after %ld cycles\n", g_pinc.rank, barRes, c);
+			else if (cap > 0 && c >= cap && barRes > 1.E-10)
+				fprintf(stderr, "[pinc] rank %d solve stopped at the PINC_MG_MAX_CYCLES cap (%ld), residual %.3e\n",
+				        g_pinc.rank, c, barRes);
+			barRes = 0; /* the loop below is the multi-launch form */
+		}
 		while (barRes > 1.E-10) {
 			if (S->useGraph) {
 				/* the V-cycle is a fixed launch sequence on fixed buffers:

@@ -201,3 +201,166 @@ def test_resid_restrict_equals_residual_then_restrict(hip, shape, hw3d):
     resn = (-6.0 * a + s) + r
     np.testing.assert_array_equal(res.cpu().numpy().reshape(tz, ty, tx), resn)
     np.testing.assert_allclose(tot.item(), float((resn * resn).sum()), rtol=1e-12)
+
+
+def _small_levels(tx, ty):
+    lv = []
+    while True:
+        lv.append((tx, ty))
+        if tx % 2 or ty % 2 or tx // 2 < 2 or ty // 2 < 2:
+            break
+        tx, ty = tx // 2, ty // 2
+    return lv
+
+
+def _small_solve(hip, phi, rho, lv, npre, npost, ncoarse, cycles, basis=None):
+    import torch
+    n = len(lv)
+    arr = (Lvl * n)(*[Lvl(2, (C.c_int * 3)(a, b, 1)) for a, b in lv])
+    res = torch.empty_like(phi)
+    out = torch.zeros(64, dtype=torch.float64, device="cuda")
+    rc = hip.pinc_hip_mg_solve_small(phi.data_ptr(), rho.data_ptr(), res.data_ptr(), n, arr, npre, npost, ncoarse,
+                                     cycles, 1e-10, None if basis is None else basis.data_ptr(), out.data_ptr(), None)
+    assert rc == 0
+    torch.cuda.synchronize()
+    return out.cpu().numpy()
+
+
+def _fourier_basis(n):
+    """The real orthonormal Fourier basis and its eigenvalues, as
+    pinc_mg.c's small_basis builds them (the launcher's coarseBasis)."""
+    hn = n // 2
+    j = np.arange(n)[:, None]
+    k = np.arange(n)[None, :]
+    Q = np.where(k == 0, 1 / np.sqrt(n),
+                 np.where(k < hn, np.sqrt(2 / n) * np.cos(2 * np.pi * (j * k % n) / n),
+                          np.where(k == hn, np.where(j % 2, -1.0, 1.0) / np.sqrt(n),
+                                   np.sqrt(2 / n) * np.sin(2 * np.pi * (j * (k - hn) % n) / n))))
+    f = np.where(np.arange(n) <= hn, np.arange(n), np.arange(n) - hn)
+    lam = 2.0 - 2.0 * np.cos(2 * np.pi * f / n)
+    return np.concatenate([Q.ravel(), lam])
+
+
+@pytest.mark.parametrize("shape", [(128, 128), (64, 32), (16, 128), (128, 64)])
+def test_small_solve_vcycle_equals_per_level_launches(hip, shape):
+    """pinc_hip_mg_solve_small without a basis: each cycle bit for bit the
+    per-level launches of the native V-cycle (k_gs_pass x 2 nPre, k_residual,
+    k_restrict, x 4, k_mg_coarse for levels 1.., k_prolong_add, k_gs_pass x
+    2 nPost), over three cycles; the history is the RMS residual after each
+    cycle (to 1e-12: another summation order)."""
+    import torch
+    vp = C.c_void_p
+    hip.pinc_hip_mg_solve_small.argtypes = [vp, vp, vp, C.c_int, vp, C.c_int, C.c_int, C.c_int, C.c_int,
+                                            C.c_double, vp, vp, vp]
+    hip.pinc_hip_residual.argtypes = [vp, vp, vp, Lvl, vp]
+    hip.pinc_hip_restrict.argtypes = [vp, vp, Lvl, C.c_int, vp]
+    hip.pinc_hip_scale.argtypes = [vp, C.c_long, C.c_double, vp]
+    hip.pinc_hip_mg_coarse.argtypes = [vp, vp, C.c_int, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp]
+    hip.pinc_hip_prolong_add.argtypes = [vp, vp, Lvl, vp]
+    tx, ty = shape
+    lv = _small_levels(tx, ty)
+    g = torch.Generator(device="cpu").manual_seed(3)
+    rho = torch.randn(tx * ty, dtype=torch.float64, generator=g)
+    rho -= rho.mean()
+    rho = rho.cuda()
+    phi0 = torch.randn(tx * ty, dtype=torch.float64, generator=g).cuda()
+    npre, npost, ncoarse = 4, 4, 10
+    phi = phi0.clone()
+    out = _small_solve(hip, phi, rho, lv, npre, npost, ncoarse, 3)
+    assert out[0] == 3
+    # the per-level launches
+    ref = phi0.clone()
+    L = [Lvl(2, (C.c_int * 3)(a, b, 1)) for a, b in lv]
+    arr = (Lvl * (len(lv) - 1))(*L[1:])
+    res = torch.empty_like(ref)
+    n1 = lv[1][0] * lv[1][1]
+    rho1 = torch.empty(n1, dtype=torch.float64, device="cuda")
+    phi1 = torch.empty(n1, dtype=torch.float64, device="cuda")
+    nb = C.c_int()
+    hist = []
+    for _ in range(3):
+        for _ in range(npre):
+            for p in (0, 1):
+                assert hip.pinc_hip_gs_pass(ref.data_ptr(), rho.data_ptr(), L[0], p, 0, None, None, C.byref(nb),
+                                            None) == 0
+        assert hip.pinc_hip_residual(res.data_ptr(), ref.data_ptr(), rho.data_ptr(), L[0], None) == 0
+        assert hip.pinc_hip_restrict(res.data_ptr(), rho1.data_ptr(), L[1], 0, None) == 0
+        assert hip.pinc_hip_scale(rho1.data_ptr(), n1, 4.0, None) == 0
+        assert hip.pinc_hip_mg_coarse(rho1.data_ptr(), phi1.data_ptr(), len(lv) - 1, arr, npre, npost, ncoarse, 0, 0,
+                                      None) == 0
+        assert hip.pinc_hip_prolong_add(ref.data_ptr(), phi1.data_ptr(), L[0], None) == 0
+        for _ in range(npost):
+            for p in (0, 1):
+                assert hip.pinc_hip_gs_pass(ref.data_ptr(), rho.data_ptr(), L[0], p, 0, None, None, C.byref(nb),
+                                            None) == 0
+        assert hip.pinc_hip_residual(res.data_ptr(), ref.data_ptr(), rho.data_ptr(), L[0], None) == 0
+        torch.cuda.synchronize()
+        hist.append(float(torch.sqrt(torch.sum(res * res) / (tx * ty))))
+    assert torch.equal(phi, ref)
+    np.testing.assert_allclose(out[2:5], hist, rtol=1e-12)
+
+
+@pytest.mark.parametrize("size", [64, 128])
+def test_small_solve_spectral_cycle_matches_numpy(hip, size):
+    """pinc_hip_mg_solve_small with the Fourier basis: one two-grid cycle
+    (multigrid:spectralCoarse) against a numpy restatement -- red-black
+    Gauss-Seidel (blk_update's order), the residual, the half-weight
+    restriction x 4, the level-1 correction equation solved exactly (numpy
+    FFT with the 5-point symbol, DC dropped), the bilinear prolongation --
+    to 1e-12 of max |phi| (the f64 matrix-core products round differently
+    from the FFT); then a full solve to an RMS residual <= 1e-10."""
+    import torch
+    vp = C.c_void_p
+    hip.pinc_hip_mg_solve_small.argtypes = [vp, vp, vp, C.c_int, vp, C.c_int, C.c_int, C.c_int, C.c_int,
+                                            C.c_double, vp, vp, vp]
+    n = size
+    lv = _small_levels(n, n)
+    g = np.random.default_rng(5)
+    r = g.standard_normal((n, n))
+    r -= r.mean()
+    p0 = g.standard_normal((n, n))
+    basis = torch.from_numpy(_fourier_basis(n // 2)).cuda()
+    rho = torch.from_numpy(r.ravel().copy()).cuda()
+    phi = torch.from_numpy(p0.ravel().copy()).cuda()
+    out = _small_solve(hip, phi, rho, lv, 4, 4, 10, 1, basis)
+    assert out[0] == 1
+    y, x = np.meshgrid(np.arange(n), np.arange(n), indexing="ij")
+
+    def smooth(a, k):
+        for _ in range(k):
+            for colour in (0, 1):
+                s = np.roll(a, -1, 1) + np.roll(a, 1, 1)
+                s = s + (np.roll(a, -1, 0) + np.roll(a, 1, 0))
+                a = np.where(((x + y) & 1) == colour, (s + r) * 0.25, a)
+        return a
+
+    def resid(a):
+        q = -4.0 * a + (np.roll(a, -1, 1) + np.roll(a, 1, 1))
+        return q + (np.roll(a, -1, 0) + np.roll(a, 1, 0)) + r
+
+    a = smooth(p0, 4)
+    q = resid(a)
+    rc = (4.0 * q + (np.roll(q, -1, 1) + np.roll(q, 1, 1)) + (np.roll(q, -1, 0) + np.roll(q, 1, 0))) / 8.0
+    r1 = rc[::2, ::2] * 4.0
+    m = n // 2
+    k = 2 * np.pi * np.fft.fftfreq(m)
+    sym = (2 - 2 * np.cos(k))[:, None] + (2 - 2 * np.cos(k))[None, :]
+    sym[0, 0] = 1.0
+    f = np.fft.fft2(r1) / sym
+    f[0, 0] = 0.0
+    p1 = np.real(np.fft.ifft2(f))
+    # bilinear prolongation (prol_low: y first, then x along the lowest odd
+    # dimension)
+    pf = np.zeros((n, n))
+    pf[::2, ::2] = p1
+    pf[1::2, ::2] = 0.5 * (p1 + np.roll(p1, -1, 0))
+    pf[:, 1::2] = 0.5 * (pf[:, ::2] + np.roll(pf[:, ::2], -1, 1))
+    a = smooth(a + pf, 4)
+    got = phi.cpu().numpy().reshape(n, n)
+    assert np.max(np.abs(got - a)) <= 1e-12 * np.max(np.abs(a))
+    np.testing.assert_allclose(out[2], np.sqrt(np.mean(resid(a) ** 2)), rtol=1e-9)
+    # a whole solve
+    out = _small_solve(hip, phi, rho, lv, 4, 4, 10, 200, basis)
+    assert out[1] <= 1e-10 and 1 <= out[0] < 200
+    got = phi.cpu().numpy().reshape(n, n)
+    assert np.sqrt(np.mean(resid(got) ** 2)) <= 1.1e-10

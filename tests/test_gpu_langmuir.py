@@ -73,3 +73,19 @@ def test_langmuir1d_spectral_frequency(sim_cls):
     om_o = ke_peak_omega(ke_o, float(cfg["time"]["timeStep"]))
     assert abs(om - 1.0) <= 0.01, om
     assert abs(om - om_o) <= 1e-6, (om, om_o)
+
+
+@pytest.mark.parametrize("coarse", [0, 1])
+def test_c2_langmuir_frequency_one_cu(sim_cls, coarse):
+    """C2's Langmuir run with the native solve in one workgroup
+    (multigrid:oneCU; coarse = 1 with the level-1 correction on the f64
+    matrix cores, as the bench runs C2): the same plasma frequency over 150
+    steps as the reference solve's golden value, and the first step's
+    kinetic energy."""
+    g = GOLD["c2"]
+    cfg = configs.config("c2")
+    cfg["multigrid"].update({"native": "1", "oneCU": "1", "spectralCoarse": str(coarse)})
+    ke = _ke_history(sim_cls, cfg, 150)
+    om = ke_peak_omega(ke, float(cfg["time"]["timeStep"]))
+    assert abs(om - g["omega_150"]) <= 5e-5, (om, g["omega_150"])
+    assert abs(ke[0] - g["KE1"]) <= 5e-7

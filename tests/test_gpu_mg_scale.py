@@ -238,3 +238,75 @@ def test_speculative_first_sweep_is_bit_identical():
     assert out["0"][0] == out["1"][0]
     for a, b in zip(out["0"][1], out["1"][1]):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("coarse", [0, 1])
+def test_one_cu_solve_matches_multi_launch_and_oracle(coarse):
+    """multigrid:oneCU (native mode, one rank, C2's 2-D 128^2): every cycle
+    of a solve and its convergence test in one workgroup
+    (pinc_hip_mg_solve_small), against the per-level launches of the same
+    cycle and the oracle's native solve on the same rho.
+
+    coarse = 0: the V-cycle (k_gs_pass, k_residual, k_restrict,
+    k_mg_coarse, k_prolong_add in the per-level form): the same operators in
+    the same expression order, so for the same cycle count phi is
+    bit-identical (only the norm's summation order differs: histories to
+    1e-12).  coarse = 1: multigrid:spectralCoarse, the two-grid cycle whose
+    level-1 correction the workgroup solves exactly through the real Fourier
+    basis on the f64 matrix cores, against rocFFT on the per-level path: the
+    same discrete problem in another rounding (cycle counts +-1, phi to 1e-9
+    of its maximum, as against the oracle).  A sequence of warm-started
+    solves whose counts differ, a cycle cap (mgSetLimit) and a history longer
+    than one launch's 60 entries."""
+    import orc
+    from pinc_amd import Sim, configs
+    cfg = configs.config("c2")
+    cfg["multigrid"]["native"] = "1"
+    cfg["multigrid"]["spectralCoarse"] = str(coarse)
+    gen = np.random.default_rng(11)
+    out = {}
+    for one in ("0", "1", "oracle"):
+        cfg["multigrid"]["oneCU"] = "0" if one == "oracle" else one
+        ini = configs.write_ini(cfg)
+        try:
+            if one == "oracle":
+                s = orc.World(ini)
+            else:
+                s = Sim(ini, perturb=False)
+            shape = s.grid(0).shape
+            inner = tuple(slice(1, -1) for _ in shape[:-1]) + (0,)
+            if not out:
+                base = np.zeros(shape)
+                base[inner] = gen.standard_normal(base[inner].shape)
+                rhos = [base * a for a in (1.0, 1.0, 1e-3, 10.0)] + [base[::-1].copy()]
+            hist, phis = [], []
+            s.mg_limit(0, 100)
+            for r in rhos:
+                s.set_grid(0, r)
+                s.op("solve")
+                hist.append(s.mg_history().tolist())
+                phis.append(s.grid(1)[inner].copy())
+            s.mg_limit(3, 100)
+            s.set_grid(0, rhos[3] * 7.0)
+            s.op("solve")
+            hist.append(s.mg_history().tolist())
+            phis.append(s.grid(1)[inner].copy())
+            s.close()
+        finally:
+            os.unlink(ini)
+        out[one] = (hist, phis)
+    (h0, p0), (h1, p1), (ho, po) = out["0"], out["1"], out["oracle"]
+    counts = [len(h) for h in h1]
+    assert len(set(counts[:-1])) > 1, counts
+    assert counts[-1] == 3
+    for k, (a, b, pa, pb) in enumerate(zip(h0, h1, p0, p1)):
+        if coarse:
+            assert abs(len(a) - len(b)) <= 1, (k, len(a), len(b))
+            assert np.max(np.abs(pb - pa)) <= 1e-9 * np.max(np.abs(pa)), k
+        else:
+            assert len(a) == len(b), (k, len(a), len(b))
+            assert np.allclose(a, b, rtol=1e-12, atol=0), k
+            assert np.array_equal(pa, pb), k
+    for k, (a, b, pa, pb) in enumerate(zip(ho, h1, po, p1)):
+        assert abs(len(a) - len(b)) <= 1, (k, len(a), len(b))
+        assert np.max(np.abs(pb - pa)) <= 1e-9 * np.max(np.abs(pa)), k

@@ -177,30 +177,39 @@ def test_native_mg_graph_replay(sim_cls, case, coarse):
     several steps (the graph is reused across solves).  coarse = 1: with the
     exact level-1 solve (multigrid:spectralCoarse), whose rocFFT execution
     and copies are captured into the graph too; "c2" is the
-    bench's C2 line (2-D 128^2, graph and spectral coarse solve on).  The
-    kernels are the same; the deposit's atomics make rho differ by rounding
-    between any two runs, so phi is compared to 1e-9 of its scale and the
-    cycle count to 1."""
+    bench's C2 line (2-D 128^2, spectral coarse solve on) with the graph
+    and, as the bench runs it, with the whole solve in one workgroup
+    (multigrid:oneCU: the level-1 correction on the f64 matrix cores).  The
+    kernels are the same (the one-workgroup solve: the same operators); the
+    deposit's atomics make rho differ by rounding between any two runs, so
+    phi is compared to 1e-9 of its scale and the cycle count to 1 (2 over
+    the three steps' solves for the one-workgroup solve, whose coarse
+    correction rounds differently)."""
     if case == "c2":
         cfg = configs.bench_config("c2", 128)
         kw = dict(perturb=True)
+        variants = [("0", "0"), ("1", "0"), ("0", "1")]
     else:
         cfg = configs.config("warm", true_size=(32, 32, 64), ppc=8, nalloc_pc=16, levels=4)
         cfg["multigrid"]["native"] = "1"
         cfg["multigrid"]["spectralCoarse"] = str(coarse)
         kw = dict(maxwell=True, perturb=False, seed=3)
+        variants = [("0", "0"), ("1", "0")]
     out = {}
-    for graph in ("0", "1"):
+    for graph, one in variants:
         cfg["multigrid"]["graph"] = graph
+        cfg["multigrid"]["oneCU"] = one
         with sim_cls(configs.write_ini(cfg), **kw) as s:
             s.init()
             for _ in range(3):
                 s.step()
-            out[graph] = (s.grid(1).copy(), s.cycles, s.energy()[:2])
-    scale = np.abs(out["0"][0]).max()
-    np.testing.assert_allclose(out["1"][0], out["0"][0], rtol=0, atol=1e-9 * scale)
-    assert abs(out["0"][1] - out["1"][1]) <= 1
-    np.testing.assert_allclose(out["1"][2], out["0"][2], rtol=1e-9)
+            out[graph, one] = (s.grid(1).copy(), s.cycles, s.energy()[:2])
+    ref = out["0", "0"]
+    scale = np.abs(ref[0]).max()
+    for v in variants[1:]:
+        np.testing.assert_allclose(out[v][0], ref[0], rtol=0, atol=1e-9 * scale)
+        assert abs(ref[1] - out[v][1]) <= (2 if v[1] == "1" else 1), (v, ref[1], out[v][1])
+        np.testing.assert_allclose(out[v][2], ref[2], rtol=1e-9)
 
 
 @pytest.mark.parametrize("layout", ["sorted", "scattered", "mixed"])
