@@ -1486,11 +1486,6 @@ constexpr int kPushGroupMin = PINC_PUSH_GROUP_MIN;
 #ifndef PINC_PUSH_COUNT_RUNS
 #define PINC_PUSH_COUNT_RUNS 1
 #endif
-// 1: the sorting push ranks a thread's item pairs of one brick with one LDS
-// atomic and stores them as 16-B pairs
-#ifndef PINC_PUSH_SORT_PAIRS
-#define PINC_PUSH_SORT_PAIRS 0
-#endif
 #ifndef PINC_PUSH_RHO_LDS
 #define PINC_PUSH_RHO_LDS 2048
 #endif
@@ -2298,32 +2293,6 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	if (SORT) {
 		static_assert(kInCellCap <= 256 && kPushChunk <= (1 << 23), "rank/brick packing");
 		int no = 0;  // (trace: items outside ib)
-#if PINC_PUSH_SORT_PAIRS
-		// items k, k + 1 of a thread are consecutive particles, mostly of one
-		// brick: such a pair takes two consecutive ranks from one LDS atomic
-		// and is stored as one 16-B pair below
-#pragma unroll
-		for (int k = 0; k < kPushItems; k += 2) {
-			int c0[3] = {0, 0, 0}, c1[3] = {0, 0, 0};
-#pragma unroll
-			for (int d = 0; d < ND; d++) {
-				c0[d] = sort_cell(p[k][d], vv[k][d]);
-				c1[d] = sort_cell(p[k + 1][d], vv[k + 1][d]);
-			}
-			const bool ok0 = (valid >> k) & 1u, ok1 = (valid >> (k + 1)) & 1u;
-			const int lb0 = ok0 ? brick_inside<ND>(a.tg, ib, c0) : -1;
-			const int lb1 = ok1 ? brick_inside<ND>(a.tg, ib, c1) : -1;
-			const bool pair = lb0 >= 0 && lb0 == lb1;
-			const int r0 = lb0 >= 0 ? atomicAdd(&bCnt[lb0], pair ? 2 : 1) : 0;
-			const int r1 = pair ? r0 + 1 : (lb1 >= 0 ? atomicAdd(&bCnt[lb1], 1) : 0);
-			const bool out0 = ok0 && lb0 < 0, out1 = ok1 && lb1 < 0;
-			const int g0 = agg_add(a.cursor, out0 ? brick_first_key<ND>(a.tg, c0) : 0, out0);
-			const int g1 = agg_add(a.cursor, out1 ? brick_first_key<ND>(a.tg, c1) : 0, out1);
-			rlL[k * kPushThreads + threadIdx.x] = lb0 >= 0 ? (r0 << 8 | lb0) : (ok0 ? ~g0 : -1);
-			rlL[(k + 1) * kPushThreads + threadIdx.x] = lb1 >= 0 ? (r1 << 8 | lb1) : (ok1 ? ~g1 : -1);
-			no += out0 + out1;
-		}
-#else
 #pragma unroll
 		for (int k = 0; k < kPushItems; k++) {
 			int c[3] = {0, 0, 0};
@@ -2341,7 +2310,6 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 			rlL[k * kPushThreads + threadIdx.x] = rl;  // (stored at once: no item's rank stays live)
 			no += rl < 0 && ok;
 		}
-#endif
 		if (a.diag) {
 			no = wave_sum_i(no);
 			if (lane == 0 && no) atomicAdd(&a.diag[0], (unsigned long long)no);
@@ -2685,26 +2653,6 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 		// that share a brick took consecutive ranks from its LDS counter, so
 		// their stores cover one contiguous range (coalesced like the plain
 		// push's) and no staging through LDS is needed
-#if PINC_PUSH_SORT_PAIRS
-		// a pair ranked together goes out as one 16-B store (8-B aligned:
-		// gfx950 takes dword-aligned 16-B global stores)
-		typedef double dvec2u __attribute__((ext_vector_type(2), aligned(8)));
-		unsigned pairDone = 0;
-#pragma unroll
-		for (int k = 0; k < kPushItems; k += 2) {
-			const int r0 = rlL[k * kPushThreads + threadIdx.x], r1 = rlL[(k + 1) * kPushThreads + threadIdx.x];
-			if (r0 < 0 || r1 != r0 + 256) continue;  // (same brick, consecutive ranks)
-			const long o = (long)bBase[r0 & 255] + (r0 >> 8);
-#pragma unroll
-			for (int d = 0; d < ND; d++) {
-				*reinterpret_cast<dvec2u *>(a.xo[d] + o) = dvec2u{p[k][d], p[k + 1][d]};
-				*reinterpret_cast<dvec2u *>(a.vo[d] + o) = dvec2u{vv[k][d], vv[k + 1][d]};
-			}
-			pairDone |= 3u << k;
-		}
-#else
-		const unsigned pairDone = 0;
-#endif
 #pragma unroll
 		for (int k = 0; k < kPushItems; k++) {
 			if (!((valid >> k) & 1u)) continue;
@@ -2713,7 +2661,6 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 			const long o = r >= 0 ? (long)bBase[r & 255] + (r >> 8) : (long)~r;
 #pragma unroll
 			for (int d = 0; d < ND; d++) {
-				if ((pairDone >> k) & 1u) break;
 				// (nontemporal, 8 B per lane: 24.4 -> 33.5 ms per sorting push,
 				// profiles/r06i_count_runs_sort_nt_ab.txt)
 				a.xo[d][o] = p[k][d];
