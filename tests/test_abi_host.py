@@ -161,3 +161,31 @@ def test_push_chunk_placement_is_a_bijection(lib, nb):
     assert xcd.min() >= 0 and xcd.max() <= 7
     counts = np.bincount(xcd, minlength=8)
     assert counts.max() - counts.min() <= 1, counts
+
+
+class _Lvl(C.Structure):
+    _fields_ = [("nd", C.c_int), ("T", C.c_int * 3)]
+
+
+@pytest.mark.parametrize("case", ["3d", "odd_x", "too_many", "not_halving", "spectral_not_square", "cycles"])
+def test_small_solve_rejects_bad_levels(lib, case):
+    """pinc_hip_mg_solve_small checks its levels on the host before any
+    launch (no GPU needed): a 3-D level, an x extent that is not a power of
+    two, more than 16384 points, levels that do not halve, a non-square
+    level 1 with the spectral basis, a cycle cap below 1 -- each returns a
+    nonzero code and names itself in pinc_hip_error_string."""
+    h = lib.HIP
+    vp = C.c_void_p
+    h.pinc_hip_mg_solve_small.argtypes = [vp, vp, vp, C.c_int, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_double,
+                                          vp, vp, vp]
+    h.pinc_hip_error_string.restype = C.c_char_p
+    shapes = {"3d": [(3, 16, 16, 16), (3, 8, 8, 8)], "odd_x": [(2, 96, 64, 1), (2, 48, 32, 1)],
+              "too_many": [(2, 256, 128, 1), (2, 128, 64, 1)], "not_halving": [(2, 128, 128, 1), (2, 32, 64, 1)],
+              "spectral_not_square": [(2, 128, 64, 1), (2, 64, 32, 1)], "cycles": [(2, 128, 128, 1), (2, 64, 64, 1)]}
+    lv = shapes[case]
+    arr = (_Lvl * len(lv))(*[_Lvl(nd, (C.c_int * 3)(a, b, c)) for nd, a, b, c in lv])
+    basis = C.c_void_p(1) if case == "spectral_not_square" else None  # never dereferenced: rejected first
+    cycles = 0 if case == "cycles" else 10
+    rc = h.pinc_hip_mg_solve_small(None, None, None, len(lv), arr, 4, 4, 10, cycles, 1e-10, basis, None, None)
+    assert rc != 0
+    assert b"mg_solve_small" in h.pinc_hip_error_string()
