@@ -1332,7 +1332,9 @@ __global__ __launch_bounds__(1024) void k_mg_coarse(const double *__restrict__ r
 // Native mode, one rank, a 2-D level 0 of at most kSmallMax points (x extent
 // a power of two; C2's 128^2): every cycle of a solve, and the convergence
 // test, in one 1024-thread workgroup.  Each thread owns fixed level-0 points
-// of alternating colours and keeps their rho in registers; phi lives in LDS
+// of alternating colours and holds their rho in registers while it smooths
+// them (loaded per smoothing: 16 slots' worth live across the whole cycle
+// would spill at 1024 threads); phi lives in LDS
 // (colour-major) while it is smoothed, then goes through memory (phi, its own
 // buffer; the residual through res) while the LDS holds the coarse solve:
 // the V-cycle of levels 1.. (coarse_body), or with multigrid:spectralCoarse
@@ -1443,7 +1445,7 @@ __global__ __launch_bounds__(1024) void k_mg_solve_small2(double *phi, const dou
 	// the per-colour bases, recomputed from the thread index at the top of
 	// each phase (refresh: the index through an empty asm), so that neither
 	// they nor the slots' addresses (5 per slot) stay live across the cycle
-	// loop -- only rho's registers do
+	// loop
 	int tid = t;
 	int y0, xc[2], own[2], xpI[2], xmI[2], ob[2], g0[2];
 	auto refresh = [&]() {
