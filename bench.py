@@ -274,7 +274,8 @@ def main() -> int:
     ap.add_argument("--ppc", type=int, default=None, help="particles per cell per species (c4: 64, c3: 32)")
     ap.add_argument("--mg-graph", type=int, default=None,
                     help="1: native multigrid replays each V-cycle as a captured HIP graph (multigrid:graph); "
-                         "default 1 for the launch-bound C2, 0 elsewhere (neutral at C4)")
+                         "default 1 for C2 (where --mg-one-cu, on by default, bypasses it), 0 elsewhere "
+                         "(neutral at C4)")
     ap.add_argument("--mg-one-cu", type=int, default=None,
                     help="1: a native one-rank 2-D solve of at most 16384 points runs all its cycles and the "
                          "convergence test in one workgroup (multigrid:oneCU, pinc_hip_mg_solve_small; with "
