@@ -1374,8 +1374,6 @@ __device__ __forceinline__ f64x4 mm_tile(const double *A, const double *B, int l
 		const double x = TA ? A[kk * ld + ii] : A[ii * ld + kk];
 		const double y = TB ? B[jj * ld + kk] : B[kk * ld + jj];
 		acc = __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, acc, 0, 0, 0);
-		// at most 8 operand reads (16 VGPRs) ahead
-		if ((k0 & 12) == 12) __builtin_amdgcn_sched_barrier(0);
 	}
 	return acc;
 }
