@@ -108,7 +108,7 @@ static void shard_setup(MultigridSolver *S, const dictionary *ini, const Grid *r
 enum { kSmallOut = 64, kSmallHist = 60, kSmallChunk = 1000 };
 
 /* native mode, one rank, a 2-D level 0 of at most 16384 points (a multiple
- * of 2048) with a power-of-two x extent, its levels 1.. within the one-workgroup
+ * of 2048) with a power-of-two x extent <= 1024, its levels 1.. within the one-workgroup
  * coarse solve's LDS budget: the whole solve in one launch per solve
  * (pinc_hip_mg_solve_small).  multigrid:oneCU (default 0) or PINC_MG_SMALL
  * (experiments) turn it on; it replaces multigrid:spectralCoarse. */
@@ -118,7 +118,8 @@ static int small_eligible(const MultigridSolver *S, const dictionary *ini) {
 	if (!want || !S->native || S->shard || g_pinc.nranks != 1 || S->nLevels < 2) return 0;
 	const pinc_lvl_t L = S->L[0];
 	const long n0 = (long)L.T[0] * L.T[1];
-	if (L.nd != 2 || (L.T[0] & (L.T[0] - 1)) || L.T[0] < 2 || L.T[1] % 2 || n0 > 16384 || n0 % 2048) return 0;
+	if (L.nd != 2 || (L.T[0] & (L.T[0] - 1)) || L.T[0] < 2 || L.T[0] > 1024 || L.T[1] % 2 || n0 > 16384 || n0 % 2048)
+		return 0;
 	long tot = 0;
 	for (int q = 1; q < S->nLevels; q++) tot += 3 * S->N[q];
 	return tot <= 5500 * 3 && S->nLevels - 1 <= 12;
