@@ -108,10 +108,11 @@ static void shard_setup(MultigridSolver *S, const dictionary *ini, const Grid *r
 enum { kSmallOut = 64, kSmallHist = 60, kSmallChunk = 1000 };
 
 /* native mode, one rank, a 2-D level 0 of at most 16384 points (a multiple
- * of 2048) with a power-of-two x extent <= 1024, its levels 1.. within the one-workgroup
- * coarse solve's LDS budget: the whole solve in one launch per solve
- * (pinc_hip_mg_solve_small).  multigrid:oneCU (default 0) or PINC_MG_SMALL
- * (experiments) turn it on; it replaces multigrid:spectralCoarse. */
+ * of 2048) with a power-of-two x extent <= 1024, its levels 1.. within the
+ * one-workgroup coarse solve's LDS budget: the whole solve in one launch per
+ * solve (pinc_hip_mg_solve_small).  multigrid:oneCU (default 0) or
+ * PINC_MG_SMALL (experiments) turn it on.  With multigrid:spectralCoarse the
+ * workgroup solves level 1 exactly itself (no rocFFT plan is made). */
 static int small_eligible(const MultigridSolver *S, const dictionary *ini) {
 	int want = iniHas(ini, "multigrid:oneCU") && iniGetInt(ini, "multigrid:oneCU");
 	if (getenv("PINC_MG_SMALL")) want = atoi(getenv("PINC_MG_SMALL"));
