@@ -71,6 +71,40 @@ __global__ void k_copy(double *dst, const double *src, long n) {
 		dst[i] = src[i];
 }
 
+// one slab plane per blockIdx.y, the plane's nodes (x fastest) over
+// blockIdx.x: 32-bit in-plane coordinates, no 64-bit division per node
+// (same expression per component as k_efield)
+template <int ND>
+__global__ void k_efield_planes(const double *__restrict__ phi, pinc_geom_t g, double *__restrict__ E) {
+	const int sd = ND - 1;
+	const int T0 = g.T[0], T1 = ND > 1 ? g.T[1] : 1;
+	const unsigned ps = ND == 3 ? (unsigned)T0 * T1 : ND == 2 ? (unsigned)T0 : 1u;  // nodes per slab plane
+	const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= ps) return;
+	const int p = blockIdx.y;  // slab plane 0 .. nloc+1
+	int c[3] = {0, 0, 0};
+	if (ND == 3) {
+		c[1] = (int)(i / (unsigned)T0);
+		c[0] = (int)(i - (unsigned)c[1] * T0);
+	} else if (ND == 2) {
+		c[0] = (int)i;
+	}
+	const int Ts = g.T[sd];
+	c[sd] = wrap(g.off + p - 1, Ts);
+	const long gs[3] = {1, T0, (long)T0 * T1};
+	long gi = 0;
+#pragma unroll
+	for (int d = 0; d < ND; d++) gi += (long)c[d] * gs[d];
+	const long idx = (long)p * ps + i;
+#pragma unroll
+	for (int d = 0; d < ND; d++) {
+		const int Td = g.T[d];
+		const long up = gi + (long)(wrap(c[d] + 1, Td) - c[d]) * gs[d];
+		const long dn = gi + (long)(wrap(c[d] - 1, Td) - c[d]) * gs[d];
+		E[idx * ND + d] = 0.5 * (phi[up] - phi[dn]);
+	}
+}
+
 template <int ND>
 __global__ void k_efield(const double *__restrict__ phi, pinc_geom_t g, double *__restrict__ E) {
 	// slab nodes: non-slab dims periodic [0,T), slab dim planes 0..nloc+1
@@ -240,6 +274,13 @@ extern "C" int pinc_hip_copy_plane(double *dst, const double *slab, pinc_geom_t 
 extern "C" int pinc_hip_efield(const double *phi, pinc_geom_t g, double *E, void *stream) {
 	long n = plane_size(g) * (g.nloc + 2);
 	hipStream_t st = (hipStream_t)stream;
+	if (plane_size(g) < (1L << 31) && g.nloc + 2 <= 65535) {
+		const dim3 grid((unsigned)ceil_div(plane_size(g), kThreads), (unsigned)(g.nloc + 2));
+		if (g.nd == 3) hipLaunchKernelGGL(k_efield_planes<3>, grid, dim3(kThreads), 0, st, phi, g, E);
+		else if (g.nd == 2) hipLaunchKernelGGL(k_efield_planes<2>, grid, dim3(kThreads), 0, st, phi, g, E);
+		else hipLaunchKernelGGL(k_efield_planes<1>, grid, dim3(kThreads), 0, st, phi, g, E);
+		return check_launch("efield");
+	}
 	if (g.nd == 3) hipLaunchKernelGGL(k_efield<3>, dim3(grid_for(n)), dim3(kThreads), 0, st, phi, g, E);
 	else if (g.nd == 2) hipLaunchKernelGGL(k_efield<2>, dim3(grid_for(n)), dim3(kThreads), 0, st, phi, g, E);
 	else hipLaunchKernelGGL(k_efield<1>, dim3(grid_for(n)), dim3(kThreads), 0, st, phi, g, E);
