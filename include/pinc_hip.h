@@ -277,6 +277,10 @@ int pinc_hip_deposit(pinc_pop_t pop, int s, pinc_geom_t g, double *rhoSlab, void
  * n doubles of the slab E grid; qm/mq are device arrays. */
 int pinc_hip_field_chain(const double *E, double *Es, long n, const double *qm, const double *mq,
                          double pre, int s, void *stream);
+/* Every species' Es of pinc_hip_field_chain in one pass over E (the same
+ * running chain, bit-identical): species s at Es + s n, s < nSpecies. */
+int pinc_hip_field_chain_all(const double *E, double *Es, long n, const double *qm, const double *mq, double pre,
+                             int nSpecies, void *stream);
 
 /* order 0 (nearest grid point, node (int)(x + 0.5)): puDistrND0
  * (pusher.c:640-668) adds one unit per particle of species s (the caller

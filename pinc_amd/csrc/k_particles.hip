@@ -707,6 +707,23 @@ __global__ void k_field_chain(const double *__restrict__ E, double *__restrict__
 	}
 }
 
+// every species' rescaled copy of E in one pass over E (k_field_chain's
+// chain for species s is species s-1's times mq[s-1] qm[s] / qm[s-1]... in
+// the same expression order: the running v of the loop above), species s at
+// Es + s n
+__global__ void k_field_chain_all(const double *__restrict__ E, double *__restrict__ Es, long n,
+                                  const double *__restrict__ qm, const double *__restrict__ mq, double pre,
+                                  int nSpecies) {
+	for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+		double v = E[i] * pre;
+		Es[i] = v * qm[0];
+		for (int s = 1; s < nSpecies; s++) {
+			v = (v * qm[s - 1]) * mq[s - 1];
+			Es[(long)s * n + i] = v * qm[s];
+		}
+	}
+}
+
 // Boris rotation parameters of one species (puGet3DRotationParameters,
 // pusher.c:485-505)
 struct BorisRot {
@@ -3239,6 +3256,19 @@ extern "C" int pinc_hip_deposit(pinc_pop_t pop, int s, pinc_geom_t g, double *rh
 	else
 		hipLaunchKernelGGL((k_deposit_tiled<1, false>), dim3(nb), dim3(kThreads), 0, st, x0, x1, x2, b0, n, g, rho);
 	return check_launch("deposit");
+}
+
+extern "C" int pinc_hip_field_chain_all(const double *E, double *Es, long n, const double *qm, const double *mq,
+                                        double pre, int nSpecies, void *stream) {
+	if (n > 0 && (!E || !Es || !qm || !mq)) return set_error(hipErrorInvalidValue, "field_chain_all: null array");
+	if (nSpecies < 1 || nSpecies > PINC_MAX_SPECIES)
+		return set_error(hipErrorInvalidValue, "field_chain_all: species count");
+	if (n <= 0) return 0;
+	long nb = ceil_div(n, (long)kThreads * 4);
+	if (nb > 8192) nb = 8192;
+	hipLaunchKernelGGL(k_field_chain_all, dim3(nb), dim3(kThreads), 0, (hipStream_t)stream, E, Es, n, qm, mq, pre,
+	                   nSpecies);
+	return check_launch("field chain (all species)");
 }
 
 extern "C" int pinc_hip_field_chain(const double *E, double *Es, long n, const double *qm,

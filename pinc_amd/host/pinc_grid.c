@@ -169,6 +169,7 @@ void gFree(Grid *g) {
 		pinc_hip_free(g->dev->recv[0]);
 		pinc_hip_free(g->dev->recv[1]);
 		pinc_hip_free(g->dev->scaled);
+		pinc_hip_free(g->dev->scaledAll);
 		pinc_hip_free(g->dev->lit);
 		free(g->dev);
 	}

@@ -189,6 +189,8 @@ struct PincDevGrid {
 	int ghostsValid;    /* slab ghost planes already hold periodic images */
 	double *recv[2];    /* halo receive planes (multi-rank) */
 	double *scaled;     /* E as rescaled for the species being pushed (lazy) */
+	double *scaledAll;  /* every species' rescaled E, one pass per push round (lazy) */
+	int scaledAllS;     /* species it holds room for */
 	/* sharded multigrid (phi only): this rank's slab with extOff halo planes
 	 * on each side, extPlanes planes in all, owned by the solver */
 	double *ext;

@@ -462,11 +462,20 @@ static int push_all(Population *pop, Grid *E, double *const *xout) {
 		pinc_push_t a;
 		memset(&a, 0, sizeof(a));
 		if (E) {
+			/* every species' rescaled E in one pass over E at the first
+			 * species (E does not change during the round) */
 			PincDevGrid *eg = E->dev;
-			if (!eg->scaled) pinc_check(pinc_hip_malloc((void **)&eg->scaled, eg->n * sizeof(double)), "E scaled");
-			pinc_check(pinc_hip_field_chain(eg->d, eg->scaled, eg->n, dv->qm, dv->mq, 1.0, s, g_pinc.stream),
-			           "E chain");
-			a.Es = eg->scaled;
+			if (eg->scaledAllS < pop->nSpecies) {
+				pinc_hip_free(eg->scaledAll);
+				pinc_check(pinc_hip_malloc((void **)&eg->scaledAll, (long)pop->nSpecies * eg->n * sizeof(double)),
+				           "E scaled");
+				eg->scaledAllS = pop->nSpecies;
+			}
+			if (s == 0)
+				pinc_check(pinc_hip_field_chain_all(eg->d, eg->scaledAll, eg->n, dv->qm, dv->mq, 1.0, pop->nSpecies,
+				                                    g_pinc.stream),
+				           "E chain");
+			a.Es = eg->scaledAll + (long)s * eg->n;
 			a.kick = 1;
 		}
 		pinc_pop_t p = pinc_devpop(pop);
@@ -653,12 +662,19 @@ void pinc_pending_vel(const Population *pop, int s, double *const *dst) {
 		msg(ERROR, "internal: E was freed, reallocated or touched between puAcc and a re-kick of the pending "
 		           "sorting push");
 	PincDevGrid *eg = dv->pendingE->dev;
-	pinc_check(pinc_hip_field_chain(eg->d, eg->scaled, eg->n, dv->qm, dv->mq, 1.0, s, g_pinc.stream), "E chain");
+	/* species s's rescaled E of the push round (E unchanged since: checked
+	 * above), else made here */
+	const double *es = eg->scaledAll && s < eg->scaledAllS ? eg->scaledAll + (long)s * eg->n : NULL;
+	if (!es) {
+		if (!eg->scaled) pinc_check(pinc_hip_malloc((void **)&eg->scaled, eg->n * sizeof(double)), "E scaled");
+		pinc_check(pinc_hip_field_chain(eg->d, eg->scaled, eg->n, dv->qm, dv->mq, 1.0, s, g_pinc.stream), "E chain");
+		es = eg->scaled;
+	}
 	pinc_pop_t p = pinc_devpop(pop);
 	/* (species s only is touched: indices iStart[s] .. iStop[s] - 1) */
 	for (int d = 0; d < nd; d++) p.v[d] = dst[d] - a;
 	int nb = 0;
-	pinc_check(pinc_hip_accelerate(p, s, eg->geom, eg->scaled, dv->kePartial, &nb, g_pinc.stream), "pending kick");
+	pinc_check(pinc_hip_accelerate(p, s, eg->geom, es, dv->kePartial, &nb, g_pinc.stream), "pending kick");
 }
 
 /* The populations with a pending fused push (main.c has one).  Before a
