@@ -339,6 +339,10 @@ int pinc_hip_copy_plane(double *dst, const double *slab, pinc_geom_t g, int plan
  * global periodic phi (ghost planes then equal the neighbours' values
  * bit for bit, so the TOHALO is implied). */
 int pinc_hip_efield(const double *phiGlobal, pinc_geom_t g, double *Eslab, void *stream);
+/* The same with E = h (phi_up - phi_dn): h = 0.5 is pinc_hip_efield, h = -0.5
+ * its result followed by gMul(E, -1) (main.c:247) bit for bit, in one pass
+ * (regular()'s step); other h are rejected. */
+int pinc_hip_efield_scaled(const double *phi, pinc_geom_t g, double *E, double h, void *stream);
 /* deterministic two-stage sums: *out = sum(a) ; sum(a*b) */
 int pinc_hip_sum(const double *a, long n, double *partial, double *out, void *stream);
 int pinc_hip_dot(const double *a, const double *b, long n, double *partial, double *out, void *stream);

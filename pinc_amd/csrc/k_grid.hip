@@ -75,7 +75,7 @@ __global__ void k_copy(double *dst, const double *src, long n) {
 // blockIdx.x: 32-bit in-plane coordinates, no 64-bit division per node
 // (same expression per component as k_efield)
 template <int ND>
-__global__ void k_efield_planes(const double *__restrict__ phi, pinc_geom_t g, double *__restrict__ E) {
+__global__ void k_efield_planes(const double *__restrict__ phi, pinc_geom_t g, double *__restrict__ E, double h) {
 	const int sd = ND - 1;
 	const int T0 = g.T[0], T1 = ND > 1 ? g.T[1] : 1;
 	const unsigned ps = ND == 3 ? (unsigned)T0 * T1 : ND == 2 ? (unsigned)T0 : 1u;  // nodes per slab plane
@@ -101,12 +101,12 @@ __global__ void k_efield_planes(const double *__restrict__ phi, pinc_geom_t g, d
 		const int Td = g.T[d];
 		const long up = gi + (long)(wrap(c[d] + 1, Td) - c[d]) * gs[d];
 		const long dn = gi + (long)(wrap(c[d] - 1, Td) - c[d]) * gs[d];
-		E[idx * ND + d] = 0.5 * (phi[up] - phi[dn]);
+		E[idx * ND + d] = h * (phi[up] - phi[dn]);
 	}
 }
 
 template <int ND>
-__global__ void k_efield(const double *__restrict__ phi, pinc_geom_t g, double *__restrict__ E) {
+__global__ void k_efield(const double *__restrict__ phi, pinc_geom_t g, double *__restrict__ E, double h) {
 	// slab nodes: non-slab dims periodic [0,T), slab dim planes 0..nloc+1
 	int T[3] = {g.T[0], g.T[1], g.T[2]};
 	int sd = ND - 1;
@@ -129,7 +129,7 @@ __global__ void k_efield(const double *__restrict__ phi, pinc_geom_t g, double *
 		for (int d = 0; d < ND; d++) {
 			long up = gi + (long)(wrap(c[d] + 1, T[d]) - c[d]) * gs[d];
 			long dn = gi + (long)(wrap(c[d] - 1, T[d]) - c[d]) * gs[d];
-			E[idx * ND + d] = 0.5 * (phi[up] - phi[dn]);
+			E[idx * ND + d] = h * (phi[up] - phi[dn]);
 		}
 	}
 }
@@ -271,20 +271,28 @@ extern "C" int pinc_hip_copy_plane(double *dst, const double *slab, pinc_geom_t 
 	return check_launch("copy_plane");
 }
 
-extern "C" int pinc_hip_efield(const double *phi, pinc_geom_t g, double *E, void *stream) {
+// h = 0.5: gFinDiff1st (grid.c:226-261); h = -0.5: the same followed by
+// gMul(E, -1) (main.c:247), bit for bit (the negation and the halving are
+// exact, and IEEE rounding is symmetric in the sign)
+extern "C" int pinc_hip_efield_scaled(const double *phi, pinc_geom_t g, double *E, double h, void *stream) {
+	if (h != 0.5 && h != -0.5) return set_error(hipErrorInvalidValue, "efield: h must be 0.5 or -0.5");
 	long n = plane_size(g) * (g.nloc + 2);
 	hipStream_t st = (hipStream_t)stream;
 	if (plane_size(g) < (1L << 31) && g.nloc + 2 <= 65535) {
 		const dim3 grid((unsigned)ceil_div(plane_size(g), kThreads), (unsigned)(g.nloc + 2));
-		if (g.nd == 3) hipLaunchKernelGGL(k_efield_planes<3>, grid, dim3(kThreads), 0, st, phi, g, E);
-		else if (g.nd == 2) hipLaunchKernelGGL(k_efield_planes<2>, grid, dim3(kThreads), 0, st, phi, g, E);
-		else hipLaunchKernelGGL(k_efield_planes<1>, grid, dim3(kThreads), 0, st, phi, g, E);
+		if (g.nd == 3) hipLaunchKernelGGL(k_efield_planes<3>, grid, dim3(kThreads), 0, st, phi, g, E, h);
+		else if (g.nd == 2) hipLaunchKernelGGL(k_efield_planes<2>, grid, dim3(kThreads), 0, st, phi, g, E, h);
+		else hipLaunchKernelGGL(k_efield_planes<1>, grid, dim3(kThreads), 0, st, phi, g, E, h);
 		return check_launch("efield");
 	}
-	if (g.nd == 3) hipLaunchKernelGGL(k_efield<3>, dim3(grid_for(n)), dim3(kThreads), 0, st, phi, g, E);
-	else if (g.nd == 2) hipLaunchKernelGGL(k_efield<2>, dim3(grid_for(n)), dim3(kThreads), 0, st, phi, g, E);
-	else hipLaunchKernelGGL(k_efield<1>, dim3(grid_for(n)), dim3(kThreads), 0, st, phi, g, E);
+	if (g.nd == 3) hipLaunchKernelGGL(k_efield<3>, dim3(grid_for(n)), dim3(kThreads), 0, st, phi, g, E, h);
+	else if (g.nd == 2) hipLaunchKernelGGL(k_efield<2>, dim3(grid_for(n)), dim3(kThreads), 0, st, phi, g, E, h);
+	else hipLaunchKernelGGL(k_efield<1>, dim3(grid_for(n)), dim3(kThreads), 0, st, phi, g, E, h);
 	return check_launch("efield");
+}
+
+extern "C" int pinc_hip_efield(const double *phi, pinc_geom_t g, double *E, void *stream) {
+	return pinc_hip_efield_scaled(phi, g, E, 0.5, stream);
 }
 
 extern "C" int pinc_hip_reduce(const double *partial, int n, double div, double *out, void *stream) {

@@ -334,7 +334,16 @@ void gHaloOp(funPtr sliceOp, Grid *grid, const MpiInfo *mpiInfo, opDirection dir
 	msg(ERROR, "gHaloOp: unsupported slice operation / direction on the device path");
 }
 
-void gFinDiff1st(const Grid *scalar, Grid *field) {
+static void fin_diff(const Grid *scalar, Grid *field, double h);
+
+void gFinDiff1st(const Grid *scalar, Grid *field) { fin_diff(scalar, field, 0.5); }
+
+/* gFinDiff1st followed by gMul(field, -1) in one pass, bit for bit the two
+ * (the step of regular(): main.c:245-247, where the TOHALO between them
+ * commutes with the exact negation) */
+void pinc_fin_diff_neg(const Grid *scalar, Grid *field) { fin_diff(scalar, field, -0.5); }
+
+static void fin_diff(const Grid *scalar, Grid *field, double h) {
 	pinc_grid_touch(field);
 	if (scalar->dev->ext) {
 		/* sharded multigrid: the extended slab holds planes off-hz .. of the
@@ -347,7 +356,7 @@ void gFinDiff1st(const Grid *scalar, Grid *field) {
 		pinc_geom_t g = field->dev->geom;
 		g.T[g.nd - 1] = scalar->dev->extPlanes;
 		g.off = scalar->dev->extOff;
-		pinc_check(pinc_hip_efield(scalar->dev->ext, g, field->dev->d, g_pinc.stream), "efield");
+		pinc_check(pinc_hip_efield_scaled(scalar->dev->ext, g, field->dev->d, h, g_pinc.stream), "efield");
 		/* a halo of one plane gives E on the true planes only: its ghost
 		 * planes then come from the neighbours (TOHALO) */
 		field->dev->ghostsValid = sv->extOff >= 2;
@@ -356,7 +365,7 @@ void gFinDiff1st(const Grid *scalar, Grid *field) {
 	const double *phi = scalar->dev->global ? scalar->dev->global : scalar->dev->d + scalar->dev->planeSize;
 	if (!scalar->dev->global && g_pinc.nranks > 1)
 		msg(ERROR, "gFinDiff1st needs the global potential (run the solver first)");
-	pinc_check(pinc_hip_efield(phi, field->dev->geom, field->dev->d, g_pinc.stream), "efield");
+	pinc_check(pinc_hip_efield_scaled(phi, field->dev->geom, field->dev->d, h, g_pinc.stream), "efield");
 	field->dev->ghostsValid = 1;
 }
 

@@ -322,6 +322,10 @@ struct MultigridSolver {
 	double *smallBasis; /* with multigrid:spectralCoarse: level 1's Fourier basis and eigenvalues */
 };
 
+/* gFinDiff1st and gMul(field, -1) in one pass, bit for bit the two
+ * (pinc_grid.c; regular()'s step) */
+void pinc_fin_diff_neg(const Grid *scalar, Grid *field);
+
 /* collectives over RCCL or the host transport (pinc_comm.c) */
 void pinc_comm_exchange(int nOps, const int *sendPeer, void *const *sendbuf, const long *sendBytes,
                         const int *recvPeer, void *const *recvbuf, const long *recvBytes, const char *what);

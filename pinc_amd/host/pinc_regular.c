@@ -209,9 +209,10 @@ static void sim_step(PincSim *S) {
 	S->solve(S->solver, S->rho, S->phi, S->mpi);
 	pinc_phase_begin(5);
 	gHaloOp((funPtr)setSlice, S->phi, S->mpi, TOHALO);
-	gFinDiff1st(S->phi, S->E);
+	/* gFinDiff1st, gHaloOp(E), gMul(E, -1): the negation in the finite
+	 * difference's own pass (exact, so it commutes with the halo copy) */
+	pinc_fin_diff_neg(S->phi, S->E);
 	gHaloOp((funPtr)setSlice, S->E, S->mpi, TOHALO);
-	gMul(S->E, -1.);
 	pinc_phase_end(5);
 	S->acc(pop, S->E);
 	pinc_phase_begin(7);
@@ -359,6 +360,11 @@ int pinc_sim_op(PincSim *S, const char *op) {
 		gFinDiff1st(S->phi, S->E);
 		gHaloOp((funPtr)setSlice, S->E, S->mpi, TOHALO);
 		gMul(S->E, -1.);
+	} else if (!strcmp(op, "efield_fused")) {
+		/* the step's form (sim_step) */
+		gHaloOp((funPtr)setSlice, S->phi, S->mpi, TOHALO);
+		pinc_fin_diff_neg(S->phi, S->E);
+		gHaloOp((funPtr)setSlice, S->E, S->mpi, TOHALO);
 	} else if (!strcmp(op, "acc")) S->acc(S->pop, S->E);
 	else if (!strcmp(op, "energy")) {
 		pSumKinEnergy(S->pop);

@@ -466,3 +466,29 @@ def test_literal_loop_tiled_one_rank_crossing_z(sim_cls, sort_interval):
         zs = s.particles(0)[0][:, 2]
         assert np.sum(zs < 1.5) > 0 and np.sum(zs > 16.5) > 0
     w.close()
+
+
+@pytest.mark.parametrize("case", ["cold3d", "langmuir2d", "shard"])
+def test_fused_negated_efield_equals_operators(sim_cls, case):
+    """regular()'s step computes E with the negation of gMul(E, -1)
+    (main.c:247) inside gFinDiff1st's pass (pinc_fin_diff_neg): E is bit
+    for bit the one of gFinDiff1st, gHaloOp(E), gMul(E, -1) run as separate
+    operators, on one rank's grid and on the sharded solver's extended slab
+    (one rank, multigrid:shard = 1)."""
+    if case == "shard":
+        cfg = configs.config("warm", true_size=(32, 32, 32), ppc=2, nalloc_pc=4, levels=3)
+        cfg["multigrid"].update({"native": "1", "shard": "1"})
+        ini = configs.write_ini(cfg)
+    else:
+        ini = _ini(case)
+    out = {}
+    with sim_cls(ini) as s:
+        s.init()
+        s.op("distr")
+        s.op("solve")
+        for op in ("efield", "efield_fused", "efield"):  # same phi (the deposit's atomics differ between runs)
+            s.op(op)
+            out.setdefault(op, []).append(s.grid(2).copy())
+    assert np.array_equal(out["efield"][0], out["efield_fused"][0])
+    assert np.array_equal(out["efield"][1], out["efield_fused"][0])
+    assert np.abs(out["efield"][0]).max() > 0
