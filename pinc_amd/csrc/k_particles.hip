@@ -1529,6 +1529,11 @@ constexpr int kPushGroups = PINC_PUSH_GROUPS;
 #ifndef PINC_PUSH_THREADS
 #define PINC_PUSH_THREADS 256
 #endif
+// wave priority (s_setprio) of a block's particle-load phase (> 0), or of
+// everything after it (< 0); 0: off
+#ifndef PINC_PUSH_PRIO
+#define PINC_PUSH_PRIO 0
+#endif
 // 1: per-item periodic images only in blocks that straddle a boundary (k_push)
 #ifndef PINC_PUSH_IMG_GATE
 #define PINC_PUSH_IMG_GATE 1
@@ -2022,6 +2027,9 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 		              reinterpret_cast<unsigned long>(a.xo[d]) | reinterpret_cast<unsigned long>(a.vo[d])) & 15);
 
 	unsigned long long tsub = 0;  // (trace mode: thread 0's last timestamp)
+	// (PINC_PUSH_PRIO: a block's waves issue their particle loads at raised
+	// wave priority, so the memory pipe is fed before older blocks' compute)
+	if (PINC_PUSH_PRIO > 0) __builtin_amdgcn_s_setprio(PINC_PUSH_PRIO);
 	PUSH_TS(0);
 	// ---- phase A: load every item, cell box of the input positions (periodic
 	// images nearest to the cell of the block's first item)
@@ -2137,6 +2145,8 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 			}
 		}
 	}
+	// (negative: the loads at priority 0, the rest of the block at -PRIO)
+	if (PINC_PUSH_PRIO != 0) __builtin_amdgcn_s_setprio(PINC_PUSH_PRIO > 0 ? 0 : -PINC_PUSH_PRIO);
 	int cref[3] = {0, 0, 0};
 #pragma unroll
 	for (int d = 0; d < ND; d++) cref[d] = __builtin_amdgcn_readfirstlane((int)xref[d]);
