@@ -1529,6 +1529,13 @@ constexpr int kPushGroups = PINC_PUSH_GROUPS;
 #ifndef PINC_PUSH_THREADS
 #define PINC_PUSH_THREADS 256
 #endif
+// 1: the sorting push orders each brick's run by cell (per (brick, cell)
+// counters for blocks whose brick box holds at most kCellRankBricks bricks of
+// at most 16 cells), so repeated sorts keep a brick's particles cell-contiguous
+#ifndef PINC_SORT_CELLRANK
+#define PINC_SORT_CELLRANK 1
+#endif
+constexpr int kCellRankBricks = 64;
 // wave priority (s_setprio) of a block's particle-load phase (> 0), or of
 // everything after it (< 0); 0: off
 #ifndef PINC_PUSH_PRIO
@@ -1981,6 +1988,9 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	__shared__ int wmov[NW];
 	// sorting push, per item: its rank code (phase C) and its flag (phase D)
 	__shared__ int rlL[SORT ? kPushChunk : 1];
+	// sorting push with PINC_SORT_CELLRANK: counters, then exclusive offsets,
+	// of (brick, cell in brick)
+	__shared__ int ccL[(SORT && PINC_SORT_CELLRANK) ? kCellRankBricks * 16 : 1];
 	__shared__ unsigned char stageF[SORT ? kPushChunk : 1];
 	const Geo32 G = make_geo32(a.g);
 	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -2281,6 +2291,11 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	const int myCopy = (lane & (nCopy - 1)) * rStride;
 	for (int t = threadIdx.x; t < (PINC_PUSH_COPIES ? nCopy * rStride : rB.vol); t += kPushThreads) rhoL[t] = 0.0;
 	for (int t = threadIdx.x; t < (SORT ? kInCellCap : obb.vol); t += kPushThreads) cntOut[t] = 0;
+	// (cell ranking: block-uniform; bricks of at most 16 cells)
+	const int brickCellBits = a.tg.bs[0] + a.tg.bs[1] + a.tg.bs[2];
+	const bool cellRank = SORT && PINC_SORT_CELLRANK && ib.vol <= kCellRankBricks && brickCellBits <= 4;
+	if (cellRank)
+		for (int t = threadIdx.x; t < ib.vol * 16; t += kPushThreads) ccL[t] = 0;
 	if (KICK && !(PINC_PUSH_SKIP & 2)) {
 		const BoxRcp eq = box_rcp(eB);
 		for (int t = threadIdx.x; t < eB.vol; t += kPushThreads) {
@@ -2319,6 +2334,7 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 	// after it +1 %).
 	if (SORT) {
 		static_assert(kInCellCap <= 256 && kPushChunk <= (1 << 23), "rank/brick packing");
+		static_assert(kCellRankBricks <= 64 && kPushChunk <= (1 << 20), "rank/brick/cell packing");
 		int no = 0;  // (trace: items outside ib)
 #pragma unroll
 		for (int k = 0; k < kPushItems; k++) {
@@ -2330,10 +2346,24 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 			// plain LDS atomics: a wave's lanes share a few bricks (same-address
 			// conflicts), cheaper than aggregating the groups with ballots and
 			// shuffles (C4 electron sorting push 36.2 -> 33.5 ms)
-			const int rank = lb >= 0 ? atomicAdd(&bCnt[lb], 1) : 0;
+			int rank = 0, rl = -1;
+			if (cellRank) {
+				// the cell's index inside its brick, x fastest (clamped as brick_inside)
+				int ci = 0, sh = 0;
+#pragma unroll
+				for (int d = 0; d < ND; d++) {
+					ci |= (clamp_cell<ND>(a.tg, d, c[d]) & ((1 << a.tg.bs[d]) - 1)) << sh;
+					sh += a.tg.bs[d];
+				}
+				rank = lb >= 0 ? atomicAdd(&ccL[lb * 16 + ci], 1) : 0;
+				rl = rank << 10 | lb << 4 | ci;
+			} else {
+				rank = lb >= 0 ? atomicAdd(&bCnt[lb], 1) : 0;
+				rl = rank << 8 | lb;
+			}
 			const bool out = ok && lb < 0;
 			const int g = agg_add(a.cursor, out ? brick_first_key<ND>(a.tg, c) : 0, out);
-			const int rl = lb >= 0 ? (rank << 8 | lb) : (ok ? ~g : -1);
+			rl = lb >= 0 ? rl : (ok ? ~g : -1);
 			rlL[k * kPushThreads + threadIdx.x] = rl;  // (stored at once: no item's rank stays live)
 			no += rl < 0 && ok;
 		}
@@ -2346,7 +2376,20 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 		static_assert(kInCellCap <= kPushThreads, "one reservation per thread");
 		// one global reservation per brick of ib, one range of its first
 		// cell's cursor
-		const int bm = (int)threadIdx.x < ib.vol ? bCnt[threadIdx.x] : 0;
+		int bm = 0;
+		if (cellRank) {
+			// each brick's cell counters to exclusive offsets inside its run
+			if ((int)threadIdx.x < ib.vol) {
+#pragma unroll
+				for (int q = 0; q < 16; q++) {
+					const int v = ccL[threadIdx.x * 16 + q];
+					ccL[threadIdx.x * 16 + q] = bm;
+					bm += v;
+				}
+			}
+		} else {
+			bm = (int)threadIdx.x < ib.vol ? bCnt[threadIdx.x] : 0;
+		}
 		// the global reservation's result is first needed by the stores after
 		// the kick: its round trip overlaps the kick (resBase, one VGPR)
 		if (bm) resBase = atomicAdd(&a.cursor[brick_key<ND>(a.tg, ib, threadIdx.x)], bm);
@@ -2685,7 +2728,9 @@ __global__ __launch_bounds__(kPushThreads) __attribute__((amdgpu_waves_per_eu(PI
 			if (!((valid >> k) & 1u)) continue;
 			const long i = item(k);
 			const int r = rlL[k * kPushThreads + threadIdx.x];
-			const long o = r >= 0 ? (long)bBase[r & 255] + (r >> 8) : (long)~r;
+			const long o = r < 0      ? (long)~r
+			               : cellRank ? (long)bBase[(r >> 4) & 63] + ccL[r & 1023] + (r >> 10)
+			                          : (long)bBase[r & 255] + (r >> 8);
 #pragma unroll
 			for (int d = 0; d < ND; d++) {
 				// (nontemporal, 8 B per lane: 24.4 -> 33.5 ms per sorting push,
